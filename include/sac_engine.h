@@ -1,0 +1,180 @@
+/*
+ * sac_engine.h — C ABI of the MI355X (gfx950) SAC update engine.
+ *
+ * This is the drop-in boundary for the reference's hot path: the SAC gradient
+ * step and the replay buffer it samples from.  The reference has no native or
+ * FFI layer (pure Python/PyTorch); each entry point below replaces a Python
+ * method of the reference and is bound from Python with ctypes by
+ * soft-actor-critic_amd/sac/_engine.py (the host-side mirror of the reference
+ * API; binding recipe in INTEGRATION.md).
+ *
+ * Conventions
+ *   - every pointer is a DEVICE pointer (HBM) unless named *_host;
+ *   - all launches are asynchronous on the given HIP stream (hipStream_t passed
+ *     as void*; NULL = legacy default stream); no entry point synchronises the
+ *     device except sac_engine_create (one-off table upload) and the profiling
+ *     entry point;
+ *   - parameters, Adam moments and replay storage are owned by the caller (the
+ *     PyTorch caching allocator); the engine keeps raw pointers only;
+ *   - return 0 on success, a negative SAC_E* code on error; sac_last_error()
+ *     returns a description of the last error of the calling thread.
+ *
+ * Layouts
+ *   - network parameters: one flat fp32 buffer per network, Linear layers in
+ *     order, each as weight [out][in] (nn.Linear layout) followed by bias [out]
+ *     — i.e. the concatenation of reference state_dict() values
+ *     (net.0.weight, net.0.bias, net.2.weight, ...; sac/models.py:141-149);
+ *   - Adam exp_avg / exp_avg_sq buffers use the same flat layout;
+ *   - replay storage is struct-of-arrays, fp32, ring-ordered:
+ *     obs[cap][obs_dim], act[cap][act_dim], rew[cap], next_obs[cap][obs_dim],
+ *     done[cap]; state[0] = number of valid rows, state[1] = next write slot
+ *     (the oldest row once full).
+ */
+#ifndef SAC_ENGINE_H
+#define SAC_ENGINE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SAC_MAX_LAYERS 8
+
+enum sac_status {
+  SAC_OK = 0,
+  SAC_E_INVALID = -1,     /* bad argument / unsupported shape */
+  SAC_E_HIP = -2,         /* HIP runtime error */
+  SAC_E_NOT_ENOUGH = -3,  /* replay holds fewer rows than the batch (ValueError in Python) */
+};
+
+enum sac_activation {     /* reference sac/models.py:104-112 _ACTIVATIONS */
+  SAC_ACT_IDENTITY = 0, SAC_ACT_RELU = 1, SAC_ACT_TANH = 2, SAC_ACT_ELU = 3,
+  SAC_ACT_LEAKY_RELU = 4, SAC_ACT_GELU = 5, SAC_ACT_SELU = 6
+};
+
+enum sac_precision {
+  SAC_PREC_FP32 = 0,      /* v_mfma_f32_16x16x4_f32: exact-fp32 products (parity mode) */
+  SAC_PREC_BF16 = 1       /* v_mfma_f32_16x16x32_bf16, fp32 accumulate, fp32 master weights */
+};
+
+/* Shape + hyper-parameters.  Mirrors the YAML keys the reference reads
+ * (sac.*, q_net.*, policy_net.*, train.batch_size; sac/agent.py:22-115). */
+typedef struct sac_engine_config {
+  int32_t obs_dim, act_dim, batch;
+  int32_t q_layers;                         /* number of Linear layers of Q   */
+  int32_t q_dims[SAC_MAX_LAYERS + 1];       /* q_dims[0]=obs+act ... q_dims[q_layers]=1 */
+  int32_t q_hidden_act, q_out_act;
+  int32_t pi_layers;
+  int32_t pi_dims[SAC_MAX_LAYERS + 1];      /* pi_dims[0]=obs ... pi_dims[pi_layers]=2*act */
+  int32_t pi_hidden_act, pi_out_act;
+  float gamma, tau;
+  float log_std_min, log_std_max, action_scale;
+  float actor_lr, critic_lr;
+  double alpha_lr;
+  float beta1, beta2, adam_eps;             /* torch.optim.Adam defaults 0.9, 0.999, 1e-8 */
+  int32_t auto_entropy;                     /* sac.auto_entropy_tuning */
+  float target_entropy;                     /* -act_dim (agent.py:43) */
+  int32_t precision;                        /* enum sac_precision */
+  uint64_t seed;                            /* device RNG (replay indices, eps) */
+} sac_engine_config;
+
+/* Caller-owned device state of one learner. */
+typedef struct sac_engine_buffers {
+  float *pi, *q1, *q2, *q1t, *q2t;          /* flat fp32 parameters */
+  float *pi_m, *pi_v, *q1_m, *q1_v, *q2_m, *q2_v;  /* Adam exp_avg / exp_avg_sq */
+  double *alpha_state;   /* [4]: log_alpha, alpha, adam m, adam v (fp64, agent.py:45-55) */
+  double *opt_steps;     /* [4]: Adam step of policy, q1, q2, alpha optimizers */
+  uint64_t *rng_step;    /* [1]: device RNG step counter */
+  float *stats;          /* [4 + 2*batch]: losses Lq1,Lq2,Lpi,Lalpha; y[batch]; log_pi[batch] */
+  void *workspace;       /* sac_engine_workspace_bytes() bytes, 256-B aligned */
+  size_t workspace_bytes;
+} sac_engine_buffers;
+
+typedef struct sac_replay {
+  float *obs, *act, *rew, *next_obs, *done;
+  int64_t capacity;
+  int32_t obs_dim, act_dim;
+  int64_t *state;        /* device [2]: size, next write slot */
+} sac_replay;
+
+typedef struct sac_engine sac_engine;
+
+const char *sac_last_error(void);
+const char *sac_version(void);
+
+/* Workspace the engine needs for this config (activations, packed compute
+ * copies of the weights, split-K partials, tile tables). */
+size_t sac_engine_workspace_bytes(const sac_engine_config *cfg);
+
+/* Validates cfg, lays out the workspace, uploads the tile tables and writes the
+ * packed compute copies of the weights (one synchronous call).
+ * Replaces: SAC.__init__ network/optimizer setup, sac/agent.py:22-124. */
+int sac_engine_create(const sac_engine_config *cfg, const sac_engine_buffers *buf,
+                      void *stream, sac_engine **out);
+void sac_engine_destroy(sac_engine *e);
+
+/* Re-derive the packed compute copies after the host changed parameters
+ * (load_state_dict, load_agent: sac/agent.py:538-554). */
+int sac_engine_sync_params(sac_engine *e, void *stream);
+
+/* n_steps consecutive SAC gradient steps (sample -> target -> critic -> actor ->
+ * alpha -> Polyak), each exactly sac/agent.py:302-327.
+ *   indices : NULL => device sampler (Philox-keyed Feistel permutation:
+ *             distinct uniform rows, as random.sample, replay_buffer.py:39);
+ *             else [n_steps][batch] int32 LOGICAL positions (0 = oldest row,
+ *             the deque order of the reference).
+ *   eps     : NULL => device Philox normals; else [n_steps][2][batch][act_dim]
+ *             fp32 (target eps, then actor eps: the two rsample draws,
+ *             sac/models.py:83).
+ * Replaces: SAC.training_step (sac/agent.py:302-327) and the methods it calls
+ * (sample_batch 166, compute_target_q_values 195, update_q_networks 213,
+ * update_policy_network 238, update_entropy_temperature 263,
+ * soft_update_target_networks 282). */
+int sac_engine_train(sac_engine *e, const sac_replay *rb, int32_t n_steps,
+                     const int32_t *indices, const float *eps, void *stream);
+
+/* Same, replayed from a captured hipGraph of `chunk` steps (device sampler and
+ * device eps only).  n_steps need not be a multiple of chunk. */
+int sac_engine_train_graph(sac_engine *e, const sac_replay *rb, int32_t n_steps,
+                           int32_t chunk, void *stream);
+
+/* Policy action for n observations [n][obs_dim].  eps == NULL => deterministic
+ * tanh(mu)*scale (models.py:89-92); else eps [n][act_dim] and the squashed
+ * Gaussian sample (models.py:79-87).  log_pi may be NULL.
+ * Replaces: SAC.select_action (sac/agent.py:149-156). */
+int sac_policy_act(sac_engine *e, const float *obs, int32_t n, const float *eps,
+                   float *action, float *log_pi, void *stream);
+
+/* Append n transitions (packed rows [n][2*obs+act+2] = s|a|r|s'|d, device) at
+ * host-tracked (size, pos); writes the new (size, pos) to rb->state.
+ * Replaces: ReplayBuffer.push (sac/replay_buffer.py:21-30). */
+int sac_replay_push(const sac_replay *rb, const float *rows, int64_t n,
+                    int64_t size_host, int64_t pos_host, void *stream);
+
+/* Gather rows by LOGICAL index into SoA outputs (s[B][obs], a[B][act], r[B],
+ * s2[B][obs], d[B]).  Replaces: ReplayBuffer.sample + SAC.sample_batch's
+ * stacking (replay_buffer.py:32-39, agent.py:166-193). */
+int sac_replay_gather(const sac_replay *rb, const int32_t *logical_idx, int32_t batch,
+                      float *s, float *a, float *r, float *s2, float *d, void *stream);
+
+/* Device sampler alone: `batch` distinct logical indices in [0, size) for RNG
+ * (seed, step).  size is read from rb->state. */
+int sac_replay_sample_indices(const sac_replay *rb, int32_t batch, uint64_t seed,
+                              uint64_t step, int32_t *out, void *stream);
+
+/* Profiling: runs n_steps with hipEvents around each phase kernel and returns
+ * the mean device time per phase in ms: [0]=A target+critic-backward,
+ * [1]=B critic dW+Adam+Polyak, [2]=C actor, [3]=D actor dW+Adam+alpha.
+ * Synchronises the stream. */
+int sac_engine_time_phases(sac_engine *e, const sac_replay *rb, int32_t n_steps,
+                           float *ms_host, void *stream);
+
+/* Phase kernel names as they appear in rocprofv3 kernel traces. */
+const char *sac_phase_kernel_name(int32_t phase);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SAC_ENGINE_H */

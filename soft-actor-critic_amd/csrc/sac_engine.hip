@@ -1,0 +1,671 @@
+// sac_engine.hip — MI355X (gfx950) SAC gradient-step engine, C ABI in
+// include/sac_engine.h.  Design notes: DESIGN.md.
+//
+// One gradient step (reference sac/agent.py:302-327) = 4 launches:
+//
+//   A  sac_target_critic  row tiles of 16 batch rows, 16 waves.  Device sampler
+//                         + replay gather (agent.py:166-193), pi forward on s' and s
+//                         (models.py:79-87), target twin-Q and y (agent.py:195-211),
+//                         Q1/Q2 forward + backward to every layer's pre-activation
+//                         gradient (agent.py:221-234).  Writes X^T / dY^T tiles.
+//   B  sac_critic_update  32x32 weight tiles: dW = dY^T X (MFMA over the batch),
+//                         Adam (torch single-tensor math), Polyak (agent.py:282-300),
+//                         packed compute copies of the new weights.
+//   C  sac_actor          row tiles: Q1/Q2 forward on (s, a~) with the UPDATED
+//                         critics, min-Q, backward to d a~, squashed-Gaussian head
+//                         backward, pi backward (agent.py:238-260).
+//   D  sac_actor_update   pi weight tiles + Adam; one extra block runs the float64
+//                         alpha update (agent.py:263-280) and reduces the losses.
+//
+// Weights stay fp32 masters (the nn.Parameter storage); GEMM operands are packed
+// compute copies in the MFMA dtype ([out][in] and [in][out], 32-padded) that the
+// update kernels rewrite in place, so nothing is re-packed per step.
+#include "../../include/sac_engine.h"
+
+#include <algorithm>
+#include <math.h>
+#include <stdio.h>
+#include <string.h>
+#include <string>
+#include <vector>
+
+#define SAC_VERSION "sac-mi355x 0.1.0"
+
+#include "sac_phases.h"
+
+// ============================================================================ params / replay
+template <typename T>
+__global__ void pack_weights(const float* __restrict__ W, int K, int N, int Kp, int Np, T* __restrict__ Wc,
+                             T* __restrict__ WTc) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < Np * Kp; i += gridDim.x * blockDim.x) {
+    const int n = i / Kp, k = i % Kp;
+    const float v = (n < N && k < K) ? W[(size_t)n * K + k] : 0.f;
+    Wc[packed_off<T>(n, k, Kp)] = MM<T>::cvt(v);
+    if (WTc) WTc[packed_off<T>(k, n, Np)] = MM<T>::cvt(v);
+  }
+}
+
+__global__ void replay_push_kernel(sac_replay rb, const float* __restrict__ rows, int64_t n, int64_t skip, int64_t pos,
+                                   int64_t new_size, int64_t new_pos) {
+  const int O = rb.obs_dim, A = rb.act_dim, W = 2 * O + A + 2;
+  const int64_t total = (n - skip) * W;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t rr = i / W;
+    const int c = (int)(i % W);
+    const int64_t src = skip + rr;
+    const int64_t slot = (pos + src) % rb.capacity;
+    const float v = rows[src * W + c];
+    if (c < O)
+      rb.obs[slot * O + c] = v;
+    else if (c < O + A)
+      rb.act[slot * A + (c - O)] = v;
+    else if (c == O + A)
+      rb.rew[slot] = v;
+    else if (c < 2 * O + A + 1)
+      rb.next_obs[slot * O + (c - O - A - 1)] = v;
+    else
+      rb.done[slot] = v;
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    rb.state[0] = new_size;
+    rb.state[1] = new_pos;
+  }
+}
+
+// SoA gather, one float per thread-iteration over the flattened [B][W] batch.
+__global__ void replay_gather_kernel(sac_replay rb, const int32_t* __restrict__ idx, int B, float* __restrict__ s,
+                                     float* __restrict__ a, float* __restrict__ r, float* __restrict__ s2,
+                                     float* __restrict__ d) {
+  const int O = rb.obs_dim, A = rb.act_dim;
+  const int64_t size = rb.state[0], pos = rb.state[1];
+  const int W = 2 * O + A + 2;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < (int64_t)B * W;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    int64_t b, c;
+    // field-major flattening keeps each field's reads/writes contiguous
+    if (i < (int64_t)B * O) {
+      b = i / O; c = i % O;
+      const int64_t li = idx[b];
+      const int64_t sl = size < rb.capacity ? li : (pos + li) % rb.capacity;
+      s[i] = rb.obs[sl * O + c];
+    } else if (i < (int64_t)B * (2 * O)) {
+      const int64_t j = i - (int64_t)B * O;
+      b = j / O; c = j % O;
+      const int64_t li = idx[b];
+      const int64_t sl = size < rb.capacity ? li : (pos + li) % rb.capacity;
+      s2[j] = rb.next_obs[sl * O + c];
+    } else if (i < (int64_t)B * (2 * O + A)) {
+      const int64_t j = i - (int64_t)B * 2 * O;
+      b = j / A; c = j % A;
+      const int64_t li = idx[b];
+      const int64_t sl = size < rb.capacity ? li : (pos + li) % rb.capacity;
+      a[j] = rb.act[sl * A + c];
+    } else {
+      const int64_t j = i - (int64_t)B * (2 * O + A);
+      b = j >> 1;
+      const int64_t li = idx[b];
+      const int64_t sl = size < rb.capacity ? li : (pos + li) % rb.capacity;
+      if (j & 1) d[b] = rb.done[sl]; else r[b] = rb.rew[sl];
+    }
+  }
+}
+
+__global__ void replay_sample_kernel(const int64_t* __restrict__ state, int B, uint64_t seed, uint64_t step,
+                                     int32_t* __restrict__ out) {
+  const int64_t size = state[0];
+  const Feistel f = feistel_make(seed, step, size);
+  for (int b = blockIdx.x * blockDim.x + threadIdx.x; b < B; b += gridDim.x * blockDim.x)
+    out[b] = (int32_t)feistel_sample(f, b, size);
+}
+
+// ============================================================================ host side
+static thread_local std::string g_err;
+static int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+#define HIPCHK(x)                                                                                  \
+  do {                                                                                             \
+    hipError_t _e = (x);                                                                           \
+    if (_e != hipSuccess) return fail(SAC_E_HIP, std::string(#x ": ") + hipGetErrorString(_e));    \
+  } while (0)
+
+struct sac_engine {
+  sac_engine_config cfg;
+  sac_engine_buffers buf;
+  EngineDev h;            // host mirror of the device struct
+  EngineDev* d = nullptr; // in workspace
+  TileDesc* tilesB = nullptr;
+  TileDesc* tilesD = nullptr;
+  std::vector<TileDesc> hostB, hostD;
+  int nB = 0, nD = 0;
+  size_t lds_bytes = 0;
+  int nrt = 0;
+  // graph cache
+  hipGraphExec_t gexec = nullptr;
+  hipGraph_t graph = nullptr;
+  int gchunk = 0;
+  sac_replay gkey{};
+  hipStream_t cap = nullptr;
+};
+
+static inline int rup(int x, int m) { return (x + m - 1) / m * m; }
+
+struct Layout {
+  size_t off = 0;
+  size_t take(size_t bytes) {
+    off = (off + 255) & ~(size_t)255;
+    const size_t o = off;
+    off += bytes;
+    return o;
+  }
+};
+
+static int validate(const sac_engine_config* c) {
+  if (!c) return fail(SAC_E_INVALID, "null config");
+  if (c->obs_dim < 1 || c->act_dim < 1 || c->act_dim > 32) return fail(SAC_E_INVALID, "obs_dim >= 1, 1 <= act_dim <= 32");
+  if (c->batch < 1 || c->batch > (1 << 20)) return fail(SAC_E_INVALID, "batch out of range");
+  if (c->q_layers < 2 || c->q_layers > SAC_DEV_LAYERS || c->pi_layers < 2 || c->pi_layers > SAC_DEV_LAYERS)
+    return fail(SAC_E_INVALID, "networks need 1..5 hidden layers");
+  if (c->q_dims[0] != c->obs_dim + c->act_dim || c->q_dims[c->q_layers] != 1)
+    return fail(SAC_E_INVALID, "q_dims must run obs+act -> ... -> 1");
+  if (c->pi_dims[0] != c->obs_dim || c->pi_dims[c->pi_layers] != 2 * c->act_dim)
+    return fail(SAC_E_INVALID, "pi_dims must run obs -> ... -> 2*act");
+  for (int i = 0; i <= c->q_layers; ++i)
+    if (c->q_dims[i] < 1) return fail(SAC_E_INVALID, "bad q dim");
+  for (int i = 0; i <= c->pi_layers; ++i)
+    if (c->pi_dims[i] < 1) return fail(SAC_E_INVALID, "bad pi dim");
+  const int acts[4] = {c->q_hidden_act, c->q_out_act, c->pi_hidden_act, c->pi_out_act};
+  for (int a : acts)
+    if (a < 0 || a > 6) return fail(SAC_E_INVALID, "bad activation code");
+  if (c->precision != SAC_PREC_FP32 && c->precision != SAC_PREC_BF16) return fail(SAC_E_INVALID, "bad precision");
+  return SAC_OK;
+}
+
+// Lays out everything; when e != nullptr also fills e->h pointers (base = workspace).
+static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
+  const int esz = c->precision == SAC_PREC_BF16 ? 2 : 4;
+  const int B = c->batch, Bp = rup(B, 32), nrt = (B + SAC_ROWS - 1) / SAC_ROWS, Br = nrt * SAC_ROWS;
+  const int O = c->obs_dim, A = c->act_dim;
+  Layout lay;
+  const size_t o_E = lay.take(sizeof(EngineDev));
+  EngineDev h;
+  memset(&h, 0, sizeof(h));
+  auto P = [&](size_t o) -> void* { return base ? (void*)(base + o) : nullptr; };
+  int maxKp = 32, maxNo = 32;
+  size_t xt_q0 = 0;
+  for (int ni = 0; ni < 5; ++ni) {
+    const bool is_pi = ni == NET_PI;
+    const bool trainable = ni <= NET_Q2;
+    const int L = is_pi ? c->pi_layers : c->q_layers;
+    const int* dims = is_pi ? c->pi_dims : c->q_dims;
+    NetDev& nd = h.net[ni];
+    nd.L = L;
+    nd.hid_act = is_pi ? c->pi_hidden_act : c->q_hidden_act;
+    nd.out_act = is_pi ? c->pi_out_act : c->q_out_act;
+    int off = 0;
+    for (int l = 0; l < L; ++l) {
+      LayerDev& ly = nd.l[l];
+      ly.K = dims[l];
+      ly.N = dims[l + 1];
+      ly.Kp = rup(ly.K, SAC_PAD);
+      ly.Np = rup(ly.N, SAC_PAD);
+      ly.w_off = off;
+      off += ly.K * ly.N;
+      ly.b_off = off;
+      off += ly.N;
+      maxKp = std::max(maxKp, ly.Kp);
+      if (l < L - 1) maxKp = std::max(maxKp, ly.Np);
+      else maxNo = std::max(maxNo, ly.Np);
+      ly.Wc = P(lay.take((size_t)ly.Np * ly.Kp * esz));
+      if (trainable) {
+        ly.WTc = P(lay.take((size_t)ly.Kp * ly.Np * esz));
+        if (ni == NET_Q2 && l == 0) {
+          ly.XT = P(xt_q0);
+        } else {
+          const size_t o = lay.take((size_t)ly.Kp * Bp * esz);
+          if (ni == NET_Q1 && l == 0) xt_q0 = o;
+          ly.XT = P(o);
+        }
+        ly.GT = P(lay.take((size_t)ly.Np * Bp * esz));
+        ly.dbp = (float*)P(lay.take((size_t)nrt * ly.N * 4));
+      }
+      if (is_pi) ly.pstash = (float*)P(lay.take((size_t)Br * ly.Np * 4));
+    }
+  }
+  h.s_st = (float*)P(lay.take((size_t)Br * O * 4));
+  h.a_st = (float*)P(lay.take((size_t)Br * A * 4));
+  h.lp_st = (float*)P(lay.take((size_t)Br * 4));
+  h.head_st = (float*)P(lay.take((size_t)Br * 4 * A * 4));
+  h.lossp = (float*)P(lay.take((size_t)nrt * 4 * 4));
+  int nB = 0, nD = 0;
+  for (int ni = NET_PI; ni <= NET_Q2; ++ni)
+    for (int l = 0; l < h.net[ni].L; ++l)
+      (ni == NET_PI ? nD : nB) += (h.net[ni].l[l].Np / 32) * (h.net[ni].l[l].Kp / 32);
+  const size_t o_tB = lay.take((size_t)nB * sizeof(TileDesc));
+  const size_t o_tD = lay.take((size_t)nD * sizeof(TileDesc));
+  const size_t total = lay.take(0);
+
+  // LDS layout (floats)
+  const int R = SAC_ROWS;
+  h.ld = maxKp + 4;
+  h.ldo = maxNo + 4;
+  int lo = 0;
+  auto lt = [&](int floats) {
+    lo = (lo + 3) & ~3;  // 16-B alignment
+    const int o = lo;
+    lo += floats;
+    return o;
+  };
+  h.o_X = lt(2 * R * h.ld);
+  h.o_Y = lt(2 * R * h.ld);
+  const int Lhq = c->q_layers - 1, Lhp = c->pi_layers - 1;
+  for (int l = 0; l < std::max(Lhq, Lhp); ++l) {
+    int np = 0;
+    if (l < Lhq) np = std::max(np, h.net[NET_Q1].l[l].Np);
+    if (l < Lhp) np = std::max(np, h.net[NET_PI].l[l].Np);
+    h.ldp1[l] = np + 4;
+    h.o_P1[l] = lt(R * h.ldp1[l]);
+  }
+  for (int l = 0; l < Lhq; ++l) {
+    h.ldp2[l] = h.net[NET_Q2].l[l].Np + 4;
+    h.o_P2[l] = lt(R * h.ldp2[l]);
+  }
+  h.o_s = lt(R * O);
+  h.o_s2 = lt(R * O);
+  h.o_a = lt(R * A);
+  h.o_a2 = lt(R * A);
+  h.o_r = lt(R);
+  h.o_d = lt(R);
+  h.o_et = lt(R * A);
+  h.o_ea = lt(R * A);
+  h.o_out = lt(2 * R * h.ldo);
+  h.o_outp = lt(2 * R * h.ldo);
+  h.o_out2 = lt(R * h.ldo);
+  h.o_outp2 = lt(R * h.ldo);
+  h.o_lp = lt(R);
+  h.o_qt = lt(2 * R);
+  h.o_y = lt(R);
+  h.o_g = lt(R * h.ldo);
+  h.o_g2 = lt(R * h.ldo);
+  h.o_ga = lt(R * A);
+  h.o_gout = lt(R * h.ldo);
+  h.o_slot = lt(2 * R);  // int64[R]
+
+  if (e) {
+    h.B = B;
+    h.Bp = Bp;
+    h.Br = Br;
+    h.O = O;
+    h.A = A;
+    h.nrt = nrt;
+    h.auto_entropy = c->auto_entropy;
+    h.gamma = c->gamma;
+    h.tau = c->tau;
+    h.ls_min = c->log_std_min;
+    h.ls_max = c->log_std_max;
+    h.scale = c->action_scale;
+    h.actor_lr = c->actor_lr;
+    h.critic_lr = c->critic_lr;
+    h.beta1 = c->beta1;
+    h.beta2 = c->beta2;
+    h.adam_eps = c->adam_eps;
+    h.target_entropy = c->target_entropy;
+    h.alpha_lr = c->alpha_lr;
+    h.seed = c->seed;
+    float* parts[5] = {e->buf.pi, e->buf.q1, e->buf.q2, e->buf.q1t, e->buf.q2t};
+    float* ms[3] = {e->buf.pi_m, e->buf.q1_m, e->buf.q2_m};
+    float* vs[3] = {e->buf.pi_v, e->buf.q1_v, e->buf.q2_v};
+    for (int ni = 0; ni < 5; ++ni) {
+      h.net[ni].P = parts[ni];
+      h.net[ni].M = ni < 3 ? ms[ni] : nullptr;
+      h.net[ni].V = ni < 3 ? vs[ni] : nullptr;
+    }
+    h.alpha_state = e->buf.alpha_state;
+    h.opt_steps = e->buf.opt_steps;
+    h.rng_step = e->buf.rng_step;
+    h.stats = e->buf.stats;
+    e->h = h;
+    e->d = (EngineDev*)(base + o_E);
+    e->tilesB = (TileDesc*)(base + o_tB);
+    e->tilesD = (TileDesc*)(base + o_tD);
+    e->nB = nB;
+    e->nD = nD;
+    e->lds_bytes = (size_t)lo * 4;
+    e->nrt = nrt;
+    // self-contained update tiles (phase B: critics + Polyak, phase D: policy)
+    const int esz2 = esz;
+    e->hostB.clear();
+    e->hostD.clear();
+    for (int ni = NET_PI; ni <= NET_Q2; ++ni) {
+      const NetDev& nd = h.net[ni];
+      const NetDev& tn = h.net[ni == NET_PI ? NET_PI : ni + 2];
+      for (int l = 0; l < nd.L; ++l) {
+        const LayerDev& ly = nd.l[l];
+        for (int nt = 0; nt < ly.Np / 32; ++nt)
+          for (int kt = 0; kt < ly.Kp / 32; ++kt) {
+            TileDesc t;
+            memset(&t, 0, sizeof(t));
+            t.GT = (const char*)ly.GT + (size_t)nt * 32 * Bp * esz2;
+            t.XT = (const char*)ly.XT + (size_t)kt * 32 * Bp * esz2;
+            t.W = nd.P + ly.w_off;
+            t.Wm = nd.M + ly.w_off;
+            t.Wv = nd.V + ly.w_off;
+            t.b = nd.P + ly.b_off;
+            t.bm = nd.M + ly.b_off;
+            t.bv = nd.V + ly.b_off;
+            t.Wc = ly.Wc;
+            t.WTc = ly.WTc;
+            if (ni != NET_PI) {
+              t.tW = tn.P + ly.w_off;
+              t.tb = tn.P + ly.b_off;
+              t.tWc = tn.l[l].Wc;
+            }
+            t.dbp = ly.dbp;
+            t.K = ly.K;
+            t.N = ly.N;
+            t.Kp = ly.Kp;
+            t.Np = ly.Np;
+            t.n0 = nt * 32;
+            t.k0 = kt * 32;
+            t.opt = ni;
+            t.nrt = nrt;
+            (ni == NET_PI ? e->hostD : e->hostB).push_back(t);
+          }
+      }
+    }
+  }
+  return total + 256;
+}
+
+template <typename T>
+static void set_lds_attrs(size_t bytes) {
+  (void)hipFuncSetAttribute((const void*)sac_target_critic<T>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+  (void)hipFuncSetAttribute((const void*)sac_actor<T>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+  (void)hipFuncSetAttribute((const void*)sac_policy_act_kernel<T>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+}
+
+template <typename T>
+static void launch_phase(sac_engine* e, int phase, const sac_replay* rb, const int32_t* idx, const float* eps,
+                         hipStream_t s) {
+  switch (phase) {
+    case 0:
+      sac_target_critic<T><<<e->nrt, SAC_THREADS, e->lds_bytes, s>>>(e->h, *rb, idx, eps);
+      break;
+    case 1:
+      sac_critic_update<T><<<e->nB, 256, 0, s>>>(e->h, e->tilesB);
+      break;
+    case 2:
+      sac_actor<T><<<e->nrt, SAC_THREADS, e->lds_bytes, s>>>(e->h);
+      break;
+    case 3:
+      sac_actor_update<T><<<e->nD + 1, 256, 0, s>>>(e->h, e->tilesD, e->nD);
+      break;
+  }
+}
+
+static void launch_step(sac_engine* e, const sac_replay* rb, const int32_t* idx, const float* eps, hipStream_t s) {
+  for (int p = 0; p < 4; ++p) {
+    if (e->cfg.precision == SAC_PREC_BF16)
+      launch_phase<bf16>(e, p, rb, idx, eps, s);
+    else
+      launch_phase<float>(e, p, rb, idx, eps, s);
+  }
+}
+
+static int check_replay(sac_engine* e, const sac_replay* rb) {
+  if (!rb || !rb->obs || !rb->act || !rb->rew || !rb->next_obs || !rb->done || !rb->state)
+    return fail(SAC_E_INVALID, "null replay buffer");
+  if (rb->obs_dim != e->cfg.obs_dim || rb->act_dim != e->cfg.act_dim)
+    return fail(SAC_E_INVALID, "replay dims do not match the engine");
+  if (rb->capacity < e->cfg.batch) return fail(SAC_E_NOT_ENOUGH, "replay capacity smaller than the batch");
+  return SAC_OK;
+}
+
+extern "C" {
+
+const char* sac_last_error(void) { return g_err.c_str(); }
+const char* sac_version(void) { return SAC_VERSION; }
+
+size_t sac_engine_workspace_bytes(const sac_engine_config* cfg) {
+  if (validate(cfg) != SAC_OK) return 0;
+  return plan(cfg, nullptr, nullptr);
+}
+
+const char* sac_phase_kernel_name(int32_t phase) {
+  switch (phase) {
+    case 0: return "sac_target_critic";
+    case 1: return "sac_critic_update";
+    case 2: return "sac_actor";
+    case 3: return "sac_actor_update";
+    default: return "";
+  }
+}
+
+int sac_engine_sync_params(sac_engine* e, void* stream) {
+  if (!e) return fail(SAC_E_INVALID, "null engine");
+  hipStream_t s = (hipStream_t)stream;
+  const bool bf = e->cfg.precision == SAC_PREC_BF16;
+  for (int ni = 0; ni < 5; ++ni) {
+    const NetDev& nd = e->h.net[ni];
+    for (int l = 0; l < nd.L; ++l) {
+      const LayerDev& ly = nd.l[l];
+      const int blocks = std::min(1024, (ly.Np * ly.Kp + 255) / 256);
+      if (bf)
+        pack_weights<bf16><<<blocks, 256, 0, s>>>(nd.P + ly.w_off, ly.K, ly.N, ly.Kp, ly.Np, (bf16*)ly.Wc, (bf16*)ly.WTc);
+      else
+        pack_weights<float><<<blocks, 256, 0, s>>>(nd.P + ly.w_off, ly.K, ly.N, ly.Kp, ly.Np, (float*)ly.Wc,
+                                                   (float*)ly.WTc);
+    }
+  }
+  HIPCHK(hipGetLastError());
+  return SAC_OK;
+}
+
+int sac_engine_create(const sac_engine_config* cfg, const sac_engine_buffers* buf, void* stream, sac_engine** out) {
+  if (!out || !buf) return fail(SAC_E_INVALID, "null argument");
+  *out = nullptr;
+  int rc = validate(cfg);
+  if (rc) return rc;
+  const size_t need = plan(cfg, nullptr, nullptr);
+  if (!buf->workspace || buf->workspace_bytes < need)
+    return fail(SAC_E_INVALID, "workspace too small: need " + std::to_string(need) + " bytes");
+  if (((uintptr_t)buf->workspace) & 255) return fail(SAC_E_INVALID, "workspace must be 256-byte aligned");
+  if (!buf->pi || !buf->q1 || !buf->q2 || !buf->q1t || !buf->q2t || !buf->pi_m || !buf->pi_v || !buf->q1_m ||
+      !buf->q1_v || !buf->q2_m || !buf->q2_v || !buf->alpha_state || !buf->opt_steps || !buf->rng_step || !buf->stats)
+    return fail(SAC_E_INVALID, "null device buffer");
+  sac_engine* e = new sac_engine();
+  e->cfg = *cfg;
+  e->buf = *buf;
+  plan(cfg, e, (char*)buf->workspace);
+  if (e->lds_bytes > 160 * 1024) {
+    const size_t lb = e->lds_bytes;
+    delete e;
+    return fail(SAC_E_INVALID, "layer widths need " + std::to_string(lb) + " B of LDS per workgroup (max 163840)");
+  }
+  hipStream_t s = (hipStream_t)stream;
+  hipError_t err = hipMemsetAsync(buf->workspace, 0, buf->workspace_bytes, s);
+  if (err == hipSuccess) err = hipMemcpyAsync(e->d, &e->h, sizeof(EngineDev), hipMemcpyHostToDevice, s);
+  if (err == hipSuccess) err = hipMemcpyAsync(e->tilesB, e->hostB.data(), e->hostB.size() * sizeof(TileDesc), hipMemcpyHostToDevice, s);
+  if (err == hipSuccess) err = hipMemcpyAsync(e->tilesD, e->hostD.data(), e->hostD.size() * sizeof(TileDesc), hipMemcpyHostToDevice, s);
+  if (err == hipSuccess) err = hipStreamSynchronize(s);
+  if (err != hipSuccess) {
+    delete e;
+    return fail(SAC_E_HIP, std::string("engine upload: ") + hipGetErrorString(err));
+  }
+  if (cfg->precision == SAC_PREC_BF16)
+    set_lds_attrs<bf16>(e->lds_bytes);
+  else
+    set_lds_attrs<float>(e->lds_bytes);
+  rc = sac_engine_sync_params(e, stream);
+  if (rc) {
+    delete e;
+    return rc;
+  }
+  *out = e;
+  return SAC_OK;
+}
+
+void sac_engine_destroy(sac_engine* e) {
+  if (!e) return;
+  if (e->gexec) (void)hipGraphExecDestroy(e->gexec);
+  if (e->graph) (void)hipGraphDestroy(e->graph);
+  if (e->cap) (void)hipStreamDestroy(e->cap);
+  delete e;
+}
+
+int sac_engine_train(sac_engine* e, const sac_replay* rb, int32_t n_steps, const int32_t* indices, const float* eps,
+                     void* stream) {
+  if (!e) return fail(SAC_E_INVALID, "null engine");
+  int rc = check_replay(e, rb);
+  if (rc) return rc;
+  hipStream_t s = (hipStream_t)stream;
+  const size_t B = e->cfg.batch, A = e->cfg.act_dim;
+  for (int i = 0; i < n_steps; ++i)
+    launch_step(e, rb, indices ? indices + i * B : nullptr, eps ? eps + (size_t)i * 2 * B * A : nullptr, s);
+  HIPCHK(hipGetLastError());
+  return SAC_OK;
+}
+
+int sac_engine_train_graph(sac_engine* e, const sac_replay* rb, int32_t n_steps, int32_t chunk, void* stream) {
+  if (!e) return fail(SAC_E_INVALID, "null engine");
+  int rc = check_replay(e, rb);
+  if (rc) return rc;
+  if (chunk < 1) return fail(SAC_E_INVALID, "chunk >= 1");
+  hipStream_t s = (hipStream_t)stream;
+  const bool same = e->gexec && e->gchunk == chunk && !memcmp(&e->gkey, rb, sizeof(sac_replay));
+  if (!same && n_steps >= chunk) {
+    if (e->gexec) (void)hipGraphExecDestroy(e->gexec);
+    if (e->graph) (void)hipGraphDestroy(e->graph);
+    e->gexec = nullptr;
+    e->graph = nullptr;
+    if (!e->cap) HIPCHK(hipStreamCreateWithFlags(&e->cap, hipStreamNonBlocking));
+    HIPCHK(hipStreamBeginCapture(e->cap, hipStreamCaptureModeThreadLocal));
+    for (int i = 0; i < chunk; ++i) launch_step(e, rb, nullptr, nullptr, e->cap);
+    HIPCHK(hipStreamEndCapture(e->cap, &e->graph));
+    HIPCHK(hipGraphInstantiate(&e->gexec, e->graph, nullptr, nullptr, 0));
+    e->gchunk = chunk;
+    e->gkey = *rb;
+  }
+  int done = 0;
+  if (e->gexec)
+    for (; done + chunk <= n_steps; done += chunk) HIPCHK(hipGraphLaunch(e->gexec, s));
+  for (; done < n_steps; ++done) launch_step(e, rb, nullptr, nullptr, s);
+  HIPCHK(hipGetLastError());
+  return SAC_OK;
+}
+
+int sac_policy_act(sac_engine* e, const float* obs, int32_t n, const float* eps, float* action, float* log_pi,
+                   void* stream) {
+  if (!e || !obs || !action || n < 1) return fail(SAC_E_INVALID, "bad policy_act arguments");
+  hipStream_t s = (hipStream_t)stream;
+  const int blocks = (n + SAC_ROWS - 1) / SAC_ROWS;
+  if (e->cfg.precision == SAC_PREC_BF16)
+    sac_policy_act_kernel<bf16><<<blocks, SAC_THREADS, e->lds_bytes, s>>>(e->h, obs, n, eps, action, log_pi);
+  else
+    sac_policy_act_kernel<float><<<blocks, SAC_THREADS, e->lds_bytes, s>>>(e->h, obs, n, eps, action, log_pi);
+  HIPCHK(hipGetLastError());
+  return SAC_OK;
+}
+
+int sac_replay_push(const sac_replay* rb, const float* rows, int64_t n, int64_t size_host, int64_t pos_host,
+                    void* stream) {
+  if (!rb || !rows || n < 0 || rb->capacity < 1) return fail(SAC_E_INVALID, "bad replay_push arguments");
+  if (n == 0) return SAC_OK;
+  const int64_t cap = rb->capacity;
+  const int64_t skip = n > cap ? n - cap : 0;
+  const int64_t new_size = std::min(cap, size_host + n);
+  const int64_t new_pos = (pos_host + n) % cap;
+  const int64_t total = (n - skip) * (2 * rb->obs_dim + rb->act_dim + 2);
+  const int blocks = (int)std::min<int64_t>(4096, (total + 255) / 256);
+  replay_push_kernel<<<blocks, 256, 0, (hipStream_t)stream>>>(*rb, rows, n, skip, pos_host, new_size, new_pos);
+  HIPCHK(hipGetLastError());
+  return SAC_OK;
+}
+
+int sac_replay_gather(const sac_replay* rb, const int32_t* logical_idx, int32_t batch, float* s, float* a, float* r,
+                      float* s2, float* d, void* stream) {
+  if (!rb || !logical_idx || batch < 1 || !s || !a || !r || !s2 || !d) return fail(SAC_E_INVALID, "bad gather arguments");
+  const int64_t total = (int64_t)batch * (2 * rb->obs_dim + rb->act_dim + 2);
+  const int blocks = (int)std::min<int64_t>(8192, (total + 255) / 256);
+  replay_gather_kernel<<<blocks, 256, 0, (hipStream_t)stream>>>(*rb, logical_idx, batch, s, a, r, s2, d);
+  HIPCHK(hipGetLastError());
+  return SAC_OK;
+}
+
+int sac_replay_sample_indices(const sac_replay* rb, int32_t batch, uint64_t seed, uint64_t step, int32_t* out,
+                              void* stream) {
+  if (!rb || !out || batch < 1) return fail(SAC_E_INVALID, "bad sample arguments");
+  const int blocks = std::min(4096, (batch + 255) / 256);
+  replay_sample_kernel<<<blocks, 256, 0, (hipStream_t)stream>>>(rb->state, batch, seed, step, out);
+  HIPCHK(hipGetLastError());
+  return SAC_OK;
+}
+
+int sac_engine_debug_stamps(sac_engine* e, long long* dev_buf, void* stream) {
+  if (!e) return fail(SAC_E_INVALID, "null engine");
+  e->h.stamps = dev_buf;
+  (void)stream;
+  if (e->gexec) {  // graphs captured the old kernel arguments
+    (void)hipGraphExecDestroy(e->gexec);
+    (void)hipGraphDestroy(e->graph);
+    e->gexec = nullptr;
+    e->graph = nullptr;
+  }
+  return SAC_OK;
+}
+
+int sac_debug_layer_stamps(long long* host, int reset) {
+#ifdef SAC_STAMPS
+  if (reset) {
+    int z = 0;
+    HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_lcall), &z, sizeof(int)));
+    return SAC_OK;
+  }
+  HIPCHK(hipMemcpyFromSymbol(host, HIP_SYMBOL(g_lstamp), sizeof(long long) * 64 * 6));
+  return SAC_OK;
+#else
+  (void)host;
+  (void)reset;
+  return fail(SAC_E_INVALID, "not a stamps build");
+#endif
+}
+
+int sac_engine_debug_stamped(void) {
+#ifdef SAC_STAMPS
+  return 1;
+#else
+  return 0;
+#endif
+}
+
+int sac_engine_time_phases(sac_engine* e, const sac_replay* rb, int32_t n_steps, float* ms_host, void* stream) {
+  if (!e || !ms_host || n_steps < 1) return fail(SAC_E_INVALID, "bad time_phases arguments");
+  int rc = check_replay(e, rb);
+  if (rc) return rc;
+  hipStream_t s = (hipStream_t)stream;
+  std::vector<hipEvent_t> ev((size_t)n_steps * 5);
+  for (auto& x : ev) HIPCHK(hipEventCreate(&x));
+  for (int i = 0; i < n_steps; ++i) {
+    HIPCHK(hipEventRecord(ev[i * 5], s));
+    for (int p = 0; p < 4; ++p) {
+      if (e->cfg.precision == SAC_PREC_BF16)
+        launch_phase<bf16>(e, p, rb, nullptr, nullptr, s);
+      else
+        launch_phase<float>(e, p, rb, nullptr, nullptr, s);
+      HIPCHK(hipEventRecord(ev[i * 5 + p + 1], s));
+    }
+  }
+  HIPCHK(hipStreamSynchronize(s));
+  for (int p = 0; p < 4; ++p) ms_host[p] = 0.f;
+  for (int i = 0; i < n_steps; ++i)
+    for (int p = 0; p < 4; ++p) {
+      float ms = 0.f;
+      HIPCHK(hipEventElapsedTime(&ms, ev[i * 5 + p], ev[i * 5 + p + 1]));
+      ms_host[p] += ms / n_steps;
+    }
+  for (auto& x : ev) (void)hipEventDestroy(x);
+  return SAC_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,979 @@
+// sac_phases.h — device state and the four phase kernels of one SAC gradient step.
+// Included by sac_engine.hip only.  Reference cross-walk in sac_engine.hip.
+#pragma once
+#include "sac_device.h"
+
+#define SAC_DEV_LAYERS 6  // Linear layers per network supported by the kernels
+
+// ============================================================================ device state
+struct LayerDev {
+  int K, N, Kp, Np;
+  int w_off, b_off;
+  void* Wc;       // [Np][Kp] compute dtype: forward B operand
+  void* WTc;      // [Kp][Np] compute dtype: dX B operand (trainable nets)
+  void* XT;       // [Kp][Bp] layer input, transposed (trainable nets)
+  void* GT;       // [Np][Bp] d(pre-activation), transposed
+  float* dbp;     // [nrt][N] bias-gradient partial sums per row tile
+  float* pstash;  // pi only: pre-activations of the actor rows [Br][Np]
+};
+
+struct NetDev {
+  int L, hid_act, out_act;
+  float* P;
+  float* M;
+  float* V;
+  LayerDev l[SAC_DEV_LAYERS];
+};
+
+enum { NET_PI = 0, NET_Q1 = 1, NET_Q2 = 2, NET_Q1T = 3, NET_Q2T = 4 };
+
+struct EngineDev {
+  int B, Bp, Br, O, A, nrt, ld, ldo;
+  int auto_entropy;
+  float gamma, tau, ls_min, ls_max, scale, actor_lr, critic_lr, beta1, beta2, adam_eps, target_entropy;
+  double alpha_lr;
+  uint64_t seed;
+  NetDev net[5];
+  float* s_st;     // [Br][O]   states of the batch (phase A -> C)
+  float* a_st;     // [Br][A]   actor sample a~
+  float* lp_st;    // [Br]      log pi(a~|s)
+  float* head_st;  // [Br][4][A]: mu, log_std (raw), z, eps
+  float* lossp;    // [nrt][4]
+  double* alpha_state;
+  double* opt_steps;
+  uint64_t* rng_step;
+  float* stats;
+  long long* stamps;  // optional in-kernel timestamps (SAC_STAMPS builds)
+  // LDS layout (float offsets)
+  int o_X, o_Y, o_P1[SAC_DEV_LAYERS], ldp1[SAC_DEV_LAYERS], o_P2[SAC_DEV_LAYERS], ldp2[SAC_DEV_LAYERS];
+  int o_s, o_s2, o_a, o_a2, o_r, o_d, o_et, o_ea, o_out, o_outp, o_out2, o_outp2, o_lp, o_qt, o_y, o_g, o_g2,
+      o_ga, o_gout, o_slot;
+};
+
+// One 32x32 weight tile of the update phases, self-contained so a block needs a
+// single descriptor fetch before its first HBM load.
+struct TileDesc {
+  const void* GT;  // row n0 of d(pre-act)^T  [.][Bp]
+  const void* XT;  // row k0 of input^T       [.][Bp]
+  float* W;        // master weight [N][K] (layer base)
+  float* Wm;
+  float* Wv;
+  float* b;        // master bias [N]
+  float* bm;
+  float* bv;
+  void* Wc;        // packed copies [Np][Kp], [Kp][Np]
+  void* WTc;
+  float* tW;       // Polyak target master weight / bias / packed copy (critics)
+  float* tb;
+  void* tWc;
+  const float* dbp;
+  int K, N, Kp, Np, n0, k0, opt, nrt;
+};
+
+#ifdef SAC_STAMPS
+// per-call sub-layer stamps of layer_fwd_ (block 0, wave 0): [call][5]
+__device__ long long g_lstamp[64 * 6];
+__device__ int g_lcall;
+#define LSTAMP(k)                                                                            \
+  do {                                                                                       \
+    if (blockIdx.x == 0 && threadIdx.x == 0 && lcall < 64) g_lstamp[lcall * 6 + (k)] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+#else
+#define LSTAMP(k) \
+  do {            \
+  } while (0)
+#endif
+
+#ifdef SAC_STAMPS
+#define STAMP(i)                                                                               \
+  do {                                                                                         \
+    if (threadIdx.x == 0 && E.stamps) GP(long long, E.stamps)[blockIdx.x * 64 + (i)] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+#else
+#define STAMP(i) \
+  do {           \
+  } while (0)
+#endif
+
+// ============================================================================ MFMA layer steps
+// Two 16-column output tiles per wave: acc{0,1}[rt] += A(rows from LDS) x B(rows
+// b0 / b1 from HBM/L2).  Every B fragment of a batch is issued before the first
+// MFMA, so a wave pays one memory latency per batch (not per tile).  b1 == b0
+// when the wave has a single tile (duplicate loads hit L1; no divergent loads).
+template <typename T, int RT>
+__device__ __forceinline__ void mma_pair(const lf* __restrict__ arow, int lda, const AS_G T* b0, const AS_G T* b1,
+                                         bool has1, int nch, f32x4 (&acc0)[RT], f32x4 (&acc1)[RT]) {
+  constexpr int KC = MM<T>::KC;
+  constexpr int FS = 64 * MM<T>::KL;  // packed fragment stride (elements)
+  typedef typename MM<T>::Frag F;
+  int ch = 0;
+  for (; ch + 8 <= nch; ch += 8) {
+    F f0[8], f1[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      f0[u] = MM<T>::ld(b0 + (ch + u) * FS);
+      f1[u] = MM<T>::ld(b1 + (ch + u) * FS);
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) {
+        const F a = MM<T>::from_lds(arow + rt * 16 * lda + (ch + u) * KC);
+        MM<T>::mma(acc0[rt], a, f0[u]);
+        if (has1) MM<T>::mma(acc1[rt], a, f1[u]);
+      }
+  }
+  for (; ch + 2 <= nch; ch += 2) {
+    F f0[2], f1[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      f0[u] = MM<T>::ld(b0 + (ch + u) * FS);
+      f1[u] = MM<T>::ld(b1 + (ch + u) * FS);
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) {
+        const F a = MM<T>::from_lds(arow + rt * 16 * lda + (ch + u) * KC);
+        MM<T>::mma(acc0[rt], a, f0[u]);
+        if (has1) MM<T>::mma(acc1[rt], a, f1[u]);
+      }
+  }
+  if (ch < nch) {
+    const F f0 = MM<T>::ld(b0 + ch * FS), f1 = MM<T>::ld(b1 + ch * FS);
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) {
+      const F a = MM<T>::from_lds(arow + rt * 16 * lda + ch * KC);
+      MM<T>::mma(acc0[rt], a, f0);
+      if (has1) MM<T>::mma(acc1[rt], a, f1);
+    }
+  }
+}
+
+// Y[r][n] = act(sum_k X[r][k] W[n][k] + b[n]) over n < Np (padded columns -> 0).
+// P (optional) keeps the pre-activation, Pg (optional) stashes rows >= pg_row0 to HBM.
+template <typename T, int ROWS>
+__device__ __forceinline__ void layer_fwd_(const lf* __restrict__ X, int ldx, const void* Wc_, int K, int N, int Kp,
+                                           int Np, const float* bias_, int act, lf* __restrict__ P, int ldp,
+                                           lf* __restrict__ Y, int ldy, float* Pg_, int pg_row0) {
+  constexpr int RT = ROWS / 16;
+  constexpr int KC = MM<T>::KC, KL = MM<T>::KL;
+  const AS_G float* bias = GPC(float, bias_);
+  AS_G float* Pg = GP(float, Pg_);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int c = lane & 15, g = lane >> 4;
+  const AS_G T* W = GPC(T, Wc_);
+  const int NT = Np >> 4, nch = Kp / KC;
+  (void)K;
+#ifdef SAC_STAMPS
+  int lcall = 0;
+  if (blockIdx.x == 0 && threadIdx.x == 0) lcall = atomicAdd(&g_lcall, 1);
+#endif
+  LSTAMP(0);
+  for (int nt0 = wave; nt0 < NT; nt0 += 2 * SAC_NW) {
+    const int nt1 = nt0 + SAC_NW;
+    const bool has1 = nt1 < NT;
+    const int n0 = nt0 * 16 + c, n1 = (has1 ? nt1 : nt0) * 16 + c;
+    const float bn0 = bias[n0 < N ? n0 : N - 1], bn1 = bias[n1 < N ? n1 : N - 1];  // issued with the weights
+    f32x4 acc0[RT], acc1[RT];
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) acc0[rt] = acc1[rt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    LSTAMP(1);
+    mma_pair<T, RT>(X + c * ldx + g * KL, ldx, W + packed_lane<T>(nt0, Kp, lane),
+                    W + packed_lane<T>(has1 ? nt1 : nt0, Kp, lane), has1, nch, acc0, acc1);
+    LSTAMP(3);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      if (h == 1 && !has1) break;
+      const int n = h ? n1 : n0;
+      const bool nv = n < N;
+      const float bn = h ? bn1 : bn0;
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int r = rt * 16 + g * 4 + i;
+          const float p = nv ? (h ? acc1[rt][i] : acc0[rt][i]) + bn : 0.f;
+          if (P) P[r * ldp + n] = p;
+          Y[r * ldy + n] = act_fwd(act, p);
+          if (Pg && r >= pg_row0) Pg[(size_t)(r - pg_row0) * Np + n] = p;
+        }
+    }
+    LSTAMP(4);
+  }
+  LSTAMP(5);
+}
+
+// Gout[r][k] = act'(Pprev[r][k]) * sum_n G[r][n] W[n][k]   (act_prev < 0: no act')
+template <typename T, int ROWS>
+__device__ __forceinline__ void layer_bwd_(const lf* __restrict__ G, int ldg, const void* WTc_, int K, int N, int Kp,
+                                           int Np, const lf* __restrict__ Pprev, int ldp, int act_prev,
+                                           lf* __restrict__ Gout, int ldo) {
+  constexpr int RT = ROWS / 16;
+  constexpr int KC = MM<T>::KC, KL = MM<T>::KL;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int c = lane & 15, g = lane >> 4;
+  const AS_G T* WT = GPC(T, WTc_);
+  const int KT = Kp >> 4, nch = Np / KC;
+  (void)N;
+  for (int kt0 = wave; kt0 < KT; kt0 += 2 * SAC_NW) {
+    const int kt1 = kt0 + SAC_NW;
+    const bool has1 = kt1 < KT;
+    const int k0 = kt0 * 16 + c, k1 = (has1 ? kt1 : kt0) * 16 + c;
+    f32x4 acc0[RT], acc1[RT];
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) acc0[rt] = acc1[rt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    mma_pair<T, RT>(G + c * ldg + g * KL, ldg, WT + packed_lane<T>(kt0, Np, lane),
+                    WT + packed_lane<T>(has1 ? kt1 : kt0, Np, lane), has1, nch, acc0, acc1);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      if (h == 1 && !has1) break;
+      const int k = h ? k1 : k0;
+      const bool kv = k < K;
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int r = rt * 16 + g * 4 + i;
+          const float a = h ? acc1[rt][i] : acc0[rt][i];
+          float v = 0.f;
+          if (kv) v = act_prev >= 0 ? act_bwd(act_prev, Pprev[r * ldp + k], a) : a;
+          Gout[r * ldo + k] = v;
+        }
+    }
+  }
+}
+
+template <typename T, int ROWS>
+__device__ __forceinline__ void layer_fwd(const lf* X, int ldx, const LayerDev& L, const float* bias, int act, lf* P,
+                                          int ldp, lf* Y, int ldy, float* Pg, int pg_row0) {
+  layer_fwd_<T, ROWS>(X, ldx, L.Wc, L.K, L.N, L.Kp, L.Np, bias, act, P, ldp, Y, ldy, Pg, pg_row0);
+}
+template <typename T, int ROWS>
+__device__ __forceinline__ void layer_bwd(const lf* G, int ldg, const LayerDev& L, const lf* Pprev, int ldp,
+                                          int act_prev, lf* Gout, int ldo) {
+  layer_bwd_<T, ROWS>(G, ldg, L.WTc, L.K, L.N, L.Kp, L.Np, Pprev, ldp, act_prev, Gout, ldo);
+}
+
+// dst[k][col0 + r] = src[r][k] (0 for k >= K or r >= nvalid), k < Kp; with
+// dbp != null also dbp[blockIdx.x][k] = sum_{r<nvalid} src[r][k] (k < K).
+template <typename T, int ROWS>
+__device__ __forceinline__ void store_T(const lf* __restrict__ src, int lds_ld, int Kp, int K, void* dst_,
+                                                 int Bp, int col0, int nvalid, float* dbp_) {
+  AS_G T* dst = GP(T, dst_);
+  AS_G float* dbp = GP(float, dbp_);
+  constexpr int CH = ROWS / 8;
+  const int span = (Kp * CH + 63) / 64 * 64;  // whole waves iterate together (shuffles)
+  for (int i = threadIdx.x; i < span; i += SAC_THREADS) {
+    const bool live = i < Kp * CH;
+    const int k = i / CH, ch = i % CH;
+    T v[8];
+    float s = 0.f;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int r = ch * 8 + q;
+      const float x = (live && r < nvalid && k < K) ? src[r * lds_ld + k] : 0.f;
+      s += x;
+      v[q] = MM<T>::cvt(x);
+    }
+    if (live) {
+      AS_G T* d = dst + (size_t)k * Bp + col0 + ch * 8;
+      if constexpr (sizeof(T) == 2) {
+        *(AS_G u32x4*)d = *(const u32x4*)v;
+      } else {
+        *(AS_G u32x4*)d = *(const u32x4*)v;
+        *(AS_G u32x4*)(d + 4) = *(const u32x4*)(v + 4);
+      }
+    }
+    if (dbp) {
+#pragma unroll
+      for (int o = 1; o < CH; o <<= 1) s += __shfl_xor(s, o, 64);
+      if (live && ch == 0 && k < K) dbp[(size_t)blockIdx.x * K + k] = s;
+    }
+  }
+}
+
+// Full MLP forward over ROWS rows: hidden layers ping-pong Xb/Yb (stride ld), the
+// output layer writes (Pout, Yout) with stride ldo.  keepP: per-layer
+// pre-activations into lds[o_P[l]] (stride ldp[l]).  storeXT: each layer's input
+// transposed into L.XT (ROWS must be SAC_ROWS).
+template <typename T, int ROWS>
+__device__ __forceinline__ void mlp_forward(const NetDev& net, lf* Xb, lf* Yb, int ld, lf* Pout, lf* Yout, int ldo,
+                                            const int* o_P, const int* ldp, lf* lds, bool keepP, bool storeXT, int Bp,
+                                            int col0, int nvalid) {
+  lf* X = Xb;
+  lf* Y = Yb;
+  for (int l = 0; l < net.L; ++l) {
+    const LayerDev& Ly = net.l[l];
+    const bool out = l == net.L - 1;
+    if (storeXT) {
+      if constexpr (ROWS == SAC_ROWS) store_T<T, ROWS>(X, ld, Ly.Kp, Ly.K, Ly.XT, Bp, col0, nvalid, nullptr);
+    }
+    if (out)
+      layer_fwd<T, ROWS>(X, ld, Ly, net.P + Ly.b_off, net.out_act, Pout, ldo, Yout, ldo, nullptr, 0);
+    else
+      layer_fwd<T, ROWS>(X, ld, Ly, net.P + Ly.b_off, net.hid_act, keepP ? lds + o_P[l] : nullptr,
+                         keepP ? ldp[l] : 0, Y, ld, nullptr, 0);
+    __syncthreads();
+    lf* t = X;
+    X = Y;
+    Y = t;
+  }
+}
+
+// Backward from d(output pre-activation) Gout [ROWS][ldo] down to layer 0's
+// pre-activation gradient.  storeGT: each layer's dY^T + bias partial sums.
+// Returns the buffer (stride ld) holding d(pre-act of layer 0).
+template <typename T, int ROWS>
+__device__ __forceinline__ lf* mlp_backward(const NetDev& net, const lf* Gout, int ldo, lf* Xb, lf* Yb, int ld,
+                                            const int* o_P, const int* ldp, lf* lds, bool storeGT, int Bp, int col0,
+                                            int nvalid) {
+  const int Lh = net.L - 1;
+  const LayerDev& Lo = net.l[Lh];
+  if (storeGT) store_T<T, ROWS>(Gout, ldo, Lo.Np, Lo.N, Lo.GT, Bp, col0, nvalid, Lo.dbp);
+  layer_bwd<T, ROWS>(Gout, ldo, Lo, lds + o_P[Lh - 1], ldp[Lh - 1], net.hid_act, Yb, ld);
+  __syncthreads();
+  lf* G = Yb;
+  lf* Gn = Xb;
+  for (int l = Lh - 1; l >= 0; --l) {
+    const LayerDev& Ly = net.l[l];
+    if (storeGT) store_T<T, ROWS>(G, ld, Ly.Np, Ly.N, Ly.GT, Bp, col0, nvalid, Ly.dbp);
+    if (l == 0) break;
+    layer_bwd<T, ROWS>(G, ld, Ly, lds + o_P[l - 1], ldp[l - 1], net.hid_act, Gn, ld);
+    __syncthreads();
+    lf* t = G;
+    G = Gn;
+    Gn = t;
+  }
+  __syncthreads();
+  return G;
+}
+
+#define LOG2F 0.69314718055994530942f
+#define HALF_LOG_2PI 0.91893853320467274178f
+
+__device__ __forceinline__ float fmin_nan(float a, float b) { return (a != a) ? a : (a < b ? a : b); }
+
+// ============================================================================ phase A
+// sample + gather, pi on [s'; s], target twin-Q -> y, critics forward + backward.
+template <typename T>
+__global__ void __launch_bounds__(SAC_THREADS) sac_target_critic(const EngineDev E, sac_replay rb,
+                                                                  const int32_t* __restrict__ inj_idx_,
+                                                                  const float* __restrict__ inj_eps_) {
+  extern __shared__ float lds_raw[];
+  lf* lds = (lf*)lds_raw;
+  constexpr int R = SAC_ROWS;
+  const int tid = threadIdx.x;
+  STAMP(0);
+  const int B = E.B, Bp = E.Bp, O = E.O, A = E.A, ld = E.ld, ldo = E.ldo;
+  const int r0 = blockIdx.x * R;
+  const int nvalid = min(R, B - r0);
+  const AS_G int32_t* inj_idx = GPC(int32_t, inj_idx_);
+  const AS_G float* inj_eps = GPC(float, inj_eps_);
+  lf* Xb = lds + E.o_X;
+  lf* Yb = lds + E.o_Y;
+  lf* sB = lds + E.o_s;
+  lf* s2B = lds + E.o_s2;
+  lf* aB = lds + E.o_a;
+  lf* a2B = lds + E.o_a2;
+  lf* rB = lds + E.o_r;
+  lf* dB = lds + E.o_d;
+  lf* etB = lds + E.o_et;
+  lf* eaB = lds + E.o_ea;
+  lf* outB = lds + E.o_out;
+  lf* outP = lds + E.o_outp;
+  lf* lp2B = lds + E.o_lp;
+  lf* qtB = lds + E.o_qt;
+  lf* yB = lds + E.o_y;
+  lf* gqB = lds + E.o_gout;
+  AS_L int64_t* slotB = (AS_L int64_t*)(lds + E.o_slot);
+  const NetDev& pi = E.net[NET_PI];
+  const AS_G float* obs = GPC(float, rb.obs);
+  const AS_G float* nobs = GPC(float, rb.next_obs);
+  const AS_G float* ract = GPC(float, rb.act);
+  const AS_G float* rrew = GPC(float, rb.rew);
+  const AS_G float* rdone = GPC(float, rb.done);
+  AS_G float* stats = GP(float, E.stats);
+
+  if (blockIdx.x == 0 && tid < 4 && (tid < 3 || E.auto_entropy)) GP(double, E.opt_steps)[tid] += 1.0;
+
+  // ---- sample (replay_buffer.py:32-39) + gather (agent.py:166-193)
+  const uint64_t step = *GPC(uint64_t, E.rng_step);
+  if (tid < R) {
+    int64_t slot = -1;
+    const int b = r0 + tid;
+    if (b < B) {
+      const int64_t size = GPC(int64_t, rb.state)[0], pos = GPC(int64_t, rb.state)[1];
+      int64_t li;
+      if (inj_idx) {
+        li = inj_idx[b];
+      } else {
+        const Feistel f = feistel_make(E.seed, step, size);
+        li = feistel_sample(f, b, size);
+      }
+      slot = size < rb.capacity ? li : (pos + li) % rb.capacity;
+    }
+    slotB[tid] = slot;
+  }
+  __syncthreads();
+  for (int i = tid; i < R * O; i += SAC_THREADS) {
+    const int r = i / O, j = i % O;
+    const int64_t sl = slotB[r];
+    sB[i] = sl >= 0 ? obs[sl * O + j] : 0.f;
+    s2B[i] = sl >= 0 ? nobs[sl * O + j] : 0.f;
+  }
+  for (int i = tid; i < R * A; i += SAC_THREADS) {
+    const int64_t sl = slotB[i / A];
+    aB[i] = sl >= 0 ? ract[sl * A + i % A] : 0.f;
+  }
+  if (tid < R) {
+    const int64_t sl = slotB[tid];
+    rB[tid] = sl >= 0 ? rrew[sl] : 0.f;
+    dB[tid] = sl >= 0 ? rdone[sl] : 0.f;
+  }
+  {
+    const int NP = (A + 1) / 2;
+    for (int i = tid; i < 2 * R * NP; i += SAC_THREADS) {
+      const int which = i / (R * NP), rem = i % (R * NP), r = rem / NP, p = rem % NP;
+      const int b = r0 + r;
+      float n0 = 0.f, n1 = 0.f;
+      if (b < B) {
+        if (inj_eps) {
+          n0 = inj_eps[((size_t)which * B + b) * A + 2 * p];
+          if (2 * p + 1 < A) n1 = inj_eps[((size_t)which * B + b) * A + 2 * p + 1];
+        } else {
+          philox_normal2(E.seed, step, (uint32_t)b, (uint32_t)which, (uint32_t)p, n0, n1);
+        }
+      }
+      lf* dst = which ? eaB : etB;
+      dst[r * A + 2 * p] = n0;
+      if (2 * p + 1 < A) dst[r * A + 2 * p + 1] = n1;
+    }
+  }
+  __syncthreads();
+  STAMP(1);
+  for (int i = tid; i < R * O; i += SAC_THREADS) GP(float, E.s_st)[(size_t)r0 * O + i] = sB[i];
+
+  // ---- pi forward on [s' ; s] (2R rows): target sample + actor sample
+  {
+    const int Kp0 = pi.l[0].Kp;
+    for (int i = tid; i < 2 * R * Kp0; i += SAC_THREADS) {
+      const int r = i / Kp0, k = i % Kp0;
+      Xb[r * ld + k] = k < O ? (r < R ? s2B[r * O + k] : sB[(r - R) * O + k]) : 0.f;
+    }
+    __syncthreads();
+    lf* X = Xb;
+    lf* Y = Yb;
+    for (int l = 0; l < pi.L; ++l) {
+      const LayerDev& Ly = pi.l[l];
+      store_T<T, R>(X + R * ld, ld, Ly.Kp, Ly.K, Ly.XT, Bp, r0, nvalid, nullptr);  // actor rows' input
+      if (l == pi.L - 1)
+        layer_fwd<T, 2 * R>(X, ld, Ly, pi.P + Ly.b_off, pi.out_act, outP, ldo, outB, ldo, Ly.pstash + (size_t)r0 * Ly.Np, R);
+      else
+        layer_fwd<T, 2 * R>(X, ld, Ly, pi.P + Ly.b_off, pi.hid_act, nullptr, 0, Y, ld, Ly.pstash + (size_t)r0 * Ly.Np, R);
+      __syncthreads();
+      STAMP(2 + l);
+      lf* t = X;
+      X = Y;
+      Y = t;
+    }
+    // squashed-Gaussian head (models.py:79-87): one lane per (row, action dim),
+    // each row's A lanes contiguous inside one wave (AP = pow2 >= A), summed by shuffles
+    {
+      const int AP = A <= 1 ? 1 : 1 << (32 - __builtin_clz(A - 1));
+      const int rows_per_pass = SAC_THREADS / AP;
+      for (int base = 0; base < 2 * R; base += rows_per_pass) {
+        const int r = base + tid / AP, j = tid % AP;
+        const bool live = r < 2 * R && j < A;
+        float lp = 0.f, corr = 0.f;
+        if (live) {
+          const bool actor = r >= R;
+          const int rr = actor ? r - R : r;
+          const int b = r0 + rr;
+          const lf* o = outB + r * ldo;
+          const float mu = o[j], lsr = o[A + j], e = (actor ? eaB : etB)[rr * A + j];
+          const float lo = E.ls_min, hi = E.ls_max;
+          const float ls = lsr < lo ? lo : (lsr > hi ? hi : lsr);
+          const float sd = expf(ls);
+          const float z = mu + e * sd;
+          const float act = tanhf(z) * E.scale;
+          const float diff = z - mu;
+          const float var = sd * sd;
+          lp = -(diff * diff) / (2.f * var) - logf(sd) - HALF_LOG_2PI;
+          corr = 2.f * ((LOG2F - z) - softplus20(-2.f * z));
+          if (actor) {
+            AS_G float* h = GP(float, E.head_st) + (size_t)b * 4 * A;
+            h[j] = mu;
+            h[A + j] = lsr;
+            h[2 * A + j] = z;
+            h[3 * A + j] = e;
+            GP(float, E.a_st)[(size_t)b * A + j] = act;
+          } else {
+            a2B[rr * A + j] = act;
+          }
+        }
+        for (int o = 1; o < AP; o <<= 1) {
+          lp += __shfl_xor(lp, o, 64);
+          corr += __shfl_xor(corr, o, 64);
+        }
+        if (live && j == 0) {
+          const bool actor = r >= R;
+          const int rr = actor ? r - R : r;
+          const int b = r0 + rr;
+          const float v = lp - corr;
+          if (actor) {
+            GP(float, E.lp_st)[b] = v;
+            if (b < B) stats[4 + B + b] = v;
+          } else {
+            lp2B[rr] = v;
+          }
+        }
+      }
+    }
+    __syncthreads();
+    STAMP(6);
+  }
+
+  // ---- target twin-Q (agent.py:195-211)
+  const float alpha32 = (float)*GPC(double, E.alpha_state + 1);
+  for (int t = 0; t < 2; ++t) {
+    const NetDev& q = E.net[NET_Q1T + t];
+    const int Kp0 = q.l[0].Kp;
+    for (int i = tid; i < R * Kp0; i += SAC_THREADS) {
+      const int r = i / Kp0, k = i % Kp0;
+      Xb[r * ld + k] = k < O ? s2B[r * O + k] : (k < O + A ? a2B[r * A + (k - O)] : 0.f);
+    }
+    __syncthreads();
+    mlp_forward<T, R>(q, Xb, Yb, ld, outP, outB, ldo, E.o_P1, E.ldp1, lds, false, false, Bp, r0, nvalid);
+    if (tid < R) qtB[t * R + tid] = outB[tid * ldo];
+    __syncthreads();
+    STAMP(7 + t);
+  }
+  if (tid < R) {
+    const int b = r0 + tid;
+    const float mq = fmin_nan(qtB[tid], qtB[R + tid]);
+    const float y = rB[tid] + (E.gamma * (1.f - dB[tid])) * (mq - alpha32 * lp2B[tid]);
+    yB[tid] = y;
+    if (b < B) stats[4 + b] = y;
+  }
+  __syncthreads();
+
+  // ---- critics: forward, MSE, backward (agent.py:213-236)
+  for (int qi = 0; qi < 2; ++qi) {
+    const NetDev& q = E.net[NET_Q1 + qi];
+    const int Kp0 = q.l[0].Kp;
+    for (int i = tid; i < R * Kp0; i += SAC_THREADS) {
+      const int r = i / Kp0, k = i % Kp0;
+      Xb[r * ld + k] = k < O ? sB[r * O + k] : (k < O + A ? aB[r * A + (k - O)] : 0.f);
+    }
+    __syncthreads();
+    // the layer-0 input (s, a) is shared by Q1 and Q2: its X^T is stored once
+    if (qi == 0) store_T<T, R>(Xb, ld, Kp0, q.l[0].K, q.l[0].XT, Bp, r0, nvalid, nullptr);
+    lf* X = Xb;
+    lf* Y = Yb;
+    for (int l = 0; l < q.L; ++l) {
+      const LayerDev& Ly = q.l[l];
+      if (l > 0) store_T<T, R>(X, ld, Ly.Kp, Ly.K, Ly.XT, Bp, r0, nvalid, nullptr);
+      if (l == q.L - 1)
+        layer_fwd<T, R>(X, ld, Ly, q.P + Ly.b_off, q.out_act, outP, ldo, outB, ldo, nullptr, 0);
+      else
+        layer_fwd<T, R>(X, ld, Ly, q.P + Ly.b_off, q.hid_act, lds + E.o_P1[l], E.ldp1[l], Y, ld, nullptr, 0);
+      __syncthreads();
+      lf* t = X;
+      X = Y;
+      Y = t;
+    }
+    STAMP(10 + 2 * qi);
+    if (tid < 64) {  // wave 0: loss partial + dL/dq (mse_loss backward: 2(q-y)/B)
+      float sq = 0.f;
+      if (tid < R) {
+        const bool v = tid < nvalid;
+        const float d = outB[tid * ldo] - yB[tid];
+        sq = v ? d * d : 0.f;
+        float g = v ? (2.0f / (float)B) * d : 0.f;
+        if (q.out_act != ACT_ID) g = act_bwd(q.out_act, outP[tid * ldo], g);
+        for (int n = 0; n < 32; ++n) gqB[tid * ldo + n] = n == 0 ? g : 0.f;
+      }
+      sq = wave_sum(sq);
+      if (tid == 0) GP(float, E.lossp)[blockIdx.x * 4 + qi] = sq;
+    }
+    __syncthreads();
+    mlp_backward<T, R>(q, gqB, ldo, Xb, Yb, ld, E.o_P1, E.ldp1, lds, true, Bp, r0, nvalid);
+    STAMP(11 + 2 * qi);
+  }
+}
+
+// ============================================================================ phase C
+// critics on (s, a~) with the updated weights, d a~, head backward, pi backward.
+template <typename T>
+__global__ void __launch_bounds__(SAC_THREADS) sac_actor(const EngineDev E) {
+  extern __shared__ float lds_raw[];
+  lf* lds = (lf*)lds_raw;
+  constexpr int R = SAC_ROWS;
+  const int tid = threadIdx.x;
+  STAMP(32);
+  const int B = E.B, Bp = E.Bp, O = E.O, A = E.A, ld = E.ld, ldo = E.ldo;
+  const int r0 = blockIdx.x * R;
+  const int nvalid = min(R, B - r0);
+  lf* Xb = lds + E.o_X;
+  lf* Yb = lds + E.o_Y;
+  lf* sB = lds + E.o_s;
+  lf* aB = lds + E.o_a;
+  lf* lpB = lds + E.o_lp;
+  lf* g1B = lds + E.o_g;
+  lf* g2B = lds + E.o_g2;
+  lf* gaB = lds + E.o_ga;
+  lf* goutB = lds + E.o_gout;
+  lf* out1 = lds + E.o_out;
+  lf* outP1 = lds + E.o_outp;
+  lf* out2 = lds + E.o_out2;
+  lf* outP2 = lds + E.o_outp2;
+  const NetDev& pi = E.net[NET_PI];
+  const float alpha32 = (float)*GPC(double, E.alpha_state + 1);
+
+  for (int i = tid; i < R * O; i += SAC_THREADS) sB[i] = GPC(float, E.s_st)[(size_t)r0 * O + i];
+  for (int i = tid; i < R * A; i += SAC_THREADS) {
+    aB[i] = GPC(float, E.a_st)[(size_t)r0 * A + i];
+    gaB[i] = 0.f;
+  }
+  if (tid < R) lpB[tid] = GPC(float, E.lp_st)[r0 + tid];
+  __syncthreads();
+
+  // ---- Q1, Q2 on (s, a~) with the updated critics (agent.py:244-248)
+  for (int qi = 0; qi < 2; ++qi) {
+    const NetDev& q = E.net[NET_Q1 + qi];
+    const int Kp0 = q.l[0].Kp;
+    for (int i = tid; i < R * Kp0; i += SAC_THREADS) {
+      const int r = i / Kp0, k = i % Kp0;
+      Xb[r * ld + k] = k < O ? sB[r * O + k] : (k < O + A ? aB[r * A + (k - O)] : 0.f);
+    }
+    __syncthreads();
+    mlp_forward<T, R>(q, Xb, Yb, ld, qi ? outP2 : outP1, qi ? out2 : out1, ldo, qi ? E.o_P2 : E.o_P1,
+                      qi ? E.ldp2 : E.ldp1, lds, true, false, Bp, r0, nvalid);
+    STAMP(36 + qi);
+  }
+  // ---- L_pi = mean(alpha logpi - min Q) (agent.py:251-252); min backward splits ties
+  if (tid < 64) {
+    float term = 0.f;
+    if (tid < R) {
+      const bool v = tid < nvalid;
+      const float q1 = out1[tid * ldo], q2 = out2[tid * ldo];
+      const float m = fmin_nan(q1, q2);
+      term = v ? alpha32 * lpB[tid] - m : 0.f;
+      const float gm = v ? -1.0f / (float)B : 0.f;
+      float g1 = (q1 == q2) ? gm * 0.5f : (q1 > q2 ? 0.f : gm);
+      float g2 = (q1 == q2) ? gm * 0.5f : (q1 < q2 ? 0.f : gm);
+      if (E.net[NET_Q1].out_act != ACT_ID) {
+        g1 = act_bwd(E.net[NET_Q1].out_act, outP1[tid * ldo], g1);
+        g2 = act_bwd(E.net[NET_Q2].out_act, outP2[tid * ldo], g2);
+      }
+      for (int n = 0; n < 32; ++n) {
+        g1B[tid * ldo + n] = n == 0 ? g1 : 0.f;
+        g2B[tid * ldo + n] = n == 0 ? g2 : 0.f;
+      }
+    }
+    term = wave_sum(term);
+    if (tid == 0) GP(float, E.lossp)[blockIdx.x * 4 + 2] = term;
+  }
+  __syncthreads();
+
+  // ---- d a~ through both critics: dX of layer 0, action columns
+  for (int qi = 0; qi < 2; ++qi) {
+    const NetDev& q = E.net[NET_Q1 + qi];
+    lf* G0 = mlp_backward<T, R>(q, qi ? g2B : g1B, ldo, Xb, Yb, ld, qi ? E.o_P2 : E.o_P1, qi ? E.ldp2 : E.ldp1, lds,
+                                false, Bp, r0, nvalid);
+    lf* Gx = (G0 == Xb) ? Yb : Xb;
+    layer_bwd<T, R>(G0, ld, q.l[0], nullptr, 0, -1, Gx, ld);
+    __syncthreads();
+    for (int i = tid; i < R * A; i += SAC_THREADS) gaB[i] += Gx[(i / A) * ld + O + i % A];
+    __syncthreads();
+    STAMP(38 + qi);
+  }
+
+  // ---- squashed-Gaussian head backward + pi backward (agent.py:255-257)
+  for (int l = 0; l < pi.L - 1; ++l) {
+    const LayerDev& Ly = pi.l[l];
+    const int ldp = E.ldp1[l];
+    lf* P = lds + E.o_P1[l];
+    const AS_G float* ps = GPC(float, Ly.pstash) + (size_t)r0 * Ly.Np;
+    for (int i = tid; i < R * Ly.Np; i += SAC_THREADS) P[(i / Ly.Np) * ldp + i % Ly.Np] = ps[i];
+  }
+  for (int i = tid; i < R * A; i += SAC_THREADS) {  // one lane per (row, action dim)
+    const int r = i / A, j = i % A, b = r0 + r;
+    const bool v = r < nvalid;
+    const float gl = v ? alpha32 * (1.0f / (float)B) : 0.f;
+    const AS_G float* h = GPC(float, E.head_st) + (size_t)b * 4 * A;
+    const float lo = E.ls_min, hi = E.ls_max, scale = E.scale;
+    const float mu = h[j], lsr = h[A + j], z = h[2 * A + j], e = h[3 * A + j];
+    const float ls = lsr < lo ? lo : (lsr > hi ? hi : lsr);
+    const float sd = expf(ls);
+    const float t = tanhf(z);
+    const float diff = z - mu, var = sd * sd;
+    float g_z = (gaB[r * A + j] * scale) * (1.f - t * t);
+    g_z = g_z + (-gl) * 2.f * (-1.f + 2.f * softplus20_grad(-2.f * z));
+    const float two_var = 2.f * var;
+    const float g_sq = -gl / two_var;
+    const float g_twovar = gl * (diff * diff) / (two_var * two_var);
+    const float g_var = 2.f * g_twovar;
+    float g_std = 2.f * sd * g_var - gl / sd;
+    const float g_diff = 2.f * diff * g_sq;
+    g_z = g_z + g_diff;
+    const float g_mu = -g_diff + g_z;
+    g_std = g_std + g_z * e;
+    const float g_ls = g_std * sd;
+    const bool in_range = (lsr >= lo) && (lsr <= hi);
+    float gm = v ? g_mu : 0.f, gs = (v && in_range) ? g_ls : 0.f;
+    if (pi.out_act != ACT_ID) {
+      const LayerDev& Lo = pi.l[pi.L - 1];
+      const AS_G float* ps = GPC(float, Lo.pstash) + (size_t)b * Lo.Np;
+      gm = act_bwd(pi.out_act, ps[j], gm);
+      gs = act_bwd(pi.out_act, ps[A + j], gs);
+    }
+    goutB[r * ldo + j] = gm;
+    goutB[r * ldo + A + j] = gs;
+  }
+  {
+    const int NOp = 32 * ((2 * A + 31) / 32), pad = NOp - 2 * A;
+    for (int i = tid; i < R * pad; i += SAC_THREADS) goutB[(i / pad) * ldo + 2 * A + i % pad] = 0.f;
+  }
+  __syncthreads();
+  mlp_backward<T, R>(pi, goutB, ldo, Xb, Yb, ld, E.o_P1, E.ldp1, lds, true, Bp, r0, nvalid);
+  STAMP(35);
+}
+
+// ============================================================================ phases B / D
+__device__ __forceinline__ float adam_elem(float& p, float& m, float& v, float g, float w1, float b2, float w2,
+                                           float bc2s, float eps, float neg_step) {
+  const float mm = m + w1 * (g - m);  // exp_avg.lerp_(grad, 1-beta1)
+  float vv = v * b2;                  // exp_avg_sq.mul_(beta2)
+  vv = vv + (w2 * g) * g;             //   .addcmul_(grad, grad, 1-beta2)
+  const float denom = sqrtf(vv) / bc2s + eps;
+  const float pn = p + (neg_step * mm) / denom;  // param.addcdiv_(exp_avg, denom, -step_size)
+  m = mm;
+  v = vv;
+  p = pn;
+  return pn;
+}
+
+template <typename T>
+__device__ __forceinline__ void dw_adam_tile(const EngineDev& E, const TileDesc* tdp, float lr, bool polyak) {
+  constexpr int KC = MM<T>::KC, KL = MM<T>::KL;
+  __shared__ float red[32][9];
+  const TileDesc td = *tdp;
+  const int Bp = E.Bp;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int c = lane & 15, g = lane >> 4;
+  const int ns = (wave >> 1) * 16, ks = (wave & 1) * 16;
+  const int n0 = td.n0 + ns, k0 = td.k0 + ks;
+  AS_G float* W = GP(float, td.W);
+  AS_G float* Wm = GP(float, td.Wm);
+  AS_G float* Wv = GP(float, td.Wv);
+  AS_G float* tW = GP(float, td.tW);
+  // this lane's master / moment elements, fetched before the dW GEMM
+  const int k = k0 + c;
+  float p[4], m[4], v[4], tp[4];
+  bool ok[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int n = n0 + g * 4 + i;
+    ok[i] = n < td.N && k < td.K;
+    const size_t idx = ok[i] ? (size_t)n * td.K + k : 0;
+    p[i] = W[idx];
+    m[i] = Wm[idx];
+    v[i] = Wv[idx];
+    tp[i] = polyak ? tW[idx] : 0.f;
+  }
+  // bias gradient: 32 rows x 8 slices of the row-tile partial sums
+  const bool do_bias = td.k0 == 0;
+  float bsum = 0.f;
+  const int bn = threadIdx.x >> 3, bs = threadIdx.x & 7;
+  if (do_bias && td.n0 + bn < td.N)
+    for (int rt = bs; rt < td.nrt; rt += 8) bsum += GPC(float, td.dbp)[(size_t)rt * td.N + td.n0 + bn];
+
+  const AS_G T* arow = GPC(T, td.GT) + (size_t)(ns + c) * Bp + g * KL;
+  const AS_G T* brow = GPC(T, td.XT) + (size_t)(ks + c) * Bp + g * KL;
+  const int nch = Bp / KC;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  int ch = 0;
+  for (; ch + 8 <= nch; ch += 8) {
+    typename MM<T>::Frag a[8], b[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      a[u] = MM<T>::ld(arow + (ch + u) * KC);
+      b[u] = MM<T>::ld(brow + (ch + u) * KC);
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) MM<T>::mma(acc, a[u], b[u]);
+  }
+  for (; ch < nch; ++ch) MM<T>::mma(acc, MM<T>::ld(arow + ch * KC), MM<T>::ld(brow + ch * KC));
+
+  const double t = GPC(double, E.opt_steps)[td.opt];
+  const double bc1 = 1.0 - pow((double)E.beta1, t);
+  const double bc2 = 1.0 - pow((double)E.beta2, t);
+  const float neg_step = (float)(-((double)lr / bc1));
+  const float bc2s = (float)sqrt(bc2);
+  const float w1 = (float)(1.0 - (double)E.beta1), b2 = E.beta2, w2 = (float)(1.0 - (double)E.beta2);
+  const float eps = E.adam_eps, tau = E.tau, omt = (float)(1.0 - (double)E.tau);
+  AS_G T* Wc = GP(T, td.Wc);
+  AS_G T* WTc = GP(T, td.WTc);
+  AS_G T* tWc = GP(T, td.tWc);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    if (!ok[i]) continue;
+    const int n = n0 + g * 4 + i;
+    const size_t idx = (size_t)n * td.K + k;
+    const float pn = adam_elem(p[i], m[i], v[i], acc[i], w1, b2, w2, bc2s, eps, neg_step);
+    W[idx] = p[i];
+    Wm[idx] = m[i];
+    Wv[idx] = v[i];
+    Wc[packed_off<T>(n, k, td.Kp)] = MM<T>::cvt(pn);
+    WTc[packed_off<T>(k, n, td.Np)] = MM<T>::cvt(pn);
+    if (polyak) {
+      const float tn = tau * pn + omt * tp[i];
+      tW[idx] = tn;
+      tWc[packed_off<T>(n, k, td.Kp)] = MM<T>::cvt(tn);
+    }
+  }
+  if (do_bias) {
+    red[bn][bs] = bsum;
+    __syncthreads();
+    if (threadIdx.x < 32) {
+      const int n = td.n0 + threadIdx.x;
+      if (n < td.N) {
+        float gb = 0.f;
+        for (int s = 0; s < 8; ++s) gb += red[threadIdx.x][s];
+        AS_G float* bp = GP(float, td.b);
+        AS_G float* bm = GP(float, td.bm);
+        AS_G float* bv = GP(float, td.bv);
+        float pb = bp[n], mb = bm[n], vb = bv[n];
+        const float pn = adam_elem(pb, mb, vb, gb, w1, b2, w2, bc2s, eps, neg_step);
+        bp[n] = pb;
+        bm[n] = mb;
+        bv[n] = vb;
+        if (polyak) GP(float, td.tb)[n] = tau * pn + omt * GP(float, td.tb)[n];
+      }
+    }
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) sac_critic_update(const EngineDev E, const TileDesc* __restrict__ tiles) {
+  dw_adam_tile<T>(E, tiles + blockIdx.x, E.critic_lr, true);
+}
+
+__device__ __forceinline__ void alpha_and_losses(const EngineDev& E) {
+  __shared__ float red[5][256];
+  const int tid = threadIdx.x, B = E.B;
+  const float H = E.target_entropy;
+  AS_G double* st = GP(double, E.alpha_state);
+  const float la32 = (float)st[0];
+  const float mB = -1.0f / (float)B;
+  const AS_G float* lp = GPC(float, E.lp_st);
+  const AS_G float* lossp = GPC(float, E.lossp);
+  float sg = 0.f, sl = 0.f, l0 = 0.f, l1 = 0.f, l2 = 0.f;
+  for (int b = tid; b < B; b += blockDim.x) {
+    const float term = lp[b] + H;
+    sg += mB * term;
+    sl += la32 * term;
+  }
+  for (int rt = tid; rt < E.nrt; rt += blockDim.x) {
+    l0 += lossp[rt * 4 + 0];
+    l1 += lossp[rt * 4 + 1];
+    l2 += lossp[rt * 4 + 2];
+  }
+  red[0][tid] = sg;
+  red[1][tid] = sl;
+  red[2][tid] = l0;
+  red[3][tid] = l1;
+  red[4][tid] = l2;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if (tid < s)
+      for (int j = 0; j < 5; ++j) red[j][tid] += red[j][tid + s];
+    __syncthreads();
+  }
+  if (tid == 0) {
+    AS_G float* stats = GP(float, E.stats);
+    stats[0] = red[2][0] / (float)B;
+    stats[1] = red[3][0] / (float)B;
+    stats[2] = red[4][0] / (float)B;
+    if (E.auto_entropy) {
+      stats[3] = -(red[1][0] / (float)B);
+      const double gr = (double)red[0][0];
+      const double b1 = (double)E.beta1, b2 = (double)E.beta2;
+      const double m = st[2] + (1.0 - b1) * (gr - st[2]);
+      const double v = st[3] * b2 + (1.0 - b2) * gr * gr;
+      const double t = GPC(double, E.opt_steps)[3];
+      const double bc1 = 1.0 - pow(b1, t), bc2 = 1.0 - pow(b2, t);
+      const double denom = sqrt(v) / sqrt(bc2) + (double)E.adam_eps;
+      const double la = st[0] + (-(E.alpha_lr / bc1)) * m / denom;
+      st[0] = la;
+      st[1] = exp(la);
+      st[2] = m;
+      st[3] = v;
+    } else {
+      stats[3] = __builtin_nanf("");
+    }
+    *GP(uint64_t, E.rng_step) += 1;
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) sac_actor_update(const EngineDev E, const TileDesc* __restrict__ tiles,
+                                                        int ntiles) {
+  if ((int)blockIdx.x < ntiles)
+    dw_adam_tile<T>(E, tiles + blockIdx.x, E.actor_lr, false);
+  else
+    alpha_and_losses(E);
+}
+
+// ============================================================================ policy
+template <typename T>
+__global__ void __launch_bounds__(SAC_THREADS) sac_policy_act_kernel(const EngineDev E, const float* __restrict__ obs_, int n,
+                                                             const float* __restrict__ eps_, float* __restrict__ action_,
+                                                             float* __restrict__ log_pi_) {
+  extern __shared__ float lds_raw[];
+  lf* lds = (lf*)lds_raw;
+  constexpr int R = SAC_ROWS;
+  const int tid = threadIdx.x, O = E.O, A = E.A, ld = E.ld, ldo = E.ldo;
+  const int r0 = blockIdx.x * R;
+  const int nvalid = min(R, n - r0);
+  const AS_G float* obs = GPC(float, obs_);
+  const AS_G float* eps = GPC(float, eps_);
+  AS_G float* action = GP(float, action_);
+  AS_G float* log_pi = GP(float, log_pi_);
+  lf* Xb = lds + E.o_X;
+  lf* Yb = lds + E.o_Y;
+  lf* outB = lds + E.o_out;
+  lf* outP = lds + E.o_outp;
+  const NetDev& pi = E.net[NET_PI];
+  const int Kp0 = pi.l[0].Kp;
+  for (int i = tid; i < R * Kp0; i += SAC_THREADS) {
+    const int r = i / Kp0, k = i % Kp0;
+    Xb[r * ld + k] = (k < O && r < nvalid) ? obs[(size_t)(r0 + r) * O + k] : 0.f;
+  }
+  __syncthreads();
+  mlp_forward<T, R>(pi, Xb, Yb, ld, outP, outB, ldo, E.o_P1, E.ldp1, lds, false, false, 0, 0, 0);
+  if (tid < nvalid) {
+    const int b = r0 + tid;
+    const lf* o = outB + tid * ldo;
+    const float lo = E.ls_min, hi = E.ls_max, scale = E.scale;
+    float lp_sum = 0.f, corr_sum = 0.f;
+    for (int j = 0; j < A; ++j) {
+      if (!eps) {
+        action[(size_t)b * A + j] = tanhf(o[j]) * scale;
+        continue;
+      }
+      const float mu = o[j], lsr = o[A + j], e = eps[(size_t)b * A + j];
+      const float ls = lsr < lo ? lo : (lsr > hi ? hi : lsr);
+      const float sd = expf(ls);
+      const float z = mu + e * sd;
+      action[(size_t)b * A + j] = tanhf(z) * scale;
+      const float diff = z - mu;
+      const float var = sd * sd;
+      lp_sum += -(diff * diff) / (2.f * var) - logf(sd) - HALF_LOG_2PI;
+      corr_sum += 2.f * ((LOG2F - z) - softplus20(-2.f * z));
+    }
+    if (eps && log_pi) log_pi[b] = lp_sum - corr_sum;
+  }
+}

@@ -1,0 +1,141 @@
+"""ctypes binding of ``libsac_engine.so`` (C ABI: include/sac_engine.h).
+
+PyTorch supplies device memory and streams; every compute call goes through the
+HIP library.  There is deliberately no fallback: if the library or a GPU is
+missing, ``load_library()`` / ``Engine(...)`` raise ``EngineUnavailable``.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Optional, Sequence
+
+import torch
+
+MAX_LAYERS = 8
+PREC_FP32, PREC_BF16 = 0, 1
+
+_LIB_NAME = "libsac_engine.so"
+_PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+class EngineUnavailable(RuntimeError):
+    """The HIP engine cannot run here (library not built or no MI355X device)."""
+
+
+class EngineError(RuntimeError):
+    pass
+
+
+c_int32_p = ctypes.POINTER(ctypes.c_int32)
+
+
+class EngineConfig(ctypes.Structure):
+    _fields_ = [
+        ("obs_dim", ctypes.c_int32), ("act_dim", ctypes.c_int32), ("batch", ctypes.c_int32),
+        ("q_layers", ctypes.c_int32), ("q_dims", ctypes.c_int32 * (MAX_LAYERS + 1)),
+        ("q_hidden_act", ctypes.c_int32), ("q_out_act", ctypes.c_int32),
+        ("pi_layers", ctypes.c_int32), ("pi_dims", ctypes.c_int32 * (MAX_LAYERS + 1)),
+        ("pi_hidden_act", ctypes.c_int32), ("pi_out_act", ctypes.c_int32),
+        ("gamma", ctypes.c_float), ("tau", ctypes.c_float),
+        ("log_std_min", ctypes.c_float), ("log_std_max", ctypes.c_float), ("action_scale", ctypes.c_float),
+        ("actor_lr", ctypes.c_float), ("critic_lr", ctypes.c_float), ("alpha_lr", ctypes.c_double),
+        ("beta1", ctypes.c_float), ("beta2", ctypes.c_float), ("adam_eps", ctypes.c_float),
+        ("auto_entropy", ctypes.c_int32), ("target_entropy", ctypes.c_float),
+        ("precision", ctypes.c_int32), ("seed", ctypes.c_uint64),
+    ]
+
+
+class EngineBuffers(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_void_p) for n in
+                ("pi", "q1", "q2", "q1t", "q2t", "pi_m", "pi_v", "q1_m", "q1_v", "q2_m", "q2_v",
+                 "alpha_state", "opt_steps", "rng_step", "stats", "workspace")] + [
+        ("workspace_bytes", ctypes.c_size_t)]
+
+
+class ReplayDesc(ctypes.Structure):
+    _fields_ = [("obs", ctypes.c_void_p), ("act", ctypes.c_void_p), ("rew", ctypes.c_void_p),
+                ("next_obs", ctypes.c_void_p), ("done", ctypes.c_void_p), ("capacity", ctypes.c_int64),
+                ("obs_dim", ctypes.c_int32), ("act_dim", ctypes.c_int32), ("state", ctypes.c_void_p)]
+
+
+# name -> (restype, argtypes): every symbol include/sac_engine.h declares
+SIGNATURES = {
+    "sac_last_error": (ctypes.c_char_p, []),
+    "sac_version": (ctypes.c_char_p, []),
+    "sac_engine_workspace_bytes": (ctypes.c_size_t, [ctypes.POINTER(EngineConfig)]),
+    "sac_engine_create": (ctypes.c_int, [ctypes.POINTER(EngineConfig), ctypes.POINTER(EngineBuffers),
+                                         ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p)]),
+    "sac_engine_destroy": (None, [ctypes.c_void_p]),
+    "sac_engine_sync_params": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
+    "sac_engine_train": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ReplayDesc), ctypes.c_int32,
+                                        ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    "sac_engine_train_graph": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ReplayDesc), ctypes.c_int32,
+                                              ctypes.c_int32, ctypes.c_void_p]),
+    "sac_policy_act": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p,
+                                      ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    "sac_replay_push": (ctypes.c_int, [ctypes.POINTER(ReplayDesc), ctypes.c_void_p, ctypes.c_int64,
+                                       ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p]),
+    "sac_replay_gather": (ctypes.c_int, [ctypes.POINTER(ReplayDesc), ctypes.c_void_p, ctypes.c_int32]
+                          + [ctypes.c_void_p] * 6),
+    "sac_replay_sample_indices": (ctypes.c_int, [ctypes.POINTER(ReplayDesc), ctypes.c_int32, ctypes.c_uint64,
+                                                 ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p]),
+    "sac_engine_time_phases": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ReplayDesc), ctypes.c_int32,
+                                              ctypes.POINTER(ctypes.c_float), ctypes.c_void_p]),
+    "sac_phase_kernel_name": (ctypes.c_char_p, [ctypes.c_int32]),
+}
+
+_lib: Optional[ctypes.CDLL] = None
+
+
+def library_path() -> str:
+    return os.environ.get("SAC_ENGINE_LIB", os.path.join(_PKG_ROOT, _LIB_NAME))
+
+
+def load_library() -> ctypes.CDLL:
+    """Load (once) and type every exported symbol.  Raises EngineUnavailable."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    path = library_path()
+    if not os.path.exists(path):
+        raise EngineUnavailable(
+            f"{path} not found: build it with `make -C soft-actor-critic_amd/csrc` "
+            "(or __graft_entry__.build()); there is no CPU fallback")
+    lib = ctypes.CDLL(path)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def check(rc: int) -> None:
+    if rc != 0:
+        msg = load_library().sac_last_error().decode()
+        if rc == -3:
+            raise ValueError(msg)
+        raise EngineError(f"libsac_engine error {rc}: {msg}")
+
+
+def require_gpu(device: torch.device) -> None:
+    if device.type != "cuda":
+        raise EngineUnavailable(
+            f"the SAC engine runs on MI355X (HIP) devices only; got device '{device}'. "
+            "Set train.device to 'cuda'.")
+    if not torch.cuda.is_available():
+        raise EngineUnavailable("no HIP device visible (torch.cuda.is_available() is False)")
+
+
+def stream_handle(device: torch.device) -> ctypes.c_void_p:
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def ptr(t: Optional[torch.Tensor]) -> ctypes.c_void_p:
+    return ctypes.c_void_p(0 if t is None else t.data_ptr())
+
+
+def net_dims(layers: Sequence[torch.nn.Linear]):
+    dims = [layers[0].in_features] + [lin.out_features for lin in layers]
+    return len(layers), dims

@@ -1,0 +1,459 @@
+"""Soft Actor-Critic agent (API of reference ``sac/agent.py``) on the MI355X engine.
+
+``SAC(env, config)`` accepts the reference's YAML config unchanged and exposes
+the same attributes and methods.  What changes is underneath:
+
+* ``training_step`` (agent.py:302-327) is ONE call into ``libsac_engine.so``:
+  four HIP kernels (sample+target+critic-backward, critic update, actor, actor
+  update) on the current stream, no host synchronisation and no ``.item()``;
+* the replay buffer lives in HBM (``sac.replay_buffer``);
+* ``select_action`` (agent.py:149-156) runs the policy head in a HIP kernel.
+
+Extra (optional) config keys, all under ``train``:
+    precision: 'bf16' (default; bf16 MFMA products, fp32 accumulate/master) | 'fp32'
+    rng:       'device' (default; Philox/Feistel on the GPU, graph-replayable) |
+               'reference' (Python ``random.sample`` indices + torch eps draws,
+               the reference's RNG consumption)
+    graph_chunk: steps per captured hipGraph for ``train_steps`` (default 32)
+
+Deliberate difference (documented in DESIGN.md): after ``load_agent`` the alpha
+optimizer keeps tuning ``log_alpha``; the reference rebinds ``log_alpha`` but not
+its optimizer (agent.py:550), which freezes alpha after a load.
+"""
+from __future__ import annotations
+
+import os
+import pprint
+import random
+from collections import deque
+from copy import deepcopy
+from typing import Any, Dict, Optional
+
+import numpy as np
+import torch
+import torch.optim as optim
+
+from . import _engine as E
+from .engine import SacEngine
+from .models import PolicyNetwork, QNetwork
+from .replay_buffer import ReplayBuffer, Transition
+
+try:  # progress bars are optional
+    from tqdm import tqdm as _tqdm
+except Exception:  # pragma: no cover
+    def _tqdm(it, disable=False):
+        return it
+
+
+def _make_logger(cfg, env_name, agent_name):
+    from .utils.experiment_logger import ExperimentLogger
+
+    return ExperimentLogger(cfg, env_name=env_name, agent_name=agent_name)
+
+
+class SAC:
+    def __init__(self, env, config: dict):
+        self.env = env
+        self.config = config
+        self.device = torch.device(config["train"]["device"])
+        self.replay_buffer = ReplayBuffer(config["buffer"]["capacity"], device=self.device)
+        self.obs_size = env.observation_space.shape[0]
+        self.action_size = env.action_space.shape[0]
+        # same construction order (and therefore torch RNG use) as the reference
+        self._init_policy_network()
+        self._init_q_networks()
+        self._init_optimizers()
+        self._set_seed(config["train"]["seed"])
+
+        self.target_entropy = -float(self.action_size)
+        sac_cfg = config["sac"]
+        self._auto = bool(sac_cfg["auto_entropy_tuning"])
+        tr = config["train"]
+        self.precision = tr.get("precision", "bf16")
+        self.rng_mode = tr.get("rng", "device")
+        self.graph_chunk = int(tr.get("graph_chunk", 32))
+        self.engine: Optional[SacEngine] = None
+        self._fixed_alpha = torch.tensor(sac_cfg["alpha"]).to(self.device)
+        self.alpha_optimizer = None
+        if self.device.type == "cuda":
+            self._build_engine()
+
+        self.env_name = config["logger"]["env_name"] or self._infer_env_name(env)
+        self.agent_name = config["logger"]["agent_name"] or self.__class__.__name__
+        self.logger = (_make_logger(config["logger"], self.env_name, self.agent_name)
+                       if config["logger"]["enabled"] else None)
+
+    # ------------------------------------------------------------------ construction
+    def _init_q_networks(self) -> None:
+        qc, seed = self.config["q_net"], self.config["train"]["seed"]
+        kw = dict(obs_size=self.obs_size, action_size=self.action_size, hidden_sizes=qc["hidden_sizes"],
+                  hidden_activations=qc["hidden_layers_act"], output_activation=qc["output_activation"])
+        self.q_net1 = QNetwork(seed=seed, **kw).to(self.device)
+        self.q_net2 = QNetwork(seed=seed + 1, **kw).to(self.device)
+        self.q_net1_target = deepcopy(self.q_net1).to(self.device)
+        self.q_net2_target = deepcopy(self.q_net2).to(self.device)
+
+    def _init_policy_network(self) -> None:
+        pc = self.config["policy_net"]
+        self.policy_net = PolicyNetwork(
+            obs_size=self.obs_size, action_size=self.action_size, hidden_sizes=pc["hidden_sizes"],
+            log_std_min=pc["log_std_min"], log_std_max=pc["log_std_max"], action_scale=pc["action_scale"],
+            hidden_activations=pc["hidden_layers_act"], output_activation=pc["output_activation"],
+            seed=self.config["train"]["seed"]).to(self.device)
+
+    def _init_optimizers(self) -> None:
+        s = self.config["sac"]
+        self.policy_optimizer = optim.Adam(self.policy_net.parameters(), lr=s["actor_lr"])
+        self.q1_optimizer = optim.Adam(self.q_net1.parameters(), lr=s["critic_lr"])
+        self.q2_optimizer = optim.Adam(self.q_net2.parameters(), lr=s["critic_lr"])
+
+    def _set_seed(self, seed: int) -> None:
+        np.random.seed(seed)
+        torch.manual_seed(seed)
+        random.seed(seed)
+        self.env.reset(seed=seed)
+        self.env.action_space.seed(seed)
+        self.env.observation_space.seed(seed)
+
+    def _build_engine(self) -> None:
+        s, tr = self.config["sac"], self.config["train"]
+        self.engine = SacEngine(
+            self.policy_net, self.q_net1, self.q_net2, self.q_net1_target, self.q_net2_target,
+            batch_size=tr["batch_size"], gamma=s["gamma"], tau=s["tau"], actor_lr=s["actor_lr"],
+            critic_lr=s["critic_lr"], alpha_lr=s["alpha_lr"], alpha=s["alpha"],
+            auto_entropy_tuning=self._auto, device=self.device, precision=self.precision,
+            seed=int(tr.get("engine_seed", tr["seed"])))
+        eng = self.engine
+        # torch.optim.Adam objects whose state IS the engine's device state
+        for opt, key in ((self.policy_optimizer, "pi"), (self.q1_optimizer, "q1"), (self.q2_optimizer, "q2")):
+            ms, vs = eng.adam_views(key)
+            for p, m, v in zip(eng.param_views(key), ms, vs):
+                opt.state[p] = {"step": torch.tensor(0.0), "exp_avg": m, "exp_avg_sq": v}
+        if self._auto:
+            self.log_alpha = eng.alpha_state[0]
+            self.alpha_optimizer = optim.Adam([self.log_alpha], lr=s["alpha_lr"])
+            self.alpha_optimizer.state[self.log_alpha] = {
+                "step": torch.tensor(0.0), "exp_avg": eng.alpha_state[2], "exp_avg_sq": eng.alpha_state[3]}
+
+    def _engine(self) -> SacEngine:
+        if self.engine is None:
+            E.require_gpu(self.device)
+        return self.engine
+
+    @property
+    def alpha(self) -> torch.Tensor:
+        """Current temperature: float64 0-dim when auto-tuned (agent.py:50), fp32 otherwise."""
+        if self._auto and self.engine is not None:
+            return self.engine.alpha_state[1]
+        return self._fixed_alpha
+
+    # ------------------------------------------------------------------ data
+    def store_transition(self, state: Any, action: Any, reward: float, next_state: Any, done: bool) -> None:
+        self.replay_buffer.push(state, action, reward, next_state, done)
+
+    def warmup_replay_buffer(self, env: Any, steps: int) -> None:
+        state, _ = env.reset()
+        for _ in range(steps):
+            action = env.action_space.sample()
+            next_state, reward, terminated, truncated, _ = env.step(action)
+            done = terminated or truncated
+            self.store_transition(state, action, reward, next_state, done)
+            state = next_state
+            if done:
+                state, _ = env.reset()
+
+    def select_action(self, state: Any, deterministic: bool = False) -> Any:
+        """Policy action for one observation (HIP policy kernel; agent.py:149-156)."""
+        eng = self._engine()
+        obs = torch.as_tensor(np.asarray(state, dtype=np.float32)).reshape(1, -1).to(self.device)
+        if deterministic:
+            act = eng.policy_act(obs)
+        else:
+            eps = torch.distributions.utils._standard_normal((1, self.action_size), torch.float32, self.device)
+            act = eng.policy_act(obs, eps)
+        return act.cpu().numpy()[0]
+
+    def can_update(self) -> bool:
+        if self.config["train"]["warming_steps"] > self.config["buffer"]["capacity"]:
+            print("Warning: warming_steps is greater than replay buffer capacity.")
+        return len(self.replay_buffer) >= self.config["train"]["warming_steps"]
+
+    def sample_batch(self) -> Transition:
+        """Minibatch as device tensors (agent.py:166-193), reference RNG order."""
+        return self.replay_buffer.sample_tensors(self.config["train"]["batch_size"])
+
+    # ------------------------------------------------------------------ the hot path
+    def _reference_rng_inputs(self):
+        B, A = self.config["train"]["batch_size"], self.action_size
+        idx = torch.tensor(self.replay_buffer.sample_indices(B), dtype=torch.int32)
+        sn = torch.distributions.utils._standard_normal
+        eps_t = sn((B, A), torch.float32, self.device)  # target rsample (agent.py:204)
+        eps_a = sn((B, A), torch.float32, self.device)  # actor rsample (agent.py:241)
+        return idx.reshape(1, B), torch.stack([eps_t, eps_a]).reshape(1, 2, B, A)
+
+    def training_step(self):
+        """One SAC gradient step on the engine (agent.py:302-327)."""
+        eng = self._engine()
+        if self.rng_mode == "reference":
+            idx, eps = self._reference_rng_inputs()
+            eng.train(self.replay_buffer, 1, indices=idx, eps=eps)
+        else:
+            self.replay_buffer._check(self.config["train"]["batch_size"])
+            eng.train(self.replay_buffer, 1)
+
+    def train_steps(self, n: int) -> None:
+        """n consecutive gradient steps (device RNG) replayed from a hipGraph."""
+        eng = self._engine()
+        if self.rng_mode == "reference":
+            for _ in range(n):
+                self.training_step()
+        else:
+            self.replay_buffer._check(self.config["train"]["batch_size"])
+            eng.train_graph(self.replay_buffer, n, self.graph_chunk)
+
+    def last_losses(self) -> Dict[str, float]:
+        """Losses of the last step (reads device memory: synchronises)."""
+        l = self._engine().losses()
+        return {"q1_loss": l[0], "q2_loss": l[1], "policy_loss": l[2], "alpha_loss": l[3],
+                "alpha": float(self.alpha.item())}
+
+    # Reference sub-steps.  The engine fuses them; calling one alone is not a
+    # supported mode of the fused step (see DESIGN.md "API surface").
+    def compute_target_q_values(self, rewards: Any, dones: Any, next_states: Any) -> Any:
+        """y = r + gamma (1-d)(min Qt(s',a') - alpha logpi(a'|s')), eager, no state change."""
+        with torch.no_grad():
+            next_actions, next_log_pi = self.policy_net.sample_action(next_states)
+            q1 = self.q_net1_target(next_states, next_actions)
+            q2 = self.q_net2_target(next_states, next_actions)
+            return rewards + self.config["sac"]["gamma"] * (1 - dones) * (
+                torch.min(q1, q2) - self.alpha.detach() * next_log_pi)
+
+    def _fused_only(self, name):
+        raise NotImplementedError(
+            f"SAC.{name} is fused into SAC.training_step on the MI355X engine; call training_step()")
+
+    def update_q_networks(self, *a, **k):
+        self._fused_only("update_q_networks")
+
+    def update_policy_network(self, *a, **k):
+        self._fused_only("update_policy_network")
+
+    def update_entropy_temperature(self, *a, **k):
+        self._fused_only("update_entropy_temperature")
+
+    def soft_update_target_networks(self):
+        self._fused_only("soft_update_target_networks")
+
+    # ------------------------------------------------------------------ loops
+    def run_training_loop(self, num_episodes: int, logger=None, tqdm_disable: bool = False,
+                          print_rewards: bool = False) -> Dict[str, float]:
+        active_logger = logger or self.logger
+        total_episodes = total_steps = 0
+        returns_window = deque(maxlen=100)
+        best_avg_return = -float("inf")
+        avg_return = float("nan")
+        tr = self.config["train"]
+        update_every = tr.get("update_frequency", 1)
+        n_grad = tr.get("gradient_steps_per_update", 1)
+        for episode in _tqdm(range(num_episodes), disable=tqdm_disable):
+            state, _ = self.env.reset()
+            done = False
+            episode_return = 0.0
+            total_episodes += 1
+            episode_steps = 0
+            while not done:
+                action = self.select_action(state)
+                next_state, reward, terminated, truncated, _ = self.env.step(action)
+                done = terminated or truncated
+                self.store_transition(state, action, reward, next_state, done)
+                state = next_state
+                episode_return += reward
+                episode_steps += 1
+                total_steps += 1
+                if self.can_update() and total_steps % update_every == 0:
+                    for _ in range(n_grad):
+                        self.training_step()
+                if active_logger is not None and self.config["logger"]["log_q_values"]:
+                    self._log_q_values(
+                        states=torch.FloatTensor(np.asarray(state)).unsqueeze(0).to(self.device),
+                        actions=torch.FloatTensor(np.asarray(action)).unsqueeze(0).to(self.device),
+                        logger=active_logger, step=total_steps)
+            returns_window.append(episode_return)
+            avg_return = float(np.mean(returns_window))
+            best_avg_return = max(best_avg_return, avg_return)
+            if active_logger is not None and self.config["logger"]["log_episode_stats"]:
+                active_logger.log_episode_metrics(episode_idx=episode, reward=episode_return, length=episode_steps)
+            if print_rewards:
+                print(f"Episode {episode}, Return: {episode_return:.2f}, "
+                      f"Average Return(last 100 episodes): {avg_return:.2f}")
+        metrics = {"total_episodes": total_episodes, "best_avg_return": best_avg_return,
+                   "final_avg_return": avg_return}
+        if active_logger is not None:
+            active_logger.log_hparams(self.config, metrics)
+        if self.config["logger"]["save_model"]["enabled"]:
+            save_path = self.config["logger"]["save_model"]["path"]
+            if save_path is None:
+                save_path = active_logger.run_dir
+            else:
+                os.makedirs(save_path, exist_ok=True)
+            model_path = os.path.join(save_path, "sac_agent.pth")
+            self.save_agent(model_path)
+            print(f"Agent saved to {model_path}")
+        if active_logger is not None and self.config["logger"]["log_episode_stats"]:
+            from .utils.logger_utils import save_lengths, save_rewards
+
+            save_rewards(active_logger.run_dir, active_logger.episode_rewards)
+            save_lengths(active_logger.run_dir, active_logger.episode_lengths)
+        return metrics
+
+    def eval_agent(self, num_episodes: int, render_mode: Optional[str] = None, tqdm_disable: bool = False,
+                   print_returns: bool = False, writer=None) -> float:
+        eval_env = self._get_render_environment(render_mode)
+        total_return = 0.0
+        for episode in _tqdm(range(num_episodes), disable=tqdm_disable):
+            state, _ = eval_env.reset()
+            done = False
+            episode_return = 0.0
+            length = 0
+            while not done:
+                action = self.select_action(state, deterministic=True)
+                next_state, reward, terminated, truncated, _ = eval_env.step(action)
+                done = terminated or truncated
+                state = next_state
+                episode_return += reward
+                length += 1
+            total_return += episode_return
+            if print_returns:
+                print(f"Evaluation Episode {episode}, Return: {episode_return:.2f}")
+            if writer is not None:
+                writer.add_scalar("Eval/Episode/Return", episode_return, episode)
+                writer.add_scalar("Eval/Episode/Length", length, episode)
+        avg_return = total_return / num_episodes
+        if print_returns:
+            print(f"Average Return over {num_episodes} episodes: {avg_return:.2f}")
+        if eval_env is not self.env:
+            eval_env.close()
+        return avg_return
+
+    def _get_render_environment(self, render_mode: Optional[str]):
+        if render_mode is None or getattr(self.env, "render_mode", None) == render_mode:
+            return self.env
+        spec = getattr(self.env, "spec", None)
+        if spec is not None and getattr(spec, "id", None):
+            try:
+                import gymnasium as gym
+
+                print(f"Creating new environment for evaluation with render_mode='{render_mode}'")
+                eval_env = gym.make(spec.id, render_mode=render_mode)
+                seed = self.config["train"].get("seed")
+                if seed is not None:
+                    eval_env.reset(seed=seed)
+                    eval_env.action_space.seed(seed)
+                return eval_env
+            except Exception as e:  # noqa: BLE001 - same behaviour as the reference
+                print(f"Warning: Failed to create new env for rendering: {e}. Using original env.")
+                return self.env
+        print("Warning: Cannot create new env for rendering as env.spec.id is not available. Using original env.")
+        return self.env
+
+    def _log_q_values(self, states: Any, actions: Any, logger, step: int) -> None:
+        with torch.no_grad():
+            q1 = self.q_net1(states, actions)
+            q2 = self.q_net2(states, actions)
+            logger.log_q_values(q1.mean().item(), q2.mean().item(), step)
+
+    def _infer_env_name(self, env) -> str:
+        spec = getattr(env, "spec", None)
+        if spec is not None and getattr(spec, "id", None):
+            return spec.id
+        return env.__class__.__name__
+
+    def show_config(self, indent: int = 4) -> None:
+        pprint.PrettyPrinter(indent=indent).pprint(self.config)
+
+    def print_net_architectures(self) -> None:
+        print("Policy Network Architecture:")
+        print(self.policy_net)
+        print("\nQ-Network 1 Architecture:")
+        print(self.q_net1)
+        print("\nQ-Network 2 Architecture:")
+        print(self.q_net2)
+
+    # ------------------------------------------------------------------ checkpoints
+    def _export_steps(self) -> None:
+        if self.engine is None:
+            return
+        steps = self.engine.opt_steps.cpu().tolist()
+        for opt, i in ((self.policy_optimizer, 0), (self.q1_optimizer, 1), (self.q2_optimizer, 2),
+                       (self.alpha_optimizer, 3)):
+            if opt is None:
+                continue
+            for st in opt.state.values():
+                st["step"] = torch.tensor(float(steps[i]))
+
+    def save_agent(self, filepath: str) -> None:
+        """Same checkpoint dict as the reference (agent.py:521-536)."""
+        self._export_steps()
+        ckpt = {
+            "policy_net_state_dict": self.policy_net.state_dict(),
+            "q_net1_state_dict": self.q_net1.state_dict(),
+            "q_net2_state_dict": self.q_net2.state_dict(),
+            "q_net1_target_state_dict": self.q_net1_target.state_dict(),
+            "q_net2_target_state_dict": self.q_net2_target.state_dict(),
+            "policy_optimizer_state_dict": self.policy_optimizer.state_dict(),
+            "q1_optimizer_state_dict": self.q1_optimizer.state_dict(),
+            "q2_optimizer_state_dict": self.q2_optimizer.state_dict(),
+        }
+        if self._auto:
+            ckpt["log_alpha"] = self.log_alpha.detach().clone()
+            ckpt["alpha_optimizer_state_dict"] = self.alpha_optimizer.state_dict()
+        torch.save(ckpt, filepath)
+
+    def _import_opt(self, opt, sd, key: Optional[str], step_idx: int) -> None:
+        """Load a torch Adam state_dict into the engine-owned moment buffers."""
+        eng = self.engine
+        params = list(opt.param_groups[0]["params"])
+        for g, gsd in zip(opt.param_groups, sd["param_groups"]):
+            for k, v in gsd.items():
+                if k != "params":
+                    g[k] = v
+        steps = []
+        for i, p in enumerate(params):
+            st = sd["state"].get(i)
+            cur = opt.state[p]
+            if st is None:
+                cur["exp_avg"].zero_()
+                cur["exp_avg_sq"].zero_()
+                steps.append(0.0)
+                continue
+            cur["exp_avg"].copy_(st["exp_avg"].reshape(cur["exp_avg"].shape))
+            cur["exp_avg_sq"].copy_(st["exp_avg_sq"].reshape(cur["exp_avg_sq"].shape))
+            steps.append(float(st["step"]))
+        if eng is not None and steps:
+            eng.opt_steps[step_idx] = max(steps)
+
+    def load_agent(self, filepath: str) -> None:
+        """Load a reference-format checkpoint (agent.py:538-554).
+
+        Loaded with ``weights_only=True``: checkpoints are plain tensors/dicts."""
+        ckpt = torch.load(filepath, map_location=self.device, weights_only=True)
+        self.policy_net.load_state_dict(ckpt["policy_net_state_dict"])
+        self.q_net1.load_state_dict(ckpt["q_net1_state_dict"])
+        self.q_net2.load_state_dict(ckpt["q_net2_state_dict"])
+        self.q_net1_target.load_state_dict(ckpt["q_net1_target_state_dict"])
+        self.q_net2_target.load_state_dict(ckpt["q_net2_target_state_dict"])
+        if self.engine is None:
+            self.policy_optimizer.load_state_dict(ckpt["policy_optimizer_state_dict"])
+            self.q1_optimizer.load_state_dict(ckpt["q1_optimizer_state_dict"])
+            self.q2_optimizer.load_state_dict(ckpt["q2_optimizer_state_dict"])
+            return
+        self._import_opt(self.policy_optimizer, ckpt["policy_optimizer_state_dict"], "pi", 0)
+        self._import_opt(self.q1_optimizer, ckpt["q1_optimizer_state_dict"], "q1", 1)
+        self._import_opt(self.q2_optimizer, ckpt["q2_optimizer_state_dict"], "q2", 2)
+        if self._auto and "log_alpha" in ckpt:
+            la = ckpt["log_alpha"].detach().to(torch.float64).reshape(())
+            self.engine.alpha_state[0] = la
+            self.engine.alpha_state[1] = la.exp()
+            if "alpha_optimizer_state_dict" in ckpt:
+                self._import_opt(self.alpha_optimizer, ckpt["alpha_optimizer_state_dict"], None, 3)
+        self.engine.sync_params()

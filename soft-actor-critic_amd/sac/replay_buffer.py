@@ -1,0 +1,194 @@
+"""Replay buffer resident in HBM (API of reference ``sac/replay_buffer.py``).
+
+Storage is struct-of-arrays on the device:
+``obs[cap][O] | act[cap][A] | rew[cap] | next_obs[cap][O] | done[cap]`` (fp32),
+ring-ordered with ``(size, pos)`` mirrored on the host and on the device.
+
+* ``push`` (replay_buffer.py:21-30) stages rows in pinned host memory; staged rows
+  are appended by one HIP kernel (``sac_replay_push``) before the next read, so an
+  env loop pays one small H2D copy per flush, not per field.
+* ``sample`` (replay_buffer.py:32-39) keeps the reference's RNG stream: indices
+  come from Python ``random.sample`` over positions (oldest = 0, the deque order)
+  so a seeded run selects exactly the rows the reference would; rows are gathered
+  on the device (``sac_replay_gather``) and returned as ``Transition``s.
+* ``sample_tensors`` is the batched form used by ``SAC.sample_batch``: one
+  Transition of device tensors.
+* The fused engine path samples on the device itself (Feistel permutation keyed
+  by Philox; distinct uniform rows like ``random.sample``), see DESIGN.md.
+"""
+from __future__ import annotations
+
+import random
+from collections import namedtuple
+from typing import List, Optional
+
+import numpy as np
+import torch
+
+from . import _engine as E
+
+Transition = namedtuple("Transition", ("state", "action", "reward", "next_state", "done"))
+
+
+class ReplayBuffer:
+    def __init__(self, capacity: int, device=None, obs_dim: Optional[int] = None,
+                 act_dim: Optional[int] = None, stage_rows: int = 4096):
+        """Experience replay of at most ``capacity`` transitions (FIFO eviction)."""
+        self.capacity = int(capacity)
+        if self.capacity < 1:
+            raise ValueError("capacity must be >= 1")
+        self.device = torch.device(device) if device is not None else torch.device(
+            "cuda" if torch.cuda.is_available() else "cpu")
+        self._size = 0
+        self._pos = 0
+        self._stage_rows = int(stage_rows)
+        self._staged: List[np.ndarray] = []
+        self._n_staged = 0
+        self.obs_dim = obs_dim
+        self.act_dim = act_dim
+        self._alloc_done = False
+        if obs_dim is not None and act_dim is not None:
+            self._alloc(obs_dim, act_dim)
+
+    # ------------------------------------------------------------------ storage
+    def _alloc(self, obs_dim: int, act_dim: int) -> None:
+        E.require_gpu(self.device)
+        self.obs_dim, self.act_dim = int(obs_dim), int(act_dim)
+        cap, dev = self.capacity, self.device
+        f32 = dict(dtype=torch.float32, device=dev)
+        self.obs = torch.zeros(cap, self.obs_dim, **f32)
+        self.act = torch.zeros(cap, self.act_dim, **f32)
+        self.rew = torch.zeros(cap, **f32)
+        self.next_obs = torch.zeros(cap, self.obs_dim, **f32)
+        self.done = torch.zeros(cap, **f32)
+        self.state = torch.zeros(2, dtype=torch.int64, device=dev)
+        self.row_width = 2 * self.obs_dim + self.act_dim + 2
+        self._desc = E.ReplayDesc(
+            self.obs.data_ptr(), self.act.data_ptr(), self.rew.data_ptr(), self.next_obs.data_ptr(),
+            self.done.data_ptr(), cap, self.obs_dim, self.act_dim, self.state.data_ptr())
+        self._alloc_done = True
+
+    @property
+    def desc(self) -> E.ReplayDesc:
+        self.flush()
+        return self._desc
+
+    def _row(self, state, action, reward, next_state, done) -> np.ndarray:
+        s = np.asarray(state, dtype=np.float32).reshape(-1)
+        a = np.asarray(action, dtype=np.float32).reshape(-1)
+        s2 = np.asarray(next_state, dtype=np.float32).reshape(-1)
+        if not self._alloc_done:
+            self._alloc(s.size, a.size)
+        row = np.empty(self.row_width, np.float32)
+        O, A = self.obs_dim, self.act_dim
+        row[:O] = s
+        row[O:O + A] = a
+        row[O + A] = np.float32(reward)
+        row[O + A + 1:2 * O + A + 1] = s2
+        row[-1] = np.float32(bool(done))
+        return row
+
+    # ------------------------------------------------------------------ reference API
+    def push(self, state, action, reward, next_state, done) -> None:
+        """Store a transition (replay_buffer.py:21-30)."""
+        self._staged.append(self._row(state, action, reward, next_state, done))
+        self._n_staged += 1
+        if self._n_staged >= self._stage_rows:
+            self.flush()
+
+    def push_batch(self, states, actions, rewards, next_states, dones) -> None:
+        """Append n transitions at once (device or host arrays; rows in order)."""
+        st = torch.as_tensor(states, dtype=torch.float32)
+        n = st.shape[0]
+        if n == 0:
+            return
+        if not self._alloc_done:
+            self._alloc(st.reshape(n, -1).shape[1], torch.as_tensor(actions).reshape(n, -1).shape[1])
+        self.flush()
+        dev = self.device
+        rows = torch.cat([
+            st.reshape(n, -1).to(dev),
+            torch.as_tensor(actions, dtype=torch.float32).reshape(n, -1).to(dev),
+            torch.as_tensor(rewards, dtype=torch.float32).reshape(n, 1).to(dev),
+            torch.as_tensor(next_states, dtype=torch.float32).reshape(n, -1).to(dev),
+            torch.as_tensor(dones).to(torch.float32).reshape(n, 1).to(dev),
+        ], dim=1).contiguous()
+        self._push_device_rows(rows)
+
+    def _push_device_rows(self, rows: torch.Tensor) -> None:
+        n = rows.shape[0]
+        lib = E.load_library()
+        E.check(lib.sac_replay_push(ctypes_ref(self._desc), E.ptr(rows), n, self._size, self._pos,
+                                    E.stream_handle(self.device)))
+        self._size = min(self.capacity, self._size + n)
+        self._pos = (self._pos + n) % self.capacity
+        self._keep = rows  # keep alive until the kernel has consumed it
+
+    def flush(self) -> None:
+        """Append staged host rows with one H2D copy + one push kernel."""
+        if not self._n_staged:
+            return
+        host = torch.from_numpy(np.stack(self._staged)).pin_memory() if torch.cuda.is_available() \
+            else torch.from_numpy(np.stack(self._staged))
+        rows = host.to(self.device, non_blocking=True)
+        self._staged.clear()
+        self._n_staged = 0
+        self._push_device_rows(rows)
+        self._keep_host = host
+
+    def __len__(self) -> int:
+        return min(self.capacity, self._size + self._n_staged)
+
+    def _check(self, batch_size: int) -> None:
+        if len(self) < batch_size:
+            raise ValueError(
+                f"Not enough samples in the replay buffer to sample {batch_size} transitions. "
+                f"Current size: {len(self)}")
+
+    def sample_indices(self, batch_size: int) -> List[int]:
+        """Logical positions (0 = oldest), drawn exactly like ``random.sample``
+        over the reference deque (same consumption of Python's ``random``)."""
+        self._check(batch_size)
+        return random.sample(range(len(self)), batch_size)
+
+    def gather(self, logical_idx) -> Transition:
+        """Device gather of the given logical positions -> Transition of tensors."""
+        self.flush()
+        idx = torch.as_tensor(logical_idx, dtype=torch.int32)
+        B = idx.numel()
+        idx = idx.to(self.device, non_blocking=True)
+        f32 = dict(dtype=torch.float32, device=self.device)
+        s = torch.empty(B, self.obs_dim, **f32)
+        a = torch.empty(B, self.act_dim, **f32)
+        r = torch.empty(B, **f32)
+        s2 = torch.empty(B, self.obs_dim, **f32)
+        d = torch.empty(B, **f32)
+        lib = E.load_library()
+        E.check(lib.sac_replay_gather(ctypes_ref(self._desc), E.ptr(idx), B, E.ptr(s), E.ptr(a), E.ptr(r),
+                                      E.ptr(s2), E.ptr(d), E.stream_handle(self.device)))
+        return Transition(s, a, r, s2, d)
+
+    def sample_tensors(self, batch_size: int) -> Transition:
+        return self.gather(self.sample_indices(batch_size))
+
+    def sample(self, batch_size: int) -> List[Transition]:
+        """List of ``batch_size`` distinct transitions (replay_buffer.py:32-39).
+
+        Each field is a host numpy row (float32); ``done`` is a bool, ``reward`` a
+        Python float, as pushed."""
+        t = self.sample_tensors(batch_size)
+        s, a, r, s2, d = (x.cpu().numpy() for x in t)
+        return [Transition(s[i], a[i], float(r[i]), s2[i], bool(d[i] != 0)) for i in range(batch_size)]
+
+    def clear(self) -> None:
+        self._size = self._pos = 0
+        self._staged.clear()
+        self._n_staged = 0
+        if self._alloc_done:
+            self.state.zero_()
+
+
+def ctypes_ref(desc):
+    import ctypes
+
+    return ctypes.byref(desc)

@@ -1,0 +1,64 @@
+"""Where does a phase kernel spend its time?  Runs the C2 engine from the
+-DSAC_STAMPS build (make -C soft-actor-critic_amd/csrc stamps) and prints the
+s_memtime deltas between the STAMP(i) points, median over row-tile blocks."""
+import ctypes
+import os
+import sys
+
+R = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+os.environ.setdefault("SAC_ENGINE_LIB", os.path.join(R, "soft-actor-critic_amd", "libsac_engine_stamps.so"))
+sys.path[:0] = [R, os.path.join(R, "soft-actor-critic_amd")]
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import bench  # noqa: E402
+from sac import _engine as E  # noqa: E402
+
+cfg = sys.argv[1] if len(sys.argv) > 1 else "c2"
+prec = sys.argv[2] if len(sys.argv) > 2 else "bf16"
+dev = torch.device("cuda", 0)
+bench.CONFIGS[cfg]["capacity"] = min(bench.CONFIGS[cfg]["capacity"], 100_000)
+eng, rb, c = bench.build_engine(cfg, prec, 0, dev)
+lib = E.load_library()
+lib.sac_engine_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+assert lib.sac_engine_debug_stamped() == 1, "not the stamps build"
+nblk = (c["batch"] + 15) // 16
+buf = torch.zeros(nblk * 64, dtype=torch.int64, device=dev)
+E.check(lib.sac_engine_debug_stamps(eng.handle, E.ptr(buf), eng._stream()))
+eng.train(rb, 20)
+torch.cuda.synchronize()
+rows = []
+for it in range(10):
+    buf.zero_()
+    eng.train(rb, 1)
+    torch.cuda.synchronize()
+    rows.append(buf.view(nblk, 64).cpu().numpy())
+st = np.median(np.stack(rows), axis=0)  # [blk][64]
+names = {0: "A start", 1: "gather+eps", 2: "pi L0", 3: "pi L1", 4: "pi L2", 5: "pi L3", 6: "head",
+         7: "Qt1", 8: "Qt2", 10: "Q1 fwd", 11: "Q1 bwd", 12: "Q2 fwd", 13: "Q2 bwd",
+         32: "C start", 36: "Q1 fwd", 37: "Q2 fwd", 38: "Q1 bwd->da", 39: "Q2 bwd->da", 35: "pi bwd"}
+for base, last in ((0, 13), (32, 39)):
+    idx = [i for i in range(base, 64) if i in names and st[:, i].min() > 0]
+    idx.sort(key=lambda i: np.median(st[:, i]))
+    prev = None
+    print(f"--- phase {'A' if base == 0 else 'C'} (cycles, median over blocks)")
+    for i in idx:
+        t = np.median(st[:, i] - st[:, idx[0]])
+        if prev is not None:
+            print(f"  {names[i]:12s} +{t - prev:9.0f}   (cum {t:9.0f})")
+        prev = t
+
+# ---- sub-layer stamps of layer_fwd (block 0, wave 0) for one step
+lib.sac_debug_layer_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
+E.check(lib.sac_debug_layer_stamps(None, 1))
+eng.train(rb, 1)
+torch.cuda.synchronize()
+arr = (ctypes.c_longlong * (64 * 6))()
+E.check(lib.sac_debug_layer_stamps(arr, 0))
+a = np.array(arr, dtype=np.int64).reshape(64, 6)
+print("--- layer_fwd calls of one step (block 0 wave 0): issue->first-mfma->mfma-done->epi-done->end, cycles")
+for i in range(64):
+    if a[i, 0] == 0:
+        break
+    d = np.diff(a[i])
+    print(f"  call {i:2d}: issue {d[0]:6d}  wait-data {d[1]:6d}  mfma {d[2]:6d}  epi {d[3]:6d}  rest {d[4]:6d}  total {a[i,5]-a[i,0]:7d}")
