@@ -71,8 +71,7 @@ typedef struct sac_engine_config {
   int32_t pi_hidden_act, pi_out_act;
   float gamma, tau;
   float log_std_min, log_std_max, action_scale;
-  float actor_lr, critic_lr;
-  double alpha_lr;
+  double actor_lr, critic_lr, alpha_lr;      /* Python floats in the reference: kept in double */
   float beta1, beta2, adam_eps;             /* torch.optim.Adam defaults 0.9, 0.999, 1e-8 */
   int32_t auto_entropy;                     /* sac.auto_entropy_tuning */
   float target_entropy;                     /* -act_dim (agent.py:43) */

@@ -188,7 +188,7 @@ static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
   const int B = c->batch, Bp = rup(B, 32), nrt = (B + SAC_ROWS - 1) / SAC_ROWS, Br = nrt * SAC_ROWS;
   const int O = c->obs_dim, A = c->act_dim;
   Layout lay;
-  const size_t o_E = lay.take(sizeof(EngineDev));
+  const size_t o_E = lay.take(3072);  // EngineDev, padded for prefetch_engine()
   EngineDev h;
   memset(&h, 0, sizeof(h));
   auto P = [&](size_t o) -> void* { return base ? (void*)(base + o) : nullptr; };
@@ -238,6 +238,7 @@ static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
   h.lp_st = (float*)P(lay.take((size_t)Br * 4));
   h.head_st = (float*)P(lay.take((size_t)Br * 4 * A * 4));
   h.lossp = (float*)P(lay.take((size_t)nrt * 4 * 4));
+  h.adam_sc = (float*)P(lay.take(6 * 4));
   int nB = 0, nD = 0;
   for (int ni = NET_PI; ni <= NET_Q2; ++ni)
     for (int l = 0; l < h.net[ni].L; ++l)
@@ -390,16 +391,16 @@ static void launch_phase(sac_engine* e, int phase, const sac_replay* rb, const i
                          hipStream_t s) {
   switch (phase) {
     case 0:
-      sac_target_critic<T><<<e->nrt, SAC_THREADS, e->lds_bytes, s>>>(e->h, *rb, idx, eps);
+      sac_target_critic<T><<<e->nrt, SAC_THREADS, e->lds_bytes, s>>>(e->d, *rb, idx, eps);
       break;
     case 1:
-      sac_critic_update<T><<<e->nB, 256, 0, s>>>(e->h, e->tilesB);
+      sac_critic_update<T><<<e->nB, 256, 0, s>>>(e->d, e->tilesB);
       break;
     case 2:
-      sac_actor<T><<<e->nrt, SAC_THREADS, e->lds_bytes, s>>>(e->h);
+      sac_actor<T><<<e->nrt, SAC_THREADS, e->lds_bytes, s>>>(e->d);
       break;
     case 3:
-      sac_actor_update<T><<<e->nD + 1, 256, 0, s>>>(e->h, e->tilesD, e->nD);
+      sac_actor_update<T><<<e->nD + 1, 256, 0, s>>>(e->d, e->tilesD, e->nD);
       break;
   }
 }
@@ -561,9 +562,9 @@ int sac_policy_act(sac_engine* e, const float* obs, int32_t n, const float* eps,
   hipStream_t s = (hipStream_t)stream;
   const int blocks = (n + SAC_ROWS - 1) / SAC_ROWS;
   if (e->cfg.precision == SAC_PREC_BF16)
-    sac_policy_act_kernel<bf16><<<blocks, SAC_THREADS, e->lds_bytes, s>>>(e->h, obs, n, eps, action, log_pi);
+    sac_policy_act_kernel<bf16><<<blocks, SAC_THREADS, e->lds_bytes, s>>>(e->d, obs, n, eps, action, log_pi);
   else
-    sac_policy_act_kernel<float><<<blocks, SAC_THREADS, e->lds_bytes, s>>>(e->h, obs, n, eps, action, log_pi);
+    sac_policy_act_kernel<float><<<blocks, SAC_THREADS, e->lds_bytes, s>>>(e->d, obs, n, eps, action, log_pi);
   HIPCHK(hipGetLastError());
   return SAC_OK;
 }
@@ -605,7 +606,7 @@ int sac_replay_sample_indices(const sac_replay* rb, int32_t batch, uint64_t seed
 int sac_engine_debug_stamps(sac_engine* e, long long* dev_buf, void* stream) {
   if (!e) return fail(SAC_E_INVALID, "null engine");
   e->h.stamps = dev_buf;
-  (void)stream;
+  HIPCHK(hipMemcpyAsync(e->d, &e->h, sizeof(EngineDev), hipMemcpyHostToDevice, (hipStream_t)stream));
   if (e->gexec) {  // graphs captured the old kernel arguments
     (void)hipGraphExecDestroy(e->gexec);
     (void)hipGraphDestroy(e->graph);

@@ -30,8 +30,8 @@ enum { NET_PI = 0, NET_Q1 = 1, NET_Q2 = 2, NET_Q1T = 3, NET_Q2T = 4 };
 struct EngineDev {
   int B, Bp, Br, O, A, nrt, ld, ldo;
   int auto_entropy;
-  float gamma, tau, ls_min, ls_max, scale, actor_lr, critic_lr, beta1, beta2, adam_eps, target_entropy;
-  double alpha_lr;
+  float gamma, tau, ls_min, ls_max, scale, beta1, beta2, adam_eps, target_entropy;
+  double actor_lr, critic_lr, alpha_lr;
   uint64_t seed;
   NetDev net[5];
   float* s_st;     // [Br][O]   states of the batch (phase A -> C)
@@ -41,6 +41,7 @@ struct EngineDev {
   float* lossp;    // [nrt][4]
   double* alpha_state;
   double* opt_steps;
+  float* adam_sc;     // [3][2]: -lr/bias_correction1, sqrt(bias_correction2) of this step (pi, q1, q2)
   uint64_t* rng_step;
   float* stats;
   long long* stamps;  // optional in-kernel timestamps (SAC_STAMPS builds)
@@ -95,27 +96,89 @@ __device__ int g_lcall;
   } while (0)
 #endif
 
+// ============================================================================ kernarg prefetch
+// The ~2.8 KB EngineDev kernel argument is read field by field all through a
+// phase kernel; each first touch of a 64-B line is a scalar-cache miss (~1-2K
+// cycles) on the critical path.  Touch every line once at entry with
+// back-to-back s_loads (one latency for the whole struct).
+// All loads and their wait sit in ONE asm statement writing a declared-clobbered
+// SGPR: an asm load's destination is "written" when its statement ends, so a
+// per-load statement would let the compiler reuse the register while the load
+// is still in flight (it corrupted addresses: illegal-address fault).
+__device__ __forceinline__ void prefetch_engine(const void* p) {
+  static_assert(sizeof(EngineDev) <= 3072, "extend prefetch_engine");
+  const uint64_t base = (uint64_t)(uintptr_t)p;  // kernel-argument pointer: already uniform (SGPRs)
+  asm volatile("s_load_dword s95, %0, 0\n\t" "s_load_dword s95, %0, 64\n\t" "s_load_dword s95, %0, 128\n\t" "s_load_dword s95, %0, 192\n\t" "s_load_dword s95, %0, 256\n\t" "s_load_dword s95, %0, 320\n\t" "s_load_dword s95, %0, 384\n\t" "s_load_dword s95, %0, 448\n\t" "s_load_dword s95, %0, 512\n\t" "s_load_dword s95, %0, 576\n\t" "s_load_dword s95, %0, 640\n\t" "s_load_dword s95, %0, 704\n\t" "s_load_dword s95, %0, 768\n\t" "s_load_dword s95, %0, 832\n\t" "s_load_dword s95, %0, 896\n\t" "s_load_dword s95, %0, 960\n\t" "s_load_dword s95, %0, 1024\n\t" "s_load_dword s95, %0, 1088\n\t" "s_load_dword s95, %0, 1152\n\t" "s_load_dword s95, %0, 1216\n\t" "s_load_dword s95, %0, 1280\n\t" "s_load_dword s95, %0, 1344\n\t" "s_load_dword s95, %0, 1408\n\t" "s_load_dword s95, %0, 1472\n\t" "s_load_dword s95, %0, 1536\n\t" "s_load_dword s95, %0, 1600\n\t" "s_load_dword s95, %0, 1664\n\t" "s_load_dword s95, %0, 1728\n\t" "s_load_dword s95, %0, 1792\n\t" "s_load_dword s95, %0, 1856\n\t" "s_load_dword s95, %0, 1920\n\t" "s_load_dword s95, %0, 1984\n\t" "s_load_dword s95, %0, 2048\n\t" "s_load_dword s95, %0, 2112\n\t" "s_load_dword s95, %0, 2176\n\t" "s_load_dword s95, %0, 2240\n\t" "s_load_dword s95, %0, 2304\n\t" "s_load_dword s95, %0, 2368\n\t" "s_load_dword s95, %0, 2432\n\t" "s_load_dword s95, %0, 2496\n\t" "s_load_dword s95, %0, 2560\n\t" "s_load_dword s95, %0, 2624\n\t" "s_load_dword s95, %0, 2688\n\t" "s_load_dword s95, %0, 2752\n\t" "s_load_dword s95, %0, 2816\n\t" "s_load_dword s95, %0, 2880\n\t" "s_load_dword s95, %0, 2944\n\t" "s_load_dword s95, %0, 3008\n\t" "s_waitcnt lgkmcnt(0)" :: "s"(base) : "s95", "memory");
+}
+#define PREFETCH_ARG(ptr) prefetch_engine(ptr)
+
 // ============================================================================ MFMA layer steps
-// Two 16-column output tiles per wave: acc{0,1}[rt] += A(rows from LDS) x B(rows
-// b0 / b1 from HBM/L2).  Every B fragment of a batch is issued before the first
-// MFMA, so a wave pays one memory latency per batch (not per tile).  b1 == b0
-// when the wave has a single tile (duplicate loads hit L1; no divergent loads).
-template <typename T, int RT>
-__device__ __forceinline__ void mma_pair(const lf* __restrict__ arow, int lda, const AS_G T* b0, const AS_G T* b1,
-                                         bool has1, int nch, f32x4 (&acc0)[RT], f32x4 (&acc1)[RT]) {
-  constexpr int KC = MM<T>::KC;
-  constexpr int FS = 64 * MM<T>::KL;  // packed fragment stride (elements)
-  typedef typename MM<T>::Frag F;
-  int ch = 0;
-  for (; ch + 8 <= nch; ch += 8) {
-    F f0[8], f1[8];
+// A GEMM step streams a fragment-packed B matrix (weights W for a forward step,
+// W^T for a dX step) against activations held in LDS.  Each wave owns output
+// tile pairs (nt, nt + SAC_NW).  The weight stream is software-pipelined across
+// steps: every wave keeps the first 8-chunk batch of its first tile pair of the
+// NEXT step in registers (Pf), issued right after the current step's first MFMAs,
+// so the load latency overlaps the epilogue, the barrier and whatever non-GEMM
+// work sits between the two steps.
+struct GemmW {
+  const void* p;  // packed B matrix
+  int cols;       // reduction length (multiple of SAC_PAD)
+  int NT;         // 16-row tiles of the packed matrix = output tiles of the step
+};
+__device__ __forceinline__ GemmW gw_fwd(const LayerDev& L) { return GemmW{L.Wc, L.Kp, L.Np >> 4}; }
+__device__ __forceinline__ GemmW gw_bwd(const LayerDev& L) { return GemmW{L.WTc, L.Np, L.Kp >> 4}; }
+__device__ __forceinline__ GemmW gw_none() { return GemmW{nullptr, 0, 0}; }
+
+#ifndef SAC_PF
+#define SAC_PF 0  // cross-step register prefetch of the weight stream (see gemm_step)
+#endif
+template <typename T>
+struct Pf {
+#if SAC_PF
+  typename MM<T>::Frag f0[8], f1[8];
+#endif
+  const void* tag;  // which B matrix the registers hold (wave-uniform)
+};
+
+// Issue batch 0 (chunks 0..7, clamped) of this wave's first tile pair of step w.
+template <typename T>
+__device__ __forceinline__ void pf_issue(Pf<T>& pf, const GemmW& w) {
+  constexpr int KC = MM<T>::KC, FS = 64 * MM<T>::KL;
+  pf.tag = w.p;
+#if SAC_PF
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (!w.p || wave >= w.NT) return;
+  const int last = w.cols / KC - 1;
+  const int nt1 = wave + SAC_NW < w.NT ? wave + SAC_NW : wave;
+  const AS_G T* b0 = GPC(T, w.p) + packed_lane<T>(wave, w.cols, lane);
+  const AS_G T* b1 = GPC(T, w.p) + packed_lane<T>(nt1, w.cols, lane);
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
+  for (int u = 0; u < 8; ++u) {
+    const int cu = u < last ? u : last;
+    pf.f0[u] = MM<T>::ld(b0 + cu * FS);
+    pf.f1[u] = MM<T>::ld(b1 + cu * FS);
+  }
+#endif
+}
+
+// acc{0,1} += A x B over chunks [ch0, nch) loaded here (batches of 8 / 2 / 1:
+// every load of a batch issued before its first MFMA).
+template <typename T, int RT, int BM>
+__device__ __forceinline__ void mma_pair_from(const lf* __restrict__ arow, int lda, const AS_G T* b0, const AS_G T* b1,
+                                              bool has1, int ch0, int nch, f32x4 (&acc0)[RT], f32x4 (&acc1)[RT]) {
+  constexpr int KC = MM<T>::KC;
+  constexpr int FS = 64 * MM<T>::KL;
+  typedef typename MM<T>::Frag F;
+  int ch = ch0;
+  for (; ch + BM <= nch; ch += BM) {
+    F f0[BM], f1[BM];
+#pragma unroll
+    for (int u = 0; u < BM; ++u) {
       f0[u] = MM<T>::ld(b0 + (ch + u) * FS);
       f1[u] = MM<T>::ld(b1 + (ch + u) * FS);
     }
 #pragma unroll
-    for (int u = 0; u < 8; ++u)
+    for (int u = 0; u < BM; ++u)
 #pragma unroll
       for (int rt = 0; rt < RT; ++rt) {
         const F a = MM<T>::from_lds(arow + rt * 16 * lda + (ch + u) * KC);
@@ -150,109 +213,153 @@ __device__ __forceinline__ void mma_pair(const lf* __restrict__ arow, int lda, c
   }
 }
 
-// Y[r][n] = act(sum_k X[r][k] W[n][k] + b[n]) over n < Np (padded columns -> 0).
-// P (optional) keeps the pre-activation, Pg (optional) stashes rows >= pg_row0 to HBM.
-template <typename T, int ROWS>
-__device__ __forceinline__ void layer_fwd_(const lf* __restrict__ X, int ldx, const void* Wc_, int K, int N, int Kp,
-                                           int Np, const float* bias_, int act, lf* __restrict__ P, int ldp,
-                                           lf* __restrict__ Y, int ldy, float* Pg_, int pg_row0) {
+// One GEMM step over ROWS rows: out tile (r, col) for every col < 16*w.NT,
+// acc = sum_k A[r][k] B[col][k]; epi(h, col, acc[RT]) consumes each tile pair.
+// Batch 0 of the first pair comes from pf; the next step's batch 0 is issued
+// into pf right after those MFMAs.
+template <typename T, int ROWS, typename Epi>
+__device__ __forceinline__ void gemm_step(const lf* __restrict__ A, int lda, const GemmW& w, Pf<T>& pf,
+                                          const GemmW& next, Epi epi) {
   constexpr int RT = ROWS / 16;
   constexpr int KC = MM<T>::KC, KL = MM<T>::KL;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int c = lane & 15, g = lane >> 4;
+  const int NT = w.NT, nch = w.cols / KC;
+  if (pf.tag != w.p) pf_issue<T>(pf, w);  // chain broken by the caller: reload (uniform)
+  const AS_G T* B = GPC(T, w.p);
+  const lf* arow = A + c * lda + g * KL;
+  auto pair = [&](int nt0, bool first) {
+    const int nt1 = nt0 + SAC_NW;
+    const bool has1 = nt1 < NT;
+    const AS_G T* b0 = B + packed_lane<T>(nt0, w.cols, lane);
+    const AS_G T* b1 = B + packed_lane<T>(has1 ? nt1 : nt0, w.cols, lane);
+    f32x4 acc0[RT], acc1[RT];
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) acc0[rt] = acc1[rt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#if SAC_PF
+    int ch0 = 0;
+    if (first) {
+      ch0 = nch < 8 ? nch : 8;
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        if (u < ch0)
+#pragma unroll
+          for (int rt = 0; rt < RT; ++rt) {
+            const typename MM<T>::Frag a = MM<T>::from_lds(arow + rt * 16 * lda + u * KC);
+            MM<T>::mma(acc0[rt], a, pf.f0[u]);
+            if (has1) MM<T>::mma(acc1[rt], a, pf.f1[u]);
+          }
+        // bound how many A fragments the scheduler hoists (register pressure)
+        if (u & 1) __builtin_amdgcn_sched_barrier(0);
+      }
+      __builtin_amdgcn_sched_barrier(0);  // old fragments consumed before the registers are reloaded
+      pf_issue<T>(pf, next);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    mma_pair_from<T, RT, 4>(arow, lda, b0, b1, has1, ch0, nch, acc0, acc1);
+#else
+    (void)first;
+    mma_pair_from<T, RT, 8>(arow, lda, b0, b1, has1, 0, nch, acc0, acc1);
+#endif
+    epi(0, nt0 * 16 + c, acc0);
+    if (has1) epi(1, nt1 * 16 + c, acc1);
+  };
+  // one instance of the pair code (runtime `first`) keeps the kernel's code small
+  bool first = true;
+  for (int nt0 = wave;; nt0 += 2 * SAC_NW) {
+    if (nt0 >= NT) {
+      if (first) pf_issue<T>(pf, next);
+      break;
+    }
+    pair(nt0, first);
+    first = false;
+  }
+}
+
+// Activations other than ReLU/identity are applied in a compact second pass by
+// the lanes that wrote the tile (same (row, col) mapping as the epilogue, so no
+// barrier): one act switch per GEMM step instead of one per accumulator element.
+template <int ROWS>
+__device__ __forceinline__ void act_pass_fwd(lf* Y, int ldy, int NT, int act) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int c = lane & 15, g = lane >> 4;
+#pragma unroll 1
+  for (int nt = wave; nt < NT; nt += SAC_NW)
+#pragma unroll 1
+    for (int e = 0; e < ROWS / 4; ++e) {
+      const int r = (e >> 2) * 16 + g * 4 + (e & 3);
+      lf* y = Y + r * ldy + nt * 16 + c;
+      *y = act_fwd(act, *y);
+    }
+}
+template <int ROWS>
+__device__ __forceinline__ void act_pass_bwd(lf* G, int ldg, const lf* P, int ldp, int NT, int K, int act) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int c = lane & 15, g = lane >> 4;
+#pragma unroll 1
+  for (int nt = wave; nt < NT; nt += SAC_NW) {
+    const int k = nt * 16 + c;
+    if (k >= K) continue;
+#pragma unroll 1
+    for (int e = 0; e < ROWS / 4; ++e) {
+      const int r = (e >> 2) * 16 + g * 4 + (e & 3);
+      G[r * ldg + k] = act_bwd(act, P[r * ldp + k], G[r * ldg + k]);
+    }
+  }
+}
+
+// Forward: Y[r][n] = act(sum_k X[r][k] W[n][k] + b[n]) for n < Np (padded -> 0).
+// P (optional) keeps the pre-activation; Pg (optional) stashes rows >= pg_row0.
+template <typename T, int ROWS>
+__device__ __forceinline__ void layer_fwd(const lf* X, int ldx, const LayerDev& L, const float* bias_, int act, lf* P,
+                                          int ldp, lf* Y, int ldy, float* Pg_, int pg_row0, Pf<T>& pf,
+                                          const GemmW& next) {
   const AS_G float* bias = GPC(float, bias_);
   AS_G float* Pg = GP(float, Pg_);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int c = lane & 15, g = lane >> 4;
-  const AS_G T* W = GPC(T, Wc_);
-  const int NT = Np >> 4, nch = Kp / KC;
-  (void)K;
-#ifdef SAC_STAMPS
-  int lcall = 0;
-  if (blockIdx.x == 0 && threadIdx.x == 0) lcall = atomicAdd(&g_lcall, 1);
-#endif
-  LSTAMP(0);
-  for (int nt0 = wave; nt0 < NT; nt0 += 2 * SAC_NW) {
-    const int nt1 = nt0 + SAC_NW;
-    const bool has1 = nt1 < NT;
-    const int n0 = nt0 * 16 + c, n1 = (has1 ? nt1 : nt0) * 16 + c;
-    const float bn0 = bias[n0 < N ? n0 : N - 1], bn1 = bias[n1 < N ? n1 : N - 1];  // issued with the weights
-    f32x4 acc0[RT], acc1[RT];
+  const int g = lane >> 4;
+  const int N = L.N, Np = L.Np;
+  // The first pair's bias is loaded before the step: a load issued after the
+  // next step's prefetch would wait for all of it (vmcnt retires in order).
+  const int n0 = wave * 16 + (lane & 15), n1 = n0 + 16 * SAC_NW;
+  const float bpre0 = bias[n0 < N ? n0 : N - 1], bpre1 = bias[n1 < N ? n1 : N - 1];
+  gemm_step<T, ROWS>(X, ldx, gw_fwd(L), pf, next, [&](int h, int n, const f32x4* acc) {
+    const bool nv = n < N;
+    const float bn = n == n0 ? bpre0 : n == n1 ? bpre1 : bias[nv ? n : N - 1];
 #pragma unroll
-    for (int rt = 0; rt < RT; ++rt) acc0[rt] = acc1[rt] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    LSTAMP(1);
-    mma_pair<T, RT>(X + c * ldx + g * KL, ldx, W + packed_lane<T>(nt0, Kp, lane),
-                    W + packed_lane<T>(has1 ? nt1 : nt0, Kp, lane), has1, nch, acc0, acc1);
-    LSTAMP(3);
+    for (int rt = 0; rt < ROWS / 16; ++rt)
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      if (h == 1 && !has1) break;
-      const int n = h ? n1 : n0;
-      const bool nv = n < N;
-      const float bn = h ? bn1 : bn0;
-#pragma unroll
-      for (int rt = 0; rt < RT; ++rt)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int r = rt * 16 + g * 4 + i;
-          const float p = nv ? (h ? acc1[rt][i] : acc0[rt][i]) + bn : 0.f;
-          if (P) P[r * ldp + n] = p;
-          Y[r * ldy + n] = act_fwd(act, p);
-          if (Pg && r >= pg_row0) Pg[(size_t)(r - pg_row0) * Np + n] = p;
-        }
-    }
-    LSTAMP(4);
-  }
-  LSTAMP(5);
+      for (int i = 0; i < 4; ++i) {
+        const int r = rt * 16 + g * 4 + i;
+        const float p = nv ? acc[rt][i] + bn : 0.f;
+        if (P) P[r * ldp + n] = p;
+        Y[r * ldy + n] = act == ACT_RELU ? (p > 0.f ? p : 0.f) : p;
+        if (Pg && r >= pg_row0) Pg[(size_t)(r - pg_row0) * Np + n] = p;
+      }
+  });
+  if (act != ACT_RELU && act != ACT_ID) act_pass_fwd<ROWS>(Y, ldy, Np >> 4, act);
 }
 
-// Gout[r][k] = act'(Pprev[r][k]) * sum_n G[r][n] W[n][k]   (act_prev < 0: no act')
-template <typename T, int ROWS>
-__device__ __forceinline__ void layer_bwd_(const lf* __restrict__ G, int ldg, const void* WTc_, int K, int N, int Kp,
-                                           int Np, const lf* __restrict__ Pprev, int ldp, int act_prev,
-                                           lf* __restrict__ Gout, int ldo) {
-  constexpr int RT = ROWS / 16;
-  constexpr int KC = MM<T>::KC, KL = MM<T>::KL;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int c = lane & 15, g = lane >> 4;
-  const AS_G T* WT = GPC(T, WTc_);
-  const int KT = Kp >> 4, nch = Np / KC;
-  (void)N;
-  for (int kt0 = wave; kt0 < KT; kt0 += 2 * SAC_NW) {
-    const int kt1 = kt0 + SAC_NW;
-    const bool has1 = kt1 < KT;
-    const int k0 = kt0 * 16 + c, k1 = (has1 ? kt1 : kt0) * 16 + c;
-    f32x4 acc0[RT], acc1[RT];
-#pragma unroll
-    for (int rt = 0; rt < RT; ++rt) acc0[rt] = acc1[rt] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    mma_pair<T, RT>(G + c * ldg + g * KL, ldg, WT + packed_lane<T>(kt0, Np, lane),
-                    WT + packed_lane<T>(has1 ? kt1 : kt0, Np, lane), has1, nch, acc0, acc1);
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      if (h == 1 && !has1) break;
-      const int k = h ? k1 : k0;
-      const bool kv = k < K;
-#pragma unroll
-      for (int rt = 0; rt < RT; ++rt)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int r = rt * 16 + g * 4 + i;
-          const float a = h ? acc1[rt][i] : acc0[rt][i];
-          float v = 0.f;
-          if (kv) v = act_prev >= 0 ? act_bwd(act_prev, Pprev[r * ldp + k], a) : a;
-          Gout[r * ldo + k] = v;
-        }
-    }
-  }
-}
-
-template <typename T, int ROWS>
-__device__ __forceinline__ void layer_fwd(const lf* X, int ldx, const LayerDev& L, const float* bias, int act, lf* P,
-                                          int ldp, lf* Y, int ldy, float* Pg, int pg_row0) {
-  layer_fwd_<T, ROWS>(X, ldx, L.Wc, L.K, L.N, L.Kp, L.Np, bias, act, P, ldp, Y, ldy, Pg, pg_row0);
-}
+// dX: Gout[r][k] = act'(Pprev[r][k]) * sum_n G[r][n] W[n][k]   (act_prev < 0: no act')
 template <typename T, int ROWS>
 __device__ __forceinline__ void layer_bwd(const lf* G, int ldg, const LayerDev& L, const lf* Pprev, int ldp,
-                                          int act_prev, lf* Gout, int ldo) {
-  layer_bwd_<T, ROWS>(G, ldg, L.WTc, L.K, L.N, L.Kp, L.Np, Pprev, ldp, act_prev, Gout, ldo);
+                                          int act_prev, lf* Gout, int ldo, Pf<T>& pf, const GemmW& next) {
+  const int g = (threadIdx.x & 63) >> 4;
+  const int K = L.K;
+  gemm_step<T, ROWS>(G, ldg, gw_bwd(L), pf, next, [&](int, int k, const f32x4* acc) {
+    const bool kv = k < K;
+#pragma unroll
+    for (int rt = 0; rt < ROWS / 16; ++rt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int r = rt * 16 + g * 4 + i;
+        float v = kv ? acc[rt][i] : 0.f;
+        if (act_prev == ACT_RELU && !(Pprev[r * ldp + k] > 0.f)) v = 0.f;
+        Gout[r * ldo + k] = v;
+      }
+  });
+  if (act_prev >= 0 && act_prev != ACT_RELU && act_prev != ACT_ID)
+    act_pass_bwd<ROWS>(Gout, ldo, Pprev, ldp, L.Kp >> 4, K, act_prev);
 }
 
 // dst[k][col0 + r] = src[r][k] (0 for k >= K or r >= nvalid), k < Kp; with
@@ -296,24 +403,25 @@ __device__ __forceinline__ void store_T(const lf* __restrict__ src, int lds_ld, 
 // Full MLP forward over ROWS rows: hidden layers ping-pong Xb/Yb (stride ld), the
 // output layer writes (Pout, Yout) with stride ldo.  keepP: per-layer
 // pre-activations into lds[o_P[l]] (stride ldp[l]).  storeXT: each layer's input
-// transposed into L.XT (ROWS must be SAC_ROWS).
+// transposed into L.XT (ROWS must be SAC_ROWS).  after: the GEMM step that follows.
 template <typename T, int ROWS>
 __device__ __forceinline__ void mlp_forward(const NetDev& net, lf* Xb, lf* Yb, int ld, lf* Pout, lf* Yout, int ldo,
                                             const int* o_P, const int* ldp, lf* lds, bool keepP, bool storeXT, int Bp,
-                                            int col0, int nvalid) {
+                                            int col0, int nvalid, Pf<T>& pf, const GemmW& after) {
   lf* X = Xb;
   lf* Y = Yb;
   for (int l = 0; l < net.L; ++l) {
     const LayerDev& Ly = net.l[l];
     const bool out = l == net.L - 1;
+    const GemmW next = out ? after : gw_fwd(net.l[l + 1]);
     if (storeXT) {
       if constexpr (ROWS == SAC_ROWS) store_T<T, ROWS>(X, ld, Ly.Kp, Ly.K, Ly.XT, Bp, col0, nvalid, nullptr);
     }
     if (out)
-      layer_fwd<T, ROWS>(X, ld, Ly, net.P + Ly.b_off, net.out_act, Pout, ldo, Yout, ldo, nullptr, 0);
+      layer_fwd<T, ROWS>(X, ld, Ly, net.P + Ly.b_off, net.out_act, Pout, ldo, Yout, ldo, nullptr, 0, pf, next);
     else
       layer_fwd<T, ROWS>(X, ld, Ly, net.P + Ly.b_off, net.hid_act, keepP ? lds + o_P[l] : nullptr,
-                         keepP ? ldp[l] : 0, Y, ld, nullptr, 0);
+                         keepP ? ldp[l] : 0, Y, ld, nullptr, 0, pf, next);
     __syncthreads();
     lf* t = X;
     X = Y;
@@ -327,11 +435,12 @@ __device__ __forceinline__ void mlp_forward(const NetDev& net, lf* Xb, lf* Yb, i
 template <typename T, int ROWS>
 __device__ __forceinline__ lf* mlp_backward(const NetDev& net, const lf* Gout, int ldo, lf* Xb, lf* Yb, int ld,
                                             const int* o_P, const int* ldp, lf* lds, bool storeGT, int Bp, int col0,
-                                            int nvalid) {
+                                            int nvalid, Pf<T>& pf, const GemmW& after) {
   const int Lh = net.L - 1;
   const LayerDev& Lo = net.l[Lh];
   if (storeGT) store_T<T, ROWS>(Gout, ldo, Lo.Np, Lo.N, Lo.GT, Bp, col0, nvalid, Lo.dbp);
-  layer_bwd<T, ROWS>(Gout, ldo, Lo, lds + o_P[Lh - 1], ldp[Lh - 1], net.hid_act, Yb, ld);
+  layer_bwd<T, ROWS>(Gout, ldo, Lo, lds + o_P[Lh - 1], ldp[Lh - 1], net.hid_act, Yb, ld, pf,
+                     Lh - 1 >= 1 ? gw_bwd(net.l[Lh - 1]) : after);
   __syncthreads();
   lf* G = Yb;
   lf* Gn = Xb;
@@ -339,7 +448,8 @@ __device__ __forceinline__ lf* mlp_backward(const NetDev& net, const lf* Gout, i
     const LayerDev& Ly = net.l[l];
     if (storeGT) store_T<T, ROWS>(G, ld, Ly.Np, Ly.N, Ly.GT, Bp, col0, nvalid, Ly.dbp);
     if (l == 0) break;
-    layer_bwd<T, ROWS>(G, ld, Ly, lds + o_P[l - 1], ldp[l - 1], net.hid_act, Gn, ld);
+    layer_bwd<T, ROWS>(G, ld, Ly, lds + o_P[l - 1], ldp[l - 1], net.hid_act, Gn, ld, pf,
+                       l - 1 >= 1 ? gw_bwd(net.l[l - 1]) : after);
     __syncthreads();
     lf* t = G;
     G = Gn;
@@ -357,9 +467,11 @@ __device__ __forceinline__ float fmin_nan(float a, float b) { return (a != a) ? 
 // ============================================================================ phase A
 // sample + gather, pi on [s'; s], target twin-Q -> y, critics forward + backward.
 template <typename T>
-__global__ void __launch_bounds__(SAC_THREADS) sac_target_critic(const EngineDev E, sac_replay rb,
+__global__ void __launch_bounds__(SAC_THREADS) sac_target_critic(const EngineDev* __restrict__ Ep, sac_replay rb,
                                                                   const int32_t* __restrict__ inj_idx_,
                                                                   const float* __restrict__ inj_eps_) {
+  PREFETCH_ARG(Ep);
+  const EngineDev& E = *Ep;
   extern __shared__ float lds_raw[];
   lf* lds = (lf*)lds_raw;
   constexpr int R = SAC_ROWS;
@@ -388,6 +500,8 @@ __global__ void __launch_bounds__(SAC_THREADS) sac_target_critic(const EngineDev
   lf* gqB = lds + E.o_gout;
   AS_L int64_t* slotB = (AS_L int64_t*)(lds + E.o_slot);
   const NetDev& pi = E.net[NET_PI];
+  Pf<T> pf;
+  pf_issue<T>(pf, gw_fwd(pi.l[0]));  // first weights stream in under the sample/gather
   const AS_G float* obs = GPC(float, rb.obs);
   const AS_G float* nobs = GPC(float, rb.next_obs);
   const AS_G float* ract = GPC(float, rb.act);
@@ -395,7 +509,17 @@ __global__ void __launch_bounds__(SAC_THREADS) sac_target_critic(const EngineDev
   const AS_G float* rdone = GPC(float, rb.done);
   AS_G float* stats = GP(float, E.stats);
 
-  if (blockIdx.x == 0 && tid < 4 && (tid < 3 || E.auto_entropy)) GP(double, E.opt_steps)[tid] += 1.0;
+  // optimizer step counters and this step's Adam bias-correction scalars
+  // (torch adam.py: step_size = lr / (1 - beta1^t), bias_correction2_sqrt), once per step
+  if (blockIdx.x == 0 && tid < 4 && (tid < 3 || E.auto_entropy)) {
+    const double t = GP(double, E.opt_steps)[tid] + 1.0;
+    GP(double, E.opt_steps)[tid] = t;
+    if (tid < 3) {
+      const double lr = tid == 0 ? E.actor_lr : E.critic_lr;
+      GP(float, E.adam_sc)[tid * 2] = (float)(-(lr / (1.0 - pow((double)E.beta1, t))));
+      GP(float, E.adam_sc)[tid * 2 + 1] = (float)sqrt(1.0 - pow((double)E.beta2, t));
+    }
+  }
 
   // ---- sample (replay_buffer.py:32-39) + gather (agent.py:166-193)
   const uint64_t step = *GPC(uint64_t, E.rng_step);
@@ -468,9 +592,11 @@ __global__ void __launch_bounds__(SAC_THREADS) sac_target_critic(const EngineDev
       const LayerDev& Ly = pi.l[l];
       store_T<T, R>(X + R * ld, ld, Ly.Kp, Ly.K, Ly.XT, Bp, r0, nvalid, nullptr);  // actor rows' input
       if (l == pi.L - 1)
-        layer_fwd<T, 2 * R>(X, ld, Ly, pi.P + Ly.b_off, pi.out_act, outP, ldo, outB, ldo, Ly.pstash + (size_t)r0 * Ly.Np, R);
+        layer_fwd<T, 2 * R>(X, ld, Ly, pi.P + Ly.b_off, pi.out_act, outP, ldo, outB, ldo,
+                            Ly.pstash + (size_t)r0 * Ly.Np, R, pf, gw_fwd(E.net[NET_Q1T].l[0]));
       else
-        layer_fwd<T, 2 * R>(X, ld, Ly, pi.P + Ly.b_off, pi.hid_act, nullptr, 0, Y, ld, Ly.pstash + (size_t)r0 * Ly.Np, R);
+        layer_fwd<T, 2 * R>(X, ld, Ly, pi.P + Ly.b_off, pi.hid_act, nullptr, 0, Y, ld, Ly.pstash + (size_t)r0 * Ly.Np,
+                            R, pf, gw_fwd(pi.l[l + 1]));
       __syncthreads();
       STAMP(2 + l);
       lf* t = X;
@@ -544,7 +670,8 @@ __global__ void __launch_bounds__(SAC_THREADS) sac_target_critic(const EngineDev
       Xb[r * ld + k] = k < O ? s2B[r * O + k] : (k < O + A ? a2B[r * A + (k - O)] : 0.f);
     }
     __syncthreads();
-    mlp_forward<T, R>(q, Xb, Yb, ld, outP, outB, ldo, E.o_P1, E.ldp1, lds, false, false, Bp, r0, nvalid);
+    mlp_forward<T, R>(q, Xb, Yb, ld, outP, outB, ldo, E.o_P1, E.ldp1, lds, false, false, Bp, r0, nvalid, pf,
+                      gw_fwd(E.net[t ? NET_Q1 : NET_Q2T].l[0]));
     if (tid < R) qtB[t * R + tid] = outB[tid * ldo];
     __syncthreads();
     STAMP(7 + t);
@@ -575,9 +702,10 @@ __global__ void __launch_bounds__(SAC_THREADS) sac_target_critic(const EngineDev
       const LayerDev& Ly = q.l[l];
       if (l > 0) store_T<T, R>(X, ld, Ly.Kp, Ly.K, Ly.XT, Bp, r0, nvalid, nullptr);
       if (l == q.L - 1)
-        layer_fwd<T, R>(X, ld, Ly, q.P + Ly.b_off, q.out_act, outP, ldo, outB, ldo, nullptr, 0);
+        layer_fwd<T, R>(X, ld, Ly, q.P + Ly.b_off, q.out_act, outP, ldo, outB, ldo, nullptr, 0, pf, gw_bwd(Ly));
       else
-        layer_fwd<T, R>(X, ld, Ly, q.P + Ly.b_off, q.hid_act, lds + E.o_P1[l], E.ldp1[l], Y, ld, nullptr, 0);
+        layer_fwd<T, R>(X, ld, Ly, q.P + Ly.b_off, q.hid_act, lds + E.o_P1[l], E.ldp1[l], Y, ld, nullptr, 0, pf,
+                        gw_fwd(q.l[l + 1]));
       __syncthreads();
       lf* t = X;
       X = Y;
@@ -598,7 +726,8 @@ __global__ void __launch_bounds__(SAC_THREADS) sac_target_critic(const EngineDev
       if (tid == 0) GP(float, E.lossp)[blockIdx.x * 4 + qi] = sq;
     }
     __syncthreads();
-    mlp_backward<T, R>(q, gqB, ldo, Xb, Yb, ld, E.o_P1, E.ldp1, lds, true, Bp, r0, nvalid);
+    mlp_backward<T, R>(q, gqB, ldo, Xb, Yb, ld, E.o_P1, E.ldp1, lds, true, Bp, r0, nvalid, pf,
+                       qi == 0 ? gw_fwd(E.net[NET_Q2].l[0]) : gw_none());
     STAMP(11 + 2 * qi);
   }
 }
@@ -606,7 +735,9 @@ __global__ void __launch_bounds__(SAC_THREADS) sac_target_critic(const EngineDev
 // ============================================================================ phase C
 // critics on (s, a~) with the updated weights, d a~, head backward, pi backward.
 template <typename T>
-__global__ void __launch_bounds__(SAC_THREADS) sac_actor(const EngineDev E) {
+__global__ void __launch_bounds__(SAC_THREADS) sac_actor(const EngineDev* __restrict__ Ep) {
+  PREFETCH_ARG(Ep);
+  const EngineDev& E = *Ep;
   extern __shared__ float lds_raw[];
   lf* lds = (lf*)lds_raw;
   constexpr int R = SAC_ROWS;
@@ -630,6 +761,8 @@ __global__ void __launch_bounds__(SAC_THREADS) sac_actor(const EngineDev E) {
   lf* outP2 = lds + E.o_outp2;
   const NetDev& pi = E.net[NET_PI];
   const float alpha32 = (float)*GPC(double, E.alpha_state + 1);
+  Pf<T> pf;
+  pf_issue<T>(pf, gw_fwd(E.net[NET_Q1].l[0]));
 
   for (int i = tid; i < R * O; i += SAC_THREADS) sB[i] = GPC(float, E.s_st)[(size_t)r0 * O + i];
   for (int i = tid; i < R * A; i += SAC_THREADS) {
@@ -649,7 +782,8 @@ __global__ void __launch_bounds__(SAC_THREADS) sac_actor(const EngineDev E) {
     }
     __syncthreads();
     mlp_forward<T, R>(q, Xb, Yb, ld, qi ? outP2 : outP1, qi ? out2 : out1, ldo, qi ? E.o_P2 : E.o_P1,
-                      qi ? E.ldp2 : E.ldp1, lds, true, false, Bp, r0, nvalid);
+                      qi ? E.ldp2 : E.ldp1, lds, true, false, Bp, r0, nvalid, pf,
+                      qi ? gw_bwd(E.net[NET_Q1].l[E.net[NET_Q1].L - 1]) : gw_fwd(E.net[NET_Q2].l[0]));
     STAMP(36 + qi);
   }
   // ---- L_pi = mean(alpha logpi - min Q) (agent.py:251-252); min backward splits ties
@@ -681,9 +815,10 @@ __global__ void __launch_bounds__(SAC_THREADS) sac_actor(const EngineDev E) {
   for (int qi = 0; qi < 2; ++qi) {
     const NetDev& q = E.net[NET_Q1 + qi];
     lf* G0 = mlp_backward<T, R>(q, qi ? g2B : g1B, ldo, Xb, Yb, ld, qi ? E.o_P2 : E.o_P1, qi ? E.ldp2 : E.ldp1, lds,
-                                false, Bp, r0, nvalid);
+                                false, Bp, r0, nvalid, pf, gw_bwd(q.l[0]));
     lf* Gx = (G0 == Xb) ? Yb : Xb;
-    layer_bwd<T, R>(G0, ld, q.l[0], nullptr, 0, -1, Gx, ld);
+    layer_bwd<T, R>(G0, ld, q.l[0], nullptr, 0, -1, Gx, ld, pf,
+                    qi ? gw_bwd(pi.l[pi.L - 1]) : gw_bwd(E.net[NET_Q2].l[E.net[NET_Q2].L - 1]));
     __syncthreads();
     for (int i = tid; i < R * A; i += SAC_THREADS) gaB[i] += Gx[(i / A) * ld + O + i % A];
     __syncthreads();
@@ -737,7 +872,7 @@ __global__ void __launch_bounds__(SAC_THREADS) sac_actor(const EngineDev E) {
     for (int i = tid; i < R * pad; i += SAC_THREADS) goutB[(i / pad) * ldo + 2 * A + i % pad] = 0.f;
   }
   __syncthreads();
-  mlp_backward<T, R>(pi, goutB, ldo, Xb, Yb, ld, E.o_P1, E.ldp1, lds, true, Bp, r0, nvalid);
+  mlp_backward<T, R>(pi, goutB, ldo, Xb, Yb, ld, E.o_P1, E.ldp1, lds, true, Bp, r0, nvalid, pf, gw_none());
   STAMP(35);
 }
 
@@ -756,7 +891,7 @@ __device__ __forceinline__ float adam_elem(float& p, float& m, float& v, float g
 }
 
 template <typename T>
-__device__ __forceinline__ void dw_adam_tile(const EngineDev& E, const TileDesc* tdp, float lr, bool polyak) {
+__device__ __forceinline__ void dw_adam_tile(const EngineDev& E, const TileDesc* tdp, bool polyak) {
   constexpr int KC = MM<T>::KC, KL = MM<T>::KL;
   __shared__ float red[32][9];
   const TileDesc td = *tdp;
@@ -807,11 +942,8 @@ __device__ __forceinline__ void dw_adam_tile(const EngineDev& E, const TileDesc*
   }
   for (; ch < nch; ++ch) MM<T>::mma(acc, MM<T>::ld(arow + ch * KC), MM<T>::ld(brow + ch * KC));
 
-  const double t = GPC(double, E.opt_steps)[td.opt];
-  const double bc1 = 1.0 - pow((double)E.beta1, t);
-  const double bc2 = 1.0 - pow((double)E.beta2, t);
-  const float neg_step = (float)(-((double)lr / bc1));
-  const float bc2s = (float)sqrt(bc2);
+  const float neg_step = GPC(float, E.adam_sc)[td.opt * 2];
+  const float bc2s = GPC(float, E.adam_sc)[td.opt * 2 + 1];
   const float w1 = (float)(1.0 - (double)E.beta1), b2 = E.beta2, w2 = (float)(1.0 - (double)E.beta2);
   const float eps = E.adam_eps, tau = E.tau, omt = (float)(1.0 - (double)E.tau);
   AS_G T* Wc = GP(T, td.Wc);
@@ -857,8 +989,10 @@ __device__ __forceinline__ void dw_adam_tile(const EngineDev& E, const TileDesc*
 }
 
 template <typename T>
-__global__ void __launch_bounds__(256) sac_critic_update(const EngineDev E, const TileDesc* __restrict__ tiles) {
-  dw_adam_tile<T>(E, tiles + blockIdx.x, E.critic_lr, true);
+__global__ void __launch_bounds__(256) sac_critic_update(const EngineDev* __restrict__ Ep,
+                                                         const TileDesc* __restrict__ tiles) {
+  const EngineDev& E = *Ep;
+  dw_adam_tile<T>(E, tiles + blockIdx.x, true);
 }
 
 __device__ __forceinline__ void alpha_and_losses(const EngineDev& E) {
@@ -919,19 +1053,22 @@ __device__ __forceinline__ void alpha_and_losses(const EngineDev& E) {
 }
 
 template <typename T>
-__global__ void __launch_bounds__(256) sac_actor_update(const EngineDev E, const TileDesc* __restrict__ tiles,
+__global__ void __launch_bounds__(256) sac_actor_update(const EngineDev* __restrict__ Ep, const TileDesc* __restrict__ tiles,
                                                         int ntiles) {
+  const EngineDev& E = *Ep;
   if ((int)blockIdx.x < ntiles)
-    dw_adam_tile<T>(E, tiles + blockIdx.x, E.actor_lr, false);
+    dw_adam_tile<T>(E, tiles + blockIdx.x, false);
   else
     alpha_and_losses(E);
 }
 
 // ============================================================================ policy
 template <typename T>
-__global__ void __launch_bounds__(SAC_THREADS) sac_policy_act_kernel(const EngineDev E, const float* __restrict__ obs_, int n,
+__global__ void __launch_bounds__(SAC_THREADS) sac_policy_act_kernel(const EngineDev* __restrict__ Ep, const float* __restrict__ obs_, int n,
                                                              const float* __restrict__ eps_, float* __restrict__ action_,
                                                              float* __restrict__ log_pi_) {
+  PREFETCH_ARG(Ep);
+  const EngineDev& E = *Ep;
   extern __shared__ float lds_raw[];
   lf* lds = (lf*)lds_raw;
   constexpr int R = SAC_ROWS;
@@ -953,7 +1090,9 @@ __global__ void __launch_bounds__(SAC_THREADS) sac_policy_act_kernel(const Engin
     Xb[r * ld + k] = (k < O && r < nvalid) ? obs[(size_t)(r0 + r) * O + k] : 0.f;
   }
   __syncthreads();
-  mlp_forward<T, R>(pi, Xb, Yb, ld, outP, outB, ldo, E.o_P1, E.ldp1, lds, false, false, 0, 0, 0);
+  Pf<T> pf;
+  pf.tag = nullptr;
+  mlp_forward<T, R>(pi, Xb, Yb, ld, outP, outB, ldo, E.o_P1, E.ldp1, lds, false, false, 0, 0, 0, pf, gw_none());
   if (tid < nvalid) {
     const int b = r0 + tid;
     const lf* o = outB + tid * ldo;

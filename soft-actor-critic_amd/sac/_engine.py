@@ -39,7 +39,7 @@ class EngineConfig(ctypes.Structure):
         ("pi_hidden_act", ctypes.c_int32), ("pi_out_act", ctypes.c_int32),
         ("gamma", ctypes.c_float), ("tau", ctypes.c_float),
         ("log_std_min", ctypes.c_float), ("log_std_max", ctypes.c_float), ("action_scale", ctypes.c_float),
-        ("actor_lr", ctypes.c_float), ("critic_lr", ctypes.c_float), ("alpha_lr", ctypes.c_double),
+        ("actor_lr", ctypes.c_double), ("critic_lr", ctypes.c_double), ("alpha_lr", ctypes.c_double),
         ("beta1", ctypes.c_float), ("beta2", ctypes.c_float), ("adam_eps", ctypes.c_float),
         ("auto_entropy", ctypes.c_int32), ("target_entropy", ctypes.c_float),
         ("precision", ctypes.c_int32), ("seed", ctypes.c_uint64),

@@ -42,7 +42,7 @@ __global__ void __launch_bounds__(SAC_THREADS) layers(const bf16* W, const float
 // fragment-packed weights: fragment (tile nt, chunk ch) = 64 lanes x 16 B contiguous
 template <int ROWS>
 __global__ void __launch_bounds__(SAC_THREADS) layers_packed(const bf16* W, const float* bias, int nl, int distinct,
-                                                             long long* out, float* sink) {
+                                                             long long* out, float* sink, float* stash, int stores) {
   extern __shared__ float lds_raw[];
   lf* lds = (lf*)lds_raw;
   constexpr int RT = ROWS / 16;
@@ -80,6 +80,10 @@ __global__ void __launch_bounds__(SAC_THREADS) layers_packed(const bf16* W, cons
           const int r = rt * 16 + g * 4 + i;
           Y[r * ld + nt0 * 16 + c] = fmaxf(acc0[rt][i], 0.f);
           Y[r * ld + nt1 * 16 + c] = fmaxf(acc1[rt][i], 0.f);
+          if (stores) {
+            GP(float, stash)[((size_t)blockIdx.x * 64 + l) * 8192 + r * 256 + nt0 * 16 + c] = acc0[rt][i];
+            GP(float, stash)[((size_t)blockIdx.x * 64 + l) * 8192 + r * 256 + nt1 * 16 + c] = acc1[rt][i];
+          }
         }
     }
     __syncthreads();
@@ -97,6 +101,8 @@ int main() {
   CHK(hipMalloc(&bias, 256 * 4));
   CHK(hipMalloc(&sink, 256 * 16 * 4));
   CHK(hipMalloc(&out, 256 * 8));
+  float* stash;
+  CHK(hipMalloc(&stash, (size_t)256 * 64 * 8192 * 4));
   CHK(hipMemset(bias, 0, 1024));
   size_t lds = 2 * 32 * 260 * 4;
   CHK(hipFuncSetAttribute((const void*)layers<16>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
@@ -106,17 +112,18 @@ int main() {
   hipEvent_t e0, e1;
   CHK(hipEventCreate(&e0)); CHK(hipEventCreate(&e1));
   std::vector<long long> h(G);
-  for (int packed : {0, 1})
+  for (int packed : {0, 1, 2})
   for (int rows : {16, 32})
     for (int distinct : {1, 0})
       for (int fresh : {1, 0}) {
+        if (packed == 0 && rows == 32) continue;
         float ms_tot = 0; double cyc = 0; int reps = 50;
         for (int r = 0; r < reps + 5; ++r) {
           if (fresh) fill<<<1024, 256>>>(W, (size_t)NL * 256 * 256, 1.0f + r);
           CHK(hipEventRecord(e0));
           if (packed) {
-            if (rows == 16) layers_packed<16><<<G, SAC_THREADS, lds>>>(W, bias, NL, distinct, out, sink);
-            else layers_packed<32><<<G, SAC_THREADS, lds>>>(W, bias, NL, distinct, out, sink);
+            if (rows == 16) layers_packed<16><<<G, SAC_THREADS, lds>>>(W, bias, NL, distinct, out, sink, stash, packed == 2);
+            else layers_packed<32><<<G, SAC_THREADS, lds>>>(W, bias, NL, distinct, out, sink, stash, packed == 2);
           } else {
             if (rows == 16) layers<16><<<G, SAC_THREADS, lds>>>(W, bias, NL, distinct, out, sink);
             else layers<32><<<G, SAC_THREADS, lds>>>(W, bias, NL, distinct, out, sink);

@@ -56,9 +56,13 @@ torch.cuda.synchronize()
 arr = (ctypes.c_longlong * (64 * 6))()
 E.check(lib.sac_debug_layer_stamps(arr, 0))
 a = np.array(arr, dtype=np.int64).reshape(64, 6)
+print("raw first rows:", a[:3].tolist())
 print("--- layer_fwd calls of one step (block 0 wave 0): issue->first-mfma->mfma-done->epi-done->end, cycles")
+prev_end = None
 for i in range(64):
     if a[i, 0] == 0:
-        break
-    d = np.diff(a[i])
-    print(f"  call {i:2d}: issue {d[0]:6d}  wait-data {d[1]:6d}  mfma {d[2]:6d}  epi {d[3]:6d}  rest {d[4]:6d}  total {a[i,5]-a[i,0]:7d}")
+        continue
+    gap = 0 if prev_end is None else a[i, 0] - prev_end
+    print(f"  call {i:2d}: gap-before {gap:7d}  tile0 (start->mma-issued) {a[i,3]-a[i,1]:6d}  epi {a[i,4]-a[i,3]:6d}"
+          f"  total {a[i,5]-a[i,0]:7d}")
+    prev_end = a[i, 5]
