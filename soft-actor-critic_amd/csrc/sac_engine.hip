@@ -25,6 +25,7 @@
 #include <algorithm>
 #include <math.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 #include <string>
 #include <vector>
@@ -300,6 +301,12 @@ static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
     h.O = O;
     h.A = A;
     h.nrt = nrt;
+    {
+      int xs = 1;  // largest power of two <= 8 with nrt * xs <= 256 blocks
+      while (xs < 8 && nrt * xs * 2 <= 256) xs *= 2;
+      if (const char* v = getenv("SAC_XS")) xs = std::max(1, atoi(v));
+      h.xs = xs;
+    }
     h.auto_entropy = c->auto_entropy;
     h.gamma = c->gamma;
     h.tau = c->tau;
@@ -391,13 +398,13 @@ static void launch_phase(sac_engine* e, int phase, const sac_replay* rb, const i
                          hipStream_t s) {
   switch (phase) {
     case 0:
-      sac_target_critic<T><<<e->nrt, SAC_THREADS, e->lds_bytes, s>>>(e->d, *rb, idx, eps);
+      sac_target_critic<T><<<e->nrt * e->h.xs, SAC_THREADS, e->lds_bytes, s>>>(e->d, *rb, idx, eps);
       break;
     case 1:
       sac_critic_update<T><<<e->nB, 256, 0, s>>>(e->d, e->tilesB);
       break;
     case 2:
-      sac_actor<T><<<e->nrt, SAC_THREADS, e->lds_bytes, s>>>(e->d);
+      sac_actor<T><<<e->nrt * e->h.xs, SAC_THREADS, e->lds_bytes, s>>>(e->d);
       break;
     case 3:
       sac_actor_update<T><<<e->nD + 1, 256, 0, s>>>(e->d, e->tilesD, e->nD);

@@ -29,6 +29,10 @@ enum { NET_PI = 0, NET_Q1 = 1, NET_Q2 = 2, NET_Q1T = 3, NET_Q2T = 4 };
 
 struct EngineDev {
   int B, Bp, Br, O, A, nrt, ld, ldo;
+  // Row-tile workgroups of phases A and C are blocks xs*i (the others exit at
+  // once): blocks are dealt round-robin over the 8 XCDs, so xs > 1 packs the
+  // tiles onto 8/xs XCDs whose L2s then share one weight stream (speed only).
+  int xs;
   int auto_entropy;
   float gamma, tau, ls_min, ls_max, scale, beta1, beta2, adam_eps, target_entropy;
   double actor_lr, critic_lr, alpha_lr;
@@ -85,10 +89,11 @@ __device__ int g_lcall;
   } while (0)
 #endif
 
+
 #ifdef SAC_STAMPS
 #define STAMP(i)                                                                               \
   do {                                                                                         \
-    if (threadIdx.x == 0 && E.stamps) GP(long long, E.stamps)[blockIdx.x * 64 + (i)] = __builtin_amdgcn_s_memtime(); \
+    if (threadIdx.x == 0 && E.stamps) GP(long long, E.stamps)[(blockIdx.x / E.xs) * 64 + (i)] = __builtin_amdgcn_s_memtime(); \
   } while (0)
 #else
 #define STAMP(i) \
@@ -143,9 +148,9 @@ struct Pf {
 // Issue batch 0 (chunks 0..7, clamped) of this wave's first tile pair of step w.
 template <typename T>
 __device__ __forceinline__ void pf_issue(Pf<T>& pf, const GemmW& w) {
-  constexpr int KC = MM<T>::KC, FS = 64 * MM<T>::KL;
   pf.tag = w.p;
 #if SAC_PF
+  constexpr int KC = MM<T>::KC, FS = 64 * MM<T>::KL;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   if (!w.p || wave >= w.NT) return;
   const int last = w.cols / KC - 1;
@@ -363,7 +368,7 @@ __device__ __forceinline__ void layer_bwd(const lf* G, int ldg, const LayerDev& 
 }
 
 // dst[k][col0 + r] = src[r][k] (0 for k >= K or r >= nvalid), k < Kp; with
-// dbp != null also dbp[blockIdx.x][k] = sum_{r<nvalid} src[r][k] (k < K).
+// dbp != null also dbp[col0 / SAC_ROWS][k] = sum_{r<nvalid} src[r][k] (k < K).
 template <typename T, int ROWS>
 __device__ __forceinline__ void store_T(const lf* __restrict__ src, int lds_ld, int Kp, int K, void* dst_,
                                                  int Bp, int col0, int nvalid, float* dbp_) {
@@ -395,7 +400,7 @@ __device__ __forceinline__ void store_T(const lf* __restrict__ src, int lds_ld, 
     if (dbp) {
 #pragma unroll
       for (int o = 1; o < CH; o <<= 1) s += __shfl_xor(s, o, 64);
-      if (live && ch == 0 && k < K) dbp[(size_t)blockIdx.x * K + k] = s;
+      if (live && ch == 0 && k < K) dbp[(size_t)(col0 / SAC_ROWS) * K + k] = s;
     }
   }
 }
@@ -476,9 +481,10 @@ __global__ void __launch_bounds__(SAC_THREADS) sac_target_critic(const EngineDev
   lf* lds = (lf*)lds_raw;
   constexpr int R = SAC_ROWS;
   const int tid = threadIdx.x;
+  if (blockIdx.x % E.xs) return;  // XCD placement: see EngineDev::xs
   STAMP(0);
   const int B = E.B, Bp = E.Bp, O = E.O, A = E.A, ld = E.ld, ldo = E.ldo;
-  const int r0 = blockIdx.x * R;
+  const int rbi = blockIdx.x / E.xs, r0 = rbi * R;
   const int nvalid = min(R, B - r0);
   const AS_G int32_t* inj_idx = GPC(int32_t, inj_idx_);
   const AS_G float* inj_eps = GPC(float, inj_eps_);
@@ -723,7 +729,7 @@ __global__ void __launch_bounds__(SAC_THREADS) sac_target_critic(const EngineDev
         for (int n = 0; n < 32; ++n) gqB[tid * ldo + n] = n == 0 ? g : 0.f;
       }
       sq = wave_sum(sq);
-      if (tid == 0) GP(float, E.lossp)[blockIdx.x * 4 + qi] = sq;
+      if (tid == 0) GP(float, E.lossp)[rbi * 4 + qi] = sq;
     }
     __syncthreads();
     mlp_backward<T, R>(q, gqB, ldo, Xb, Yb, ld, E.o_P1, E.ldp1, lds, true, Bp, r0, nvalid, pf,
@@ -742,9 +748,10 @@ __global__ void __launch_bounds__(SAC_THREADS) sac_actor(const EngineDev* __rest
   lf* lds = (lf*)lds_raw;
   constexpr int R = SAC_ROWS;
   const int tid = threadIdx.x;
+  if (blockIdx.x % E.xs) return;  // XCD placement: see EngineDev::xs
   STAMP(32);
   const int B = E.B, Bp = E.Bp, O = E.O, A = E.A, ld = E.ld, ldo = E.ldo;
-  const int r0 = blockIdx.x * R;
+  const int rbi = blockIdx.x / E.xs, r0 = rbi * R;
   const int nvalid = min(R, B - r0);
   lf* Xb = lds + E.o_X;
   lf* Yb = lds + E.o_Y;
@@ -807,7 +814,7 @@ __global__ void __launch_bounds__(SAC_THREADS) sac_actor(const EngineDev* __rest
       }
     }
     term = wave_sum(term);
-    if (tid == 0) GP(float, E.lossp)[blockIdx.x * 4 + 2] = term;
+    if (tid == 0) GP(float, E.lossp)[rbi * 4 + 2] = term;
   }
   __syncthreads();
 
