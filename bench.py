@@ -45,7 +45,7 @@ def gemm_flops(obs, act, hidden, B):
     Gq1, Gp1 = Gq - qd[0] * qd[1], Gp - pd[0] * pd[1]
     A = 2 * B * (2 * Gp + 4 * Gq + 2 * Gq1)      # pi fwd (s,s'), 2 target + 2 critic fwd, critic dX
     Bk = 2 * B * (2 * Gq)                         # critic dW
-    C = 2 * B * (2 * Gq + 2 * Gq1 + Gp1)          # critic fwd on (s,a~), dX to a~, pi dX
+    C = 2 * B * (4 * Gq + Gp1)                    # critic fwd on (s,a~), critic dX down to a~, pi dX
     D = 2 * B * Gp                                 # pi dW
     total_survey = 2 * B * (3 * Gp + Gp1 + 10 * Gq + 2 * Gq1)  # SURVEY §8d F_alg
     return [A, Bk, C, D], total_survey, Gq, Gp
@@ -197,27 +197,13 @@ def main():
 
         dist.init_process_group("nccl", device_id=device)
 
-    from sac.replicas import replica_seed
+    from sac.replicas import replica_seed, timed_region
 
     seed = replica_seed(0, rank)
     eng, rb, c = build_engine(args.config, args.precision, seed, device)
 
     eng.train_graph(rb, args.warmup, args.chunk)
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    eng.train_graph(rb, args.steps, args.chunk)
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    el = torch.tensor([elapsed], dtype=torch.float64, device=device)
-    if dist:
-        dist.all_reduce(el, op=dist.ReduceOp.MAX)
-    elapsed = float(el.item())
+    elapsed = timed_region(lambda: eng.train_graph(rb, args.steps, args.chunk), torch.cuda.synchronize, device)
     total_steps = args.steps * world
     losses = eng.losses()
     if not all(np.isfinite(losses[:3])):

@@ -12,6 +12,10 @@ extern "C" {
  * ([grid][64]); only builds with -DSAC_STAMPS write them. */
 int sac_engine_debug_stamps(sac_engine *e, long long *dev_buf, void *stream);
 int sac_engine_debug_stamped(void);
+/* Host evaluation of the device sampler (the same inline code as the sampler
+ * inside sac_engine_train and sac_replay_sample_indices): out[b] = b-th element
+ * of the Philox-keyed Feistel permutation of [0, size) for RNG (seed, step). */
+int sac_debug_sample_indices_host(int64_t size, int32_t batch, uint64_t seed, uint64_t step, int32_t *out);
 #ifdef __cplusplus
 }
 #endif

@@ -623,20 +623,11 @@ int sac_engine_debug_stamps(sac_engine* e, long long* dev_buf, void* stream) {
   return SAC_OK;
 }
 
-int sac_debug_layer_stamps(long long* host, int reset) {
-#ifdef SAC_STAMPS
-  if (reset) {
-    int z = 0;
-    HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_lcall), &z, sizeof(int)));
-    return SAC_OK;
-  }
-  HIPCHK(hipMemcpyFromSymbol(host, HIP_SYMBOL(g_lstamp), sizeof(long long) * 64 * 6));
+int sac_debug_sample_indices_host(int64_t size, int32_t batch, uint64_t seed, uint64_t step, int32_t* out) {
+  if (!out || batch < 0 || size < batch) return fail(SAC_E_INVALID, "need 0 <= batch <= size and out != NULL");
+  const Feistel f = feistel_make(seed, step, size);
+  for (int32_t b = 0; b < batch; ++b) out[b] = (int32_t)feistel_sample(f, b, size);
   return SAC_OK;
-#else
-  (void)host;
-  (void)reset;
-  return fail(SAC_E_INVALID, "not a stamps build");
-#endif
 }
 
 int sac_engine_debug_stamped(void) {

@@ -75,19 +75,6 @@ struct TileDesc {
   int K, N, Kp, Np, n0, k0, opt, nrt;
 };
 
-#ifdef SAC_STAMPS
-// per-call sub-layer stamps of layer_fwd_ (block 0, wave 0): [call][5]
-__device__ long long g_lstamp[64 * 6];
-__device__ int g_lcall;
-#define LSTAMP(k)                                                                            \
-  do {                                                                                       \
-    if (blockIdx.x == 0 && threadIdx.x == 0 && lcall < 64) g_lstamp[lcall * 6 + (k)] = __builtin_amdgcn_s_memtime(); \
-  } while (0)
-#else
-#define LSTAMP(k) \
-  do {            \
-  } while (0)
-#endif
 
 
 #ifdef SAC_STAMPS

@@ -219,14 +219,8 @@ class SAC:
 
     # Reference sub-steps.  The engine fuses them; calling one alone is not a
     # supported mode of the fused step (see DESIGN.md "API surface").
-    def compute_target_q_values(self, rewards: Any, dones: Any, next_states: Any) -> Any:
-        """y = r + gamma (1-d)(min Qt(s',a') - alpha logpi(a'|s')), eager, no state change."""
-        with torch.no_grad():
-            next_actions, next_log_pi = self.policy_net.sample_action(next_states)
-            q1 = self.q_net1_target(next_states, next_actions)
-            q2 = self.q_net2_target(next_states, next_actions)
-            return rewards + self.config["sac"]["gamma"] * (1 - dones) * (
-                torch.min(q1, q2) - self.alpha.detach() * next_log_pi)
+    def compute_target_q_values(self, *a, **k):
+        self._fused_only("compute_target_q_values")
 
     def _fused_only(self, name):
         raise NotImplementedError(

@@ -157,6 +157,24 @@ class SacEngine:
         like = self.param_views(key)
         return _views(self.m[key], like), _views(self.v[key], like)
 
+    def state_tensors(self) -> Dict[str, torch.Tensor]:
+        """Every device tensor the step reads and writes (parameters, Adam
+        moments, alpha state, step counters, RNG step)."""
+        out = {f"param/{k}": v for k, v in self.flat.items()}
+        out.update({f"m/{k}": v for k, v in self.m.items()})
+        out.update({f"v/{k}": v for k, v in self.v.items()})
+        out.update(alpha_state=self.alpha_state, opt_steps=self.opt_steps, rng_step=self.rng_step)
+        return out
+
+    def snapshot(self) -> Dict[str, torch.Tensor]:
+        return {k: v.clone() for k, v in self.state_tensors().items()}
+
+    def restore(self, snap: Dict[str, torch.Tensor]) -> None:
+        """Copy a snapshot back in place and re-pack the compute copies."""
+        for k, v in self.state_tensors().items():
+            v.copy_(snap[k])
+        self.sync_params()
+
     # ------------------------------------------------------------------ compute
     def train(self, replay, n_steps: int = 1, indices: Optional[torch.Tensor] = None,
               eps: Optional[torch.Tensor] = None) -> None:

@@ -35,6 +35,30 @@ def aggregate_metrics(values: Sequence[float], group=None, device: Optional[torc
     return {"sum": s.tolist(), "mean": (s / world).tolist(), "max": m.tolist(), "world": world}
 
 
+def timed_region(run, sync, device: Optional[torch.device] = None, group=None) -> float:
+    """Wall time of ``run()`` bracketed by (barrier + ``sync()``) on both sides,
+    MAX over ranks (the bench contract; single process when not initialised)."""
+    import time
+
+    import torch.distributed as dist
+
+    on = dist.is_available() and dist.is_initialized()
+    sync()
+    if on:
+        dist.barrier(group)
+    sync()
+    t0 = time.perf_counter()
+    run()
+    sync()
+    if on:
+        dist.barrier(group)
+    sync()
+    el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=device)
+    if on:
+        dist.all_reduce(el, op=dist.ReduceOp.MAX, group=group)
+    return float(el.item())
+
+
 def aggregate_throughput(steps: int, wall_s: float, group=None, device=None) -> float:
     """Whole-job steps/s: total steps of all replicas / slowest replica's time."""
     agg = aggregate_metrics([steps, wall_s], group, device)

@@ -1,0 +1,222 @@
+"""GPU tests of the engine beyond the single-step oracle parity
+(tests/test_gpu_parity.py): replay storage and gather, the device sampler,
+the policy kernel, graph replay, multi-step determinism and checkpoints.
+Every call goes through libsac_engine.so (C ABI)."""
+import ctypes
+import os
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+DEV = torch.device("cuda", 0)
+
+
+@pytest.fixture(scope="module")
+def lib():
+    from sac import _engine as E
+
+    return E.load_library()
+
+
+def _engine(cfgname="c1", precision="fp32", seed=0, capacity=None):
+    import bench
+
+    c = dict(bench.CONFIGS[cfgname])
+    if capacity:
+        bench.CONFIGS[cfgname] = dict(c, capacity=capacity)
+    try:
+        return bench.build_engine(cfgname, precision, seed, DEV)
+    finally:
+        bench.CONFIGS[cfgname] = c
+
+
+# ---------------------------------------------------------------- replay buffer
+def test_replay_push_gather_ring_exact():
+    """push (single rows, staged) + push_batch with wrap-around; gather by
+    logical position == the deque model of replay_buffer.py:12-30 bit-exactly."""
+    from sac.replay_buffer import ReplayBuffer
+
+    O, A, cap = 5, 2, 37
+    rng = np.random.default_rng(0)
+    rb = ReplayBuffer(cap, device=DEV, stage_rows=8)
+    model = []
+    for it in range(6):
+        n = int(rng.integers(1, 30))
+        s = rng.standard_normal((n, O), dtype=np.float32)
+        a = rng.standard_normal((n, A), dtype=np.float32)
+        r = rng.standard_normal(n).astype(np.float64)  # Python-float rewards in the reference
+        s2 = rng.standard_normal((n, O), dtype=np.float32)
+        d = rng.random(n) < 0.3
+        if it % 2 == 0:
+            for i in range(n):
+                rb.push(s[i], a[i], float(r[i]), s2[i], bool(d[i]))
+        else:
+            rb.push_batch(s, a, r.astype(np.float32), s2, d)
+        for i in range(n):
+            model.append((s[i], a[i], np.float32(r[i]), s2[i], np.float32(d[i])))
+        model = model[-cap:]
+        assert len(rb) == len(model)
+        idx = np.arange(len(model))
+        t = rb.gather(idx)
+        got = [x.cpu().numpy() for x in t]
+        for f in range(5):
+            want = np.stack([np.asarray(m[f], np.float32) for m in model])
+            assert np.array_equal(got[f].reshape(want.shape), want), (it, f)
+
+
+def test_replay_sample_api(lib):
+    from sac.replay_buffer import ReplayBuffer
+
+    rb = ReplayBuffer(100, device=DEV)
+    for i in range(10):
+        rb.push(np.full(3, i, np.float32), np.full(1, -i, np.float32), float(i), np.full(3, i + 1, np.float32),
+                i == 9)
+    with pytest.raises(ValueError, match="Not enough samples"):
+        rb.sample(11)
+    out = rb.sample(10)
+    assert sorted(int(t.state[0]) for t in out) == list(range(10))
+    for t in out:
+        i = int(t.state[0])
+        assert t.reward == float(i) and t.done == (i == 9) and np.all(t.next_state == i + 1)
+
+
+# ---------------------------------------------------------------- device sampler
+@pytest.mark.parametrize("size,batch", [(64, 64), (1000, 256), (1_000_000, 256), (1_000_000, 4096)])
+def test_device_sampler_equals_host(lib, size, batch):
+    from oracle import sampler_oracle as S
+    from sac import _engine as E
+
+    f = lib.sac_debug_sample_indices_host
+    f.argtypes = [ctypes.c_int64, ctypes.c_int32, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_void_p]
+    state = torch.tensor([size, 0], dtype=torch.int64, device=DEV)
+    desc = E.ReplayDesc(0, 0, 0, 0, 0, size, 1, 1, state.data_ptr())
+    out = torch.empty(batch, dtype=torch.int32, device=DEV)
+    for step in (0, 5, 2**33 + 1):
+        E.check(lib.sac_replay_sample_indices(ctypes.byref(desc), batch, 11, step, E.ptr(out),
+                                              E.stream_handle(DEV)))
+        host = np.zeros(batch, np.int32)
+        assert f(size, batch, 11, step, host.ctypes.data) == 0
+        dev = out.cpu().numpy()
+        assert np.array_equal(dev, host)
+        assert np.unique(dev).size == batch and dev.min() >= 0 and dev.max() < size
+        if batch <= 256:
+            assert dev.tolist() == S.sample_indices(size, batch, 11, step)
+
+
+def test_in_step_sampler_is_the_exported_sampler(lib):
+    """A device-sampled step equals the same step fed the host sampler's
+    indices for (seed, rng_step): the fused kernel gathers exactly those rows."""
+    eng, rb, c = _engine("c1", "fp32")
+    f = lib.sac_debug_sample_indices_host
+    f.argtypes = [ctypes.c_int64, ctypes.c_int32, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_void_p]
+    eng.train(rb, 3)  # move off step 0
+    snap = eng.snapshot()
+    step = int(eng.rng_step.item())
+    eng.train(rb, 1)
+    a = {k: v.clone() for k, v in eng.state_tensors().items()}
+    la = eng.stats.clone()
+    eng.restore(snap)
+    host = np.zeros(c["batch"], np.int32)
+    assert f(len(rb), c["batch"], int(eng.cfg.seed), step, host.ctypes.data) == 0
+    # device eps stay on (eps=None): only the index source differs
+    eng.train(rb, 1, indices=torch.from_numpy(host).reshape(1, -1))
+    for k, v in eng.state_tensors().items():
+        assert torch.equal(v, a[k]), k
+    assert torch.equal(eng.stats, la)
+
+
+# ---------------------------------------------------------------- determinism / graphs
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_graph_replay_equals_direct_launches(precision):
+    eng, rb, _ = _engine("c1", precision)
+    snap = eng.snapshot()
+    eng.train(rb, 40)
+    a = {k: v.clone() for k, v in eng.state_tensors().items()}
+    eng.restore(snap)
+    eng.train_graph(rb, 40, chunk=16)  # 2 full chunks + a remainder
+    for k, v in eng.state_tensors().items():
+        assert torch.equal(v, a[k]), k
+    assert int(eng.rng_step.item()) == 40
+    assert eng.opt_steps.cpu().tolist()[:3] == [40.0, 40.0, 40.0]
+
+
+def test_c2_full_size_many_steps_properties():
+    """C2 at full size (1e6-row buffer, B=256, bf16): 300 steps stay finite,
+    alpha moves the right way, and Polyak keeps targets between their start
+    and the online critics (convex combination, tau = 0.005)."""
+    eng, rb, c = _engine("c2", "bf16")
+    q1t0 = eng.flat["q1t"].clone()
+    eng.train_graph(rb, 300, chunk=50)
+    torch.cuda.synchronize()
+    losses = eng.losses()
+    assert all(np.isfinite(losses)), losses
+    assert int(eng.rng_step.item()) == 300
+    # targets moved toward the critics but by far less than the critics moved
+    d_t = (eng.flat["q1t"] - q1t0).norm().item()
+    d_q = (eng.flat["q1"] - q1t0).norm().item()
+    assert 0 < d_t < d_q
+    lp = eng.last_log_pi().cpu().numpy()
+    y = eng.last_targets().cpu().numpy()
+    assert np.all(np.isfinite(lp)) and np.all(np.isfinite(y))
+
+
+# ---------------------------------------------------------------- policy kernel
+def _torch_policy(pi, s, eps):
+    mu, log_std = pi(s)
+    if eps is None:
+        return torch.tanh(mu) * pi.action_scale, None
+    std = log_std.exp()
+    z = mu + eps * std
+    a = torch.tanh(z) * pi.action_scale
+    lp = torch.distributions.Normal(mu, std).log_prob(z).sum(-1)
+    lp = lp - (2 * (np.log(2.0) - z - torch.nn.functional.softplus(-2 * z))).sum(-1)
+    return a, lp
+
+
+@pytest.mark.parametrize("precision,tol", [("fp32", 2e-5), ("bf16", 3e-2)])
+def test_policy_act_matches_torch(precision, tol):
+    eng, rb, c = _engine("c2", precision, capacity=1000)
+    pi = eng.nets["pi"]
+    g = torch.Generator(device="cpu").manual_seed(0)
+    for n in (1, 7, 300):
+        s = torch.randn(n, c["obs"], generator=g).to(DEV)
+        eps = torch.randn(n, c["act"], generator=g).to(DEV)
+        with torch.no_grad():
+            a_ref, _ = _torch_policy(pi, s, None)
+            a2_ref, lp_ref = _torch_policy(pi, s, eps)
+        a = eng.policy_act(s)
+        a2, lp = eng.policy_act(s, eps, want_log_pi=True)
+        assert (a - a_ref).abs().max().item() <= tol
+        assert (a2 - a2_ref).abs().max().item() <= tol
+        assert ((lp - lp_ref).abs() / lp_ref.abs().clamp_min(1.0)).max().item() <= tol
+
+
+# ---------------------------------------------------------------- checkpoints
+def test_save_load_roundtrip_continues_identically(tmp_path):
+    from _gpu import make_agent
+
+    agent, fx, meta, _ = make_agent("c1_auto", "fp32")
+    agent.train_steps(5)
+    path = os.path.join(tmp_path, "ckpt.pth")
+    agent.save_agent(path)
+    other, _, _, _ = make_agent("c1_auto", "fp32")
+    other.load_agent(path)
+    for a, b in ((agent.policy_net, other.policy_net), (agent.q_net1, other.q_net1),
+                 (agent.q_net2_target, other.q_net2_target)):
+        for (ka, va), (kb, vb) in zip(a.state_dict().items(), b.state_dict().items()):
+            assert torch.equal(va, vb), ka
+    assert torch.equal(agent.engine.alpha_state[:1], other.engine.alpha_state[:1])
+    for k in ("m/pi", "v/q1", "v/q2"):
+        assert torch.equal(agent.engine.state_tensors()[k], other.engine.state_tensors()[k]), k
+    assert agent.engine.opt_steps[:3].tolist() == other.engine.opt_steps[:3].tolist()
+    # the same injected step on both gives the same result
+    B, A = meta["batch"], meta["act"]
+    idx = torch.arange(B, dtype=torch.int32).reshape(1, B)
+    e = torch.randn(1, 2, B, A, generator=torch.Generator().manual_seed(1))
+    agent.engine.train(agent.replay_buffer, 1, indices=idx, eps=e)
+    other.engine.train(other.replay_buffer, 1, indices=idx, eps=e)
+    assert torch.equal(agent.engine.flat["pi"], other.engine.flat["pi"])
+    assert torch.equal(agent.engine.stats[:4], other.engine.stats[:4])

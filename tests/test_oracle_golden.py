@@ -45,11 +45,9 @@ def test_oracle_matches_reference(name):
 @pytest.mark.parametrize("name", FULL_INIT + ["c2", "donkey_new"])
 def test_models_init_matches_reference(name):
     """sac.models with the reference seeding reproduces the reference init bit-exactly."""
-    from _fixtures import init_state_dicts
+    import json
 
     fx, _ = load(name)
-    sds = init_state_dicts.__wrapped__(name) if hasattr(init_state_dicts, "__wrapped__") else None
-    import json
     from sac.models import PolicyNetwork, QNetwork
 
     meta = json.loads(str(fx["config"]))

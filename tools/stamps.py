@@ -38,7 +38,7 @@ names = {0: "A start", 1: "gather+eps", 2: "pi L0", 3: "pi L1", 4: "pi L2", 5: "
          7: "Qt1", 8: "Qt2", 10: "Q1 fwd", 11: "Q1 bwd", 12: "Q2 fwd", 13: "Q2 bwd",
          32: "C start", 36: "Q1 fwd", 37: "Q2 fwd", 38: "Q1 bwd->da", 39: "Q2 bwd->da", 35: "pi bwd"}
 for base, last in ((0, 13), (32, 39)):
-    idx = [i for i in range(base, 64) if i in names and st[:, i].min() > 0]
+    idx = [i for i in range(base, last + 1) if i in names and st[:, i].min() > 0]
     idx.sort(key=lambda i: np.median(st[:, i]))
     prev = None
     print(f"--- phase {'A' if base == 0 else 'C'} (cycles, median over blocks)")
@@ -47,22 +47,3 @@ for base, last in ((0, 13), (32, 39)):
         if prev is not None:
             print(f"  {names[i]:12s} +{t - prev:9.0f}   (cum {t:9.0f})")
         prev = t
-
-# ---- sub-layer stamps of layer_fwd (block 0, wave 0) for one step
-lib.sac_debug_layer_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
-E.check(lib.sac_debug_layer_stamps(None, 1))
-eng.train(rb, 1)
-torch.cuda.synchronize()
-arr = (ctypes.c_longlong * (64 * 6))()
-E.check(lib.sac_debug_layer_stamps(arr, 0))
-a = np.array(arr, dtype=np.int64).reshape(64, 6)
-print("raw first rows:", a[:3].tolist())
-print("--- layer_fwd calls of one step (block 0 wave 0): issue->first-mfma->mfma-done->epi-done->end, cycles")
-prev_end = None
-for i in range(64):
-    if a[i, 0] == 0:
-        continue
-    gap = 0 if prev_end is None else a[i, 0] - prev_end
-    print(f"  call {i:2d}: gap-before {gap:7d}  tile0 (start->mma-issued) {a[i,3]-a[i,1]:6d}  epi {a[i,4]-a[i,3]:6d}"
-          f"  total {a[i,5]-a[i,0]:7d}")
-    prev_end = a[i, 5]
