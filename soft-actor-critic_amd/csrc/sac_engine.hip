@@ -3,7 +3,7 @@
 //
 // One gradient step (reference sac/agent.py:302-327) = 4 launches:
 //
-//   A  sac_target_critic  row tiles of 16 batch rows, 16 waves.  Device sampler
+//   A  sac_target_critic  row tiles of 16 batch rows, 8 waves.  Device sampler
 //                         + replay gather (agent.py:166-193), pi forward on s' and s
 //                         (models.py:79-87), target twin-Q and y (agent.py:195-211),
 //                         Q1/Q2 forward + backward to every layer's pre-activation
