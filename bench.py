@@ -205,6 +205,7 @@ def main():
     eng.train_graph(rb, args.warmup, args.chunk)
     elapsed = timed_region(lambda: eng.train_graph(rb, args.steps, args.chunk), torch.cuda.synchronize, device)
     total_steps = args.steps * world
+    eng.check()  # in-launch hand-offs all completed
     losses = eng.losses()
     if not all(np.isfinite(losses[:3])):
         raise SystemExit(f"non-finite losses after benchmark: {losses}")

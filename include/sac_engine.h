@@ -170,6 +170,11 @@ int sac_replay_sample_indices(const sac_replay *rb, int32_t batch, uint64_t seed
 int sac_engine_time_phases(sac_engine *e, const sac_replay *rb, int32_t n_steps,
                            float *ms_host, void *stream);
 
+/* Health check (synchronises the stream): SAC_E_HIP if an in-launch
+ * workgroup hand-off of the role-split phase kernels gave up waiting (the
+ * affected steps are invalid), else 0.  Replaces: nothing (diagnostic). */
+int sac_engine_check(sac_engine *e, void *stream);
+
 /* Phase kernel names as they appear in rocprofv3 kernel traces. */
 const char *sac_phase_kernel_name(int32_t phase);
 

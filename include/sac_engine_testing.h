@@ -12,6 +12,9 @@ extern "C" {
  * ([grid][64]); only builds with -DSAC_STAMPS write them. */
 int sac_engine_debug_stamps(sac_engine *e, long long *dev_buf, void *stream);
 int sac_engine_debug_stamped(void);
+/* 1 if phases A/C run role-split (per-network workgroups with in-launch
+ * hand-offs), 0 if one workgroup per row tile runs all networks. */
+int sac_engine_uses_roles(const sac_engine *e);
 /* Host evaluation of the device sampler (the same inline code as the sampler
  * inside sac_engine_train and sac_replay_sample_indices): out[b] = b-th element
  * of the Philox-keyed Feistel permutation of [0, size) for RNG (seed, step). */

@@ -240,6 +240,8 @@ static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
   h.head_st = (float*)P(lay.take((size_t)Br * 4 * A * 4));
   h.lossp = (float*)P(lay.take((size_t)nrt * 4 * 4));
   h.adam_sc = (float*)P(lay.take(6 * 4));
+  h.sync = (uint32_t*)P(lay.take((size_t)(64 + HK_COUNT * nrt * 16) * 4));
+  h.hand = (float*)P(lay.take((size_t)HK_COUNT * nrt * SAC_HAND_STRIDE * 4));
   int nB = 0, nD = 0;
   for (int ni = NET_PI; ni <= NET_Q2; ++ni)
     for (int l = 0; l < h.net[ni].L; ++l)
@@ -306,6 +308,10 @@ static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
       while (xs < 8 && nrt * xs * 2 <= 256) xs *= 2;
       if (const char* v = getenv("SAC_XS")) xs = std::max(1, atoi(v));
       h.xs = xs;
+      // role split of phases A/C: 5 * nrt workgroups must be co-resident (one per CU)
+      int roles = 5 * nrt <= 256 && SAC_ROWS * (A + 1) <= SAC_HAND_STRIDE;
+      if (const char* v = getenv("SAC_ROLES")) roles = roles && atoi(v) != 0;
+      h.roles = roles;
     }
     h.auto_entropy = c->auto_entropy;
     h.gamma = c->gamma;
@@ -388,8 +394,10 @@ static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
 
 template <typename T>
 static void set_lds_attrs(size_t bytes) {
-  (void)hipFuncSetAttribute((const void*)sac_target_critic<T>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
-  (void)hipFuncSetAttribute((const void*)sac_actor<T>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+  (void)hipFuncSetAttribute((const void*)sac_target_critic<T, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+  (void)hipFuncSetAttribute((const void*)sac_target_critic<T, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+  (void)hipFuncSetAttribute((const void*)sac_actor<T, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+  (void)hipFuncSetAttribute((const void*)sac_actor<T, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
   (void)hipFuncSetAttribute((const void*)sac_policy_act_kernel<T>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
 }
 
@@ -398,13 +406,19 @@ static void launch_phase(sac_engine* e, int phase, const sac_replay* rb, const i
                          hipStream_t s) {
   switch (phase) {
     case 0:
-      sac_target_critic<T><<<e->nrt * e->h.xs, SAC_THREADS, e->lds_bytes, s>>>(e->d, *rb, idx, eps);
+      if (e->h.roles)
+        sac_target_critic<T, true><<<e->nrt * 5, SAC_THREADS, e->lds_bytes, s>>>(e->d, *rb, idx, eps);
+      else
+        sac_target_critic<T, false><<<e->nrt * e->h.xs, SAC_THREADS, e->lds_bytes, s>>>(e->d, *rb, idx, eps);
       break;
     case 1:
       sac_critic_update<T><<<e->nB, 256, 0, s>>>(e->d, e->tilesB);
       break;
     case 2:
-      sac_actor<T><<<e->nrt * e->h.xs, SAC_THREADS, e->lds_bytes, s>>>(e->d);
+      if (e->h.roles)
+        sac_actor<T, true><<<e->nrt * 3, SAC_THREADS, e->lds_bytes, s>>>(e->d);
+      else
+        sac_actor<T, false><<<e->nrt * e->h.xs, SAC_THREADS, e->lds_bytes, s>>>(e->d);
       break;
     case 3:
       sac_actor_update<T><<<e->nD + 1, 256, 0, s>>>(e->d, e->tilesD, e->nD);
@@ -511,6 +525,15 @@ int sac_engine_create(const sac_engine_config* cfg, const sac_engine_buffers* bu
     return rc;
   }
   *out = e;
+  return SAC_OK;
+}
+
+int sac_engine_check(sac_engine* e, void* stream) {
+  if (!e) return fail(SAC_E_INVALID, "null engine");
+  uint32_t w[2] = {0, 0};
+  HIPCHK(hipMemcpyAsync(w, e->h.sync, sizeof(w), hipMemcpyDeviceToHost, (hipStream_t)stream));
+  HIPCHK(hipStreamSynchronize((hipStream_t)stream));
+  if (w[1]) return fail(SAC_E_HIP, "a workgroup hand-off timed out: results of the affected steps are invalid");
   return SAC_OK;
 }
 
@@ -629,6 +652,8 @@ int sac_debug_sample_indices_host(int64_t size, int32_t batch, uint64_t seed, ui
   for (int32_t b = 0; b < batch; ++b) out[b] = (int32_t)feistel_sample(f, b, size);
   return SAC_OK;
 }
+
+int sac_engine_uses_roles(const sac_engine* e) { return e && e->h.roles ? 1 : 0; }
 
 int sac_engine_debug_stamped(void) {
 #ifdef SAC_STAMPS

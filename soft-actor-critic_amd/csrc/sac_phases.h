@@ -33,6 +33,7 @@ struct EngineDev {
   // once): blocks are dealt round-robin over the 8 XCDs, so xs > 1 packs the
   // tiles onto 8/xs XCDs whose L2s then share one weight stream (speed only).
   int xs;
+  int roles;  // phases A / C split into per-network workgroups (see "role hand-offs")
   int auto_entropy;
   float gamma, tau, ls_min, ls_max, scale, beta1, beta2, adam_eps, target_entropy;
   double actor_lr, critic_lr, alpha_lr;
@@ -47,6 +48,8 @@ struct EngineDev {
   double* opt_steps;
   float* adam_sc;     // [3][2]: -lr/bias_correction1, sqrt(bias_correction2) of this step (pi, q1, q2)
   uint64_t* rng_step;
+  uint32_t* sync;  // [0] launch epoch (phase D advances it), [1] hand-off timeout flag, [64 + 16 k] flags
+  float* hand;     // hand-off payloads [HK_COUNT][nrt][SAC_HAND_STRIDE]
   float* stats;
   long long* stamps;  // optional in-kernel timestamps (SAC_STAMPS builds)
   // LDS layout (float offsets)
@@ -80,7 +83,7 @@ struct TileDesc {
 #ifdef SAC_STAMPS
 #define STAMP(i)                                                                               \
   do {                                                                                         \
-    if (threadIdx.x == 0 && E.stamps) GP(long long, E.stamps)[(blockIdx.x / E.xs) * 64 + (i)] = __builtin_amdgcn_s_memtime(); \
+    if (threadIdx.x == 0 && E.stamps) GP(long long, E.stamps)[blockIdx.x * 64 + (i)] = __builtin_amdgcn_s_memtime(); \
   } while (0)
 #else
 #define STAMP(i) \
@@ -456,9 +459,58 @@ __device__ __forceinline__ lf* mlp_backward(const NetDev& net, const lf* Gout, i
 
 __device__ __forceinline__ float fmin_nan(float a, float b) { return (a != a) ? a : (a < b ? a : b); }
 
+// ============================================================================ role hand-offs
+// With E.roles, phases A and C run as several workgroups per row tile, one per
+// network ("role"), that hand small per-row results to each other inside the
+// launch (MI355X_MICROARCH.md §visibility, write-through form): every payload
+// store and load is an agent-scope (sc1) access, the storing waves drain their
+// stores (s_waitcnt vmcnt(0)) before a workgroup barrier, then one lane stores
+// the flag (sc1); the consumer polls the flag with sc1 loads from one lane and
+// joins the others at a barrier.  Flags carry a per-launch epoch (E.sync[0] + 1,
+// advanced by phase D), so they are never reset.  Producers have lower block
+// indices than their consumers and the grid fits one block per CU, so every
+// spin terminates; spins are still bounded and set E.sync[1] on a timeout.
+enum HandKind { HK_PI = 0, HK_T1 = 1, HK_T2 = 2, HK_C1 = 3, HK_C2 = 4, HK_COUNT = 5 };
+#define SAC_HAND_STRIDE 576  // floats per (kind, row tile) payload: >= SAC_ROWS * (act_dim + 1)
+
+__device__ __forceinline__ AS_G uint32_t* hand_flag(const EngineDev& E, int kind, int rbi) {
+  return GP(uint32_t, E.sync) + 64 + (kind * E.nrt + rbi) * 16;  // one 64-B line per flag
+}
+__device__ __forceinline__ AS_G float* hand_data(const EngineDev& E, int kind, int rbi) {
+  return GP(float, E.hand) + (size_t)(kind * E.nrt + rbi) * SAC_HAND_STRIDE;
+}
+__device__ __forceinline__ void st_sc1(AS_G float* p, float v) {
+  __hip_atomic_store((float*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float ld_sc1(const AS_G float* p) {
+  return __hip_atomic_load((float*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// all threads: after this workgroup's sc1 payload stores
+__device__ __forceinline__ void hand_publish(const EngineDev& E, int kind, int rbi, uint32_t ep) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_store((uint32_t*)hand_flag(E, kind, rbi), ep, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+}
+// all threads: returns once flag(kind, rbi) == ep (or the spin gave up)
+__device__ __forceinline__ void hand_wait(const EngineDev& E, int kind, int rbi, uint32_t ep) {
+  if (threadIdx.x == 0) {
+    uint32_t* f = (uint32_t*)hand_flag(E, kind, rbi);
+    for (int it = 0; __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != ep; ++it) {
+      if (it > (1 << 22)) {  // ~0.3 s: a producer never ran; flag the error, do not hang the GPU
+        __hip_atomic_store((uint32_t*)GP(uint32_t, E.sync) + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+  }
+  __syncthreads();
+}
+
 // ============================================================================ phase A
 // sample + gather, pi on [s'; s], target twin-Q -> y, critics forward + backward.
-template <typename T>
+// ROLES: block = role * nrt + row tile; role 0 pi, 1/2 target critics, 3/4 critics.
+template <typename T, bool ROLES>
 __global__ void __launch_bounds__(SAC_THREADS) sac_target_critic(const EngineDev* __restrict__ Ep, sac_replay rb,
                                                                   const int32_t* __restrict__ inj_idx_,
                                                                   const float* __restrict__ inj_eps_) {
@@ -468,11 +520,21 @@ __global__ void __launch_bounds__(SAC_THREADS) sac_target_critic(const EngineDev
   lf* lds = (lf*)lds_raw;
   constexpr int R = SAC_ROWS;
   const int tid = threadIdx.x;
-  if (blockIdx.x % E.xs) return;  // XCD placement: see EngineDev::xs
+  int rbi, role;
+  if (ROLES) {
+    rbi = blockIdx.x % E.nrt;
+    role = blockIdx.x / E.nrt;
+  } else {
+    if (blockIdx.x % E.xs) return;  // XCD placement: see EngineDev::xs
+    rbi = blockIdx.x / E.xs;
+    role = -1;
+  }
+  const bool do_pi = !ROLES || role == 0;
   STAMP(0);
   const int B = E.B, Bp = E.Bp, O = E.O, A = E.A, ld = E.ld, ldo = E.ldo;
-  const int rbi = blockIdx.x / E.xs, r0 = rbi * R;
+  const int r0 = rbi * R;
   const int nvalid = min(R, B - r0);
+  const uint32_t ep = ROLES ? *GPC(uint32_t, E.sync) + 1u : 0u;
   const AS_G int32_t* inj_idx = GPC(int32_t, inj_idx_);
   const AS_G float* inj_eps = GPC(float, inj_eps_);
   lf* Xb = lds + E.o_X;
@@ -494,7 +556,7 @@ __global__ void __launch_bounds__(SAC_THREADS) sac_target_critic(const EngineDev
   AS_L int64_t* slotB = (AS_L int64_t*)(lds + E.o_slot);
   const NetDev& pi = E.net[NET_PI];
   Pf<T> pf;
-  pf_issue<T>(pf, gw_fwd(pi.l[0]));  // first weights stream in under the sample/gather
+  pf_issue<T>(pf, gw_fwd(pi.l[0]));
   const AS_G float* obs = GPC(float, rb.obs);
   const AS_G float* nobs = GPC(float, rb.next_obs);
   const AS_G float* ract = GPC(float, rb.act);
@@ -504,7 +566,7 @@ __global__ void __launch_bounds__(SAC_THREADS) sac_target_critic(const EngineDev
 
   // optimizer step counters and this step's Adam bias-correction scalars
   // (torch adam.py: step_size = lr / (1 - beta1^t), bias_correction2_sqrt), once per step
-  if (blockIdx.x == 0 && tid < 4 && (tid < 3 || E.auto_entropy)) {
+  if (do_pi && rbi == 0 && tid < 4 && (tid < 3 || E.auto_entropy)) {
     const double t = GP(double, E.opt_steps)[tid] + 1.0;
     GP(double, E.opt_steps)[tid] = t;
     if (tid < 3) {
@@ -514,7 +576,8 @@ __global__ void __launch_bounds__(SAC_THREADS) sac_target_critic(const EngineDev
     }
   }
 
-  // ---- sample (replay_buffer.py:32-39) + gather (agent.py:166-193)
+  // ---- sample (replay_buffer.py:32-39) + gather (agent.py:166-193); every role
+  // draws the same indices from (seed, step), so no role waits for another's gather
   const uint64_t step = *GPC(uint64_t, E.rng_step);
   if (tid < R) {
     int64_t slot = -1;
@@ -548,7 +611,7 @@ __global__ void __launch_bounds__(SAC_THREADS) sac_target_critic(const EngineDev
     rB[tid] = sl >= 0 ? rrew[sl] : 0.f;
     dB[tid] = sl >= 0 ? rdone[sl] : 0.f;
   }
-  {
+  if (do_pi) {
     const int NP = (A + 1) / 2;
     for (int i = tid; i < 2 * R * NP; i += SAC_THREADS) {
       const int which = i / (R * NP), rem = i % (R * NP), r = rem / NP, p = rem % NP;
@@ -569,10 +632,10 @@ __global__ void __launch_bounds__(SAC_THREADS) sac_target_critic(const EngineDev
   }
   __syncthreads();
   STAMP(1);
-  for (int i = tid; i < R * O; i += SAC_THREADS) GP(float, E.s_st)[(size_t)r0 * O + i] = sB[i];
 
   // ---- pi forward on [s' ; s] (2R rows): target sample + actor sample
-  {
+  if (do_pi) {
+    for (int i = tid; i < R * O; i += SAC_THREADS) GP(float, E.s_st)[(size_t)r0 * O + i] = sB[i];
     const int Kp0 = pi.l[0].Kp;
     for (int i = tid; i < 2 * R * Kp0; i += SAC_THREADS) {
       const int r = i / Kp0, k = i % Kp0;
@@ -629,6 +692,7 @@ __global__ void __launch_bounds__(SAC_THREADS) sac_target_critic(const EngineDev
             GP(float, E.a_st)[(size_t)b * A + j] = act;
           } else {
             a2B[rr * A + j] = act;
+            if (ROLES) st_sc1(hand_data(E, HK_PI, rbi) + rr * A + j, act);
           }
         }
         for (int o = 1; o < AP; o <<= 1) {
@@ -645,89 +709,124 @@ __global__ void __launch_bounds__(SAC_THREADS) sac_target_critic(const EngineDev
             if (b < B) stats[4 + B + b] = v;
           } else {
             lp2B[rr] = v;
+            if (ROLES) st_sc1(hand_data(E, HK_PI, rbi) + R * A + rr, v);
           }
         }
       }
     }
+    if (ROLES) hand_publish(E, HK_PI, rbi, ep);  // a~' and log pi' -> target critics and critics
     __syncthreads();
     STAMP(6);
   }
 
   // ---- target twin-Q (agent.py:195-211)
   const float alpha32 = (float)*GPC(double, E.alpha_state + 1);
-  for (int t = 0; t < 2; ++t) {
-    const NetDev& q = E.net[NET_Q1T + t];
-    const int Kp0 = q.l[0].Kp;
-    for (int i = tid; i < R * Kp0; i += SAC_THREADS) {
-      const int r = i / Kp0, k = i % Kp0;
-      Xb[r * ld + k] = k < O ? s2B[r * O + k] : (k < O + A ? a2B[r * A + (k - O)] : 0.f);
+  if (!ROLES || role == 1 || role == 2) {
+    if (ROLES) {
+      hand_wait(E, HK_PI, rbi, ep);
+      const AS_G float* h = hand_data(E, HK_PI, rbi);
+      for (int i = tid; i < R * A; i += SAC_THREADS) a2B[i] = ld_sc1(h + i);
+      __syncthreads();
+    }
+    for (int t = ROLES ? role - 1 : 0; t < (ROLES ? role : 2); ++t) {
+      const NetDev& q = E.net[NET_Q1T + t];
+      const int Kp0 = q.l[0].Kp;
+      for (int i = tid; i < R * Kp0; i += SAC_THREADS) {
+        const int r = i / Kp0, k = i % Kp0;
+        Xb[r * ld + k] = k < O ? s2B[r * O + k] : (k < O + A ? a2B[r * A + (k - O)] : 0.f);
+      }
+      __syncthreads();
+      mlp_forward<T, R>(q, Xb, Yb, ld, outP, outB, ldo, E.o_P1, E.ldp1, lds, false, false, Bp, r0, nvalid, pf,
+                        gw_fwd(E.net[t ? NET_Q1 : NET_Q2T].l[0]));
+      if (tid < R) {
+        qtB[t * R + tid] = outB[tid * ldo];
+        if (ROLES) st_sc1(hand_data(E, HK_T1 + t, rbi) + tid, outB[tid * ldo]);
+      }
+      __syncthreads();
+      STAMP(7 + t);
+    }
+    if (ROLES) hand_publish(E, HK_T1 + role - 1, rbi, ep);
+  }
+  auto compute_y = [&](bool write_stats) {
+    if (tid < R) {
+      const int b = r0 + tid;
+      const float mq = fmin_nan(qtB[tid], qtB[R + tid]);
+      const float y = rB[tid] + (E.gamma * (1.f - dB[tid])) * (mq - alpha32 * lp2B[tid]);
+      yB[tid] = y;
+      if (write_stats && b < B) stats[4 + b] = y;
     }
     __syncthreads();
-    mlp_forward<T, R>(q, Xb, Yb, ld, outP, outB, ldo, E.o_P1, E.ldp1, lds, false, false, Bp, r0, nvalid, pf,
-                      gw_fwd(E.net[t ? NET_Q1 : NET_Q2T].l[0]));
-    if (tid < R) qtB[t * R + tid] = outB[tid * ldo];
-    __syncthreads();
-    STAMP(7 + t);
-  }
-  if (tid < R) {
-    const int b = r0 + tid;
-    const float mq = fmin_nan(qtB[tid], qtB[R + tid]);
-    const float y = rB[tid] + (E.gamma * (1.f - dB[tid])) * (mq - alpha32 * lp2B[tid]);
-    yB[tid] = y;
-    if (b < B) stats[4 + b] = y;
-  }
-  __syncthreads();
+  };
+  if (!ROLES) compute_y(true);
 
   // ---- critics: forward, MSE, backward (agent.py:213-236)
-  for (int qi = 0; qi < 2; ++qi) {
-    const NetDev& q = E.net[NET_Q1 + qi];
-    const int Kp0 = q.l[0].Kp;
-    for (int i = tid; i < R * Kp0; i += SAC_THREADS) {
-      const int r = i / Kp0, k = i % Kp0;
-      Xb[r * ld + k] = k < O ? sB[r * O + k] : (k < O + A ? aB[r * A + (k - O)] : 0.f);
-    }
-    __syncthreads();
-    // the layer-0 input (s, a) is shared by Q1 and Q2: its X^T is stored once
-    if (qi == 0) store_T<T, R>(Xb, ld, Kp0, q.l[0].K, q.l[0].XT, Bp, r0, nvalid, nullptr);
-    lf* X = Xb;
-    lf* Y = Yb;
-    for (int l = 0; l < q.L; ++l) {
-      const LayerDev& Ly = q.l[l];
-      if (l > 0) store_T<T, R>(X, ld, Ly.Kp, Ly.K, Ly.XT, Bp, r0, nvalid, nullptr);
-      if (l == q.L - 1)
-        layer_fwd<T, R>(X, ld, Ly, q.P + Ly.b_off, q.out_act, outP, ldo, outB, ldo, nullptr, 0, pf, gw_bwd(Ly));
-      else
-        layer_fwd<T, R>(X, ld, Ly, q.P + Ly.b_off, q.hid_act, lds + E.o_P1[l], E.ldp1[l], Y, ld, nullptr, 0, pf,
-                        gw_fwd(q.l[l + 1]));
-      __syncthreads();
-      lf* t = X;
-      X = Y;
-      Y = t;
-    }
-    STAMP(10 + 2 * qi);
-    if (tid < 64) {  // wave 0: loss partial + dL/dq (mse_loss backward: 2(q-y)/B)
-      float sq = 0.f;
-      if (tid < R) {
-        const bool v = tid < nvalid;
-        const float d = outB[tid * ldo] - yB[tid];
-        sq = v ? d * d : 0.f;
-        float g = v ? (2.0f / (float)B) * d : 0.f;
-        if (q.out_act != ACT_ID) g = act_bwd(q.out_act, outP[tid * ldo], g);
-        for (int n = 0; n < 32; ++n) gqB[tid * ldo + n] = n == 0 ? g : 0.f;
+  if (!ROLES || role >= 3) {
+    for (int qi = ROLES ? role - 3 : 0; qi < (ROLES ? role - 2 : 2); ++qi) {
+      const NetDev& q = E.net[NET_Q1 + qi];
+      const int Kp0 = q.l[0].Kp;
+      for (int i = tid; i < R * Kp0; i += SAC_THREADS) {
+        const int r = i / Kp0, k = i % Kp0;
+        Xb[r * ld + k] = k < O ? sB[r * O + k] : (k < O + A ? aB[r * A + (k - O)] : 0.f);
       }
-      sq = wave_sum(sq);
-      if (tid == 0) GP(float, E.lossp)[rbi * 4 + qi] = sq;
+      __syncthreads();
+      // the layer-0 input (s, a) is shared by Q1 and Q2: its X^T is stored once
+      if (qi == 0) store_T<T, R>(Xb, ld, Kp0, q.l[0].K, q.l[0].XT, Bp, r0, nvalid, nullptr);
+      lf* X = Xb;
+      lf* Y = Yb;
+      for (int l = 0; l < q.L; ++l) {
+        const LayerDev& Ly = q.l[l];
+        if (l > 0) store_T<T, R>(X, ld, Ly.Kp, Ly.K, Ly.XT, Bp, r0, nvalid, nullptr);
+        if (l == q.L - 1)
+          layer_fwd<T, R>(X, ld, Ly, q.P + Ly.b_off, q.out_act, outP, ldo, outB, ldo, nullptr, 0, pf, gw_bwd(Ly));
+        else
+          layer_fwd<T, R>(X, ld, Ly, q.P + Ly.b_off, q.hid_act, lds + E.o_P1[l], E.ldp1[l], Y, ld, nullptr, 0, pf,
+                          gw_fwd(q.l[l + 1]));
+        __syncthreads();
+        lf* t = X;
+        X = Y;
+        Y = t;
+      }
+      STAMP(10 + 2 * qi);
+      if (ROLES) {  // y needs both target critics and log pi' (the forward above did not)
+        hand_wait(E, HK_T1, rbi, ep);
+        hand_wait(E, HK_T2, rbi, ep);
+        hand_wait(E, HK_PI, rbi, ep);
+        if (tid < R) {
+          qtB[tid] = ld_sc1(hand_data(E, HK_T1, rbi) + tid);
+          qtB[R + tid] = ld_sc1(hand_data(E, HK_T2, rbi) + tid);
+          lp2B[tid] = ld_sc1(hand_data(E, HK_PI, rbi) + R * A + tid);
+        }
+        __syncthreads();
+        compute_y(qi == 0);
+      }
+      if (tid < 64) {  // wave 0: loss partial + dL/dq (mse_loss backward: 2(q-y)/B)
+        float sq = 0.f;
+        if (tid < R) {
+          const bool v = tid < nvalid;
+          const float d = outB[tid * ldo] - yB[tid];
+          sq = v ? d * d : 0.f;
+          float g = v ? (2.0f / (float)B) * d : 0.f;
+          if (q.out_act != ACT_ID) g = act_bwd(q.out_act, outP[tid * ldo], g);
+          for (int n = 0; n < 32; ++n) gqB[tid * ldo + n] = n == 0 ? g : 0.f;
+        }
+        sq = wave_sum(sq);
+        if (tid == 0) GP(float, E.lossp)[rbi * 4 + qi] = sq;
+      }
+      __syncthreads();
+      mlp_backward<T, R>(q, gqB, ldo, Xb, Yb, ld, E.o_P1, E.ldp1, lds, true, Bp, r0, nvalid, pf,
+                         qi == 0 ? gw_fwd(E.net[NET_Q2].l[0]) : gw_none());
+      STAMP(11 + 2 * qi);
     }
-    __syncthreads();
-    mlp_backward<T, R>(q, gqB, ldo, Xb, Yb, ld, E.o_P1, E.ldp1, lds, true, Bp, r0, nvalid, pf,
-                       qi == 0 ? gw_fwd(E.net[NET_Q2].l[0]) : gw_none());
-    STAMP(11 + 2 * qi);
   }
 }
 
 // ============================================================================ phase C
 // critics on (s, a~) with the updated weights, d a~, head backward, pi backward.
-template <typename T>
+// ROLES: block = role * nrt + row tile; role 0 pi (head + pi backward), 1/2 critics.
+// A critic role back-propagates a UNIT seed (d Q_i / d a~) and hands (q_i,
+// dQ_i/da~) to the pi role, which applies the min-Q weights -1/B, -1/2B or 0
+// (powers of two for power-of-two batches: bit-identical to seeding them).
+template <typename T, bool ROLES>
 __global__ void __launch_bounds__(SAC_THREADS) sac_actor(const EngineDev* __restrict__ Ep) {
   PREFETCH_ARG(Ep);
   const EngineDev& E = *Ep;
@@ -735,11 +834,21 @@ __global__ void __launch_bounds__(SAC_THREADS) sac_actor(const EngineDev* __rest
   lf* lds = (lf*)lds_raw;
   constexpr int R = SAC_ROWS;
   const int tid = threadIdx.x;
-  if (blockIdx.x % E.xs) return;  // XCD placement: see EngineDev::xs
+  int rbi, role;
+  if (ROLES) {
+    rbi = blockIdx.x % E.nrt;
+    role = blockIdx.x / E.nrt;
+  } else {
+    if (blockIdx.x % E.xs) return;  // XCD placement: see EngineDev::xs
+    rbi = blockIdx.x / E.xs;
+    role = -1;
+  }
+  const bool do_pi = !ROLES || role == 0;
   STAMP(32);
   const int B = E.B, Bp = E.Bp, O = E.O, A = E.A, ld = E.ld, ldo = E.ldo;
-  const int rbi = blockIdx.x / E.xs, r0 = rbi * R;
+  const int r0 = rbi * R;
   const int nvalid = min(R, B - r0);
+  const uint32_t ep = ROLES ? *GPC(uint32_t, E.sync) + 1u : 0u;
   lf* Xb = lds + E.o_X;
   lf* Yb = lds + E.o_Y;
   lf* sB = lds + E.o_s;
@@ -758,66 +867,87 @@ __global__ void __launch_bounds__(SAC_THREADS) sac_actor(const EngineDev* __rest
   Pf<T> pf;
   pf_issue<T>(pf, gw_fwd(E.net[NET_Q1].l[0]));
 
-  for (int i = tid; i < R * O; i += SAC_THREADS) sB[i] = GPC(float, E.s_st)[(size_t)r0 * O + i];
-  for (int i = tid; i < R * A; i += SAC_THREADS) {
-    aB[i] = GPC(float, E.a_st)[(size_t)r0 * A + i];
-    gaB[i] = 0.f;
+  if (!ROLES || role >= 1) {
+    for (int i = tid; i < R * O; i += SAC_THREADS) sB[i] = GPC(float, E.s_st)[(size_t)r0 * O + i];
+    for (int i = tid; i < R * A; i += SAC_THREADS) aB[i] = GPC(float, E.a_st)[(size_t)r0 * A + i];
   }
-  if (tid < R) lpB[tid] = GPC(float, E.lp_st)[r0 + tid];
-  __syncthreads();
-
-  // ---- Q1, Q2 on (s, a~) with the updated critics (agent.py:244-248)
-  for (int qi = 0; qi < 2; ++qi) {
-    const NetDev& q = E.net[NET_Q1 + qi];
-    const int Kp0 = q.l[0].Kp;
-    for (int i = tid; i < R * Kp0; i += SAC_THREADS) {
-      const int r = i / Kp0, k = i % Kp0;
-      Xb[r * ld + k] = k < O ? sB[r * O + k] : (k < O + A ? aB[r * A + (k - O)] : 0.f);
-    }
-    __syncthreads();
-    mlp_forward<T, R>(q, Xb, Yb, ld, qi ? outP2 : outP1, qi ? out2 : out1, ldo, qi ? E.o_P2 : E.o_P1,
-                      qi ? E.ldp2 : E.ldp1, lds, true, false, Bp, r0, nvalid, pf,
-                      qi ? gw_bwd(E.net[NET_Q1].l[E.net[NET_Q1].L - 1]) : gw_fwd(E.net[NET_Q2].l[0]));
-    STAMP(36 + qi);
-  }
-  // ---- L_pi = mean(alpha logpi - min Q) (agent.py:251-252); min backward splits ties
-  if (tid < 64) {
-    float term = 0.f;
-    if (tid < R) {
-      const bool v = tid < nvalid;
-      const float q1 = out1[tid * ldo], q2 = out2[tid * ldo];
-      const float m = fmin_nan(q1, q2);
-      term = v ? alpha32 * lpB[tid] - m : 0.f;
-      const float gm = v ? -1.0f / (float)B : 0.f;
-      float g1 = (q1 == q2) ? gm * 0.5f : (q1 > q2 ? 0.f : gm);
-      float g2 = (q1 == q2) ? gm * 0.5f : (q1 < q2 ? 0.f : gm);
-      if (E.net[NET_Q1].out_act != ACT_ID) {
-        g1 = act_bwd(E.net[NET_Q1].out_act, outP1[tid * ldo], g1);
-        g2 = act_bwd(E.net[NET_Q2].out_act, outP2[tid * ldo], g2);
-      }
-      for (int n = 0; n < 32; ++n) {
-        g1B[tid * ldo + n] = n == 0 ? g1 : 0.f;
-        g2B[tid * ldo + n] = n == 0 ? g2 : 0.f;
-      }
-    }
-    term = wave_sum(term);
-    if (tid == 0) GP(float, E.lossp)[rbi * 4 + 2] = term;
+  if (do_pi) {
+    for (int i = tid; i < R * A; i += SAC_THREADS) gaB[i] = 0.f;
+    if (tid < R) lpB[tid] = GPC(float, E.lp_st)[r0 + tid];
   }
   __syncthreads();
 
-  // ---- d a~ through both critics: dX of layer 0, action columns
-  for (int qi = 0; qi < 2; ++qi) {
-    const NetDev& q = E.net[NET_Q1 + qi];
-    lf* G0 = mlp_backward<T, R>(q, qi ? g2B : g1B, ldo, Xb, Yb, ld, qi ? E.o_P2 : E.o_P1, qi ? E.ldp2 : E.ldp1, lds,
-                                false, Bp, r0, nvalid, pf, gw_bwd(q.l[0]));
-    lf* Gx = (G0 == Xb) ? Yb : Xb;
-    layer_bwd<T, R>(G0, ld, q.l[0], nullptr, 0, -1, Gx, ld, pf,
-                    qi ? gw_bwd(pi.l[pi.L - 1]) : gw_bwd(E.net[NET_Q2].l[E.net[NET_Q2].L - 1]));
+  if (!ROLES || role >= 1) {
+    const int q_lo = ROLES ? role - 1 : 0, q_hi = ROLES ? role : 2;
+    // ---- Q1, Q2 on (s, a~) with the updated critics (agent.py:244-248)
+    for (int qi = q_lo; qi < q_hi; ++qi) {
+      const NetDev& q = E.net[NET_Q1 + qi];
+      const int Kp0 = q.l[0].Kp;
+      for (int i = tid; i < R * Kp0; i += SAC_THREADS) {
+        const int r = i / Kp0, k = i % Kp0;
+        Xb[r * ld + k] = k < O ? sB[r * O + k] : (k < O + A ? aB[r * A + (k - O)] : 0.f);
+      }
+      __syncthreads();
+      mlp_forward<T, R>(q, Xb, Yb, ld, qi ? outP2 : outP1, qi ? out2 : out1, ldo, qi ? E.o_P2 : E.o_P1,
+                        qi ? E.ldp2 : E.ldp1, lds, true, false, Bp, r0, nvalid, pf,
+                        qi ? gw_bwd(E.net[NET_Q1].l[E.net[NET_Q1].L - 1]) : gw_fwd(E.net[NET_Q2].l[0]));
+      STAMP(36 + qi);
+    }
+    // ---- backward seeds.  L_pi = mean(alpha logpi - min Q) (agent.py:251-252); min
+    // backward splits ties.  ROLES: unit seeds, the pi role applies the weights.
+    if (tid < 64) {
+      float term = 0.f;
+      if (tid < R) {
+        const bool v = tid < nvalid;
+        float g1, g2;
+        if (ROLES) {
+          g1 = g2 = v ? 1.0f : 0.f;
+        } else {
+          const float q1 = out1[tid * ldo], q2 = out2[tid * ldo];
+          const float m = fmin_nan(q1, q2);
+          term = v ? alpha32 * lpB[tid] - m : 0.f;
+          const float gm = v ? -1.0f / (float)B : 0.f;
+          g1 = (q1 == q2) ? gm * 0.5f : (q1 > q2 ? 0.f : gm);
+          g2 = (q1 == q2) ? gm * 0.5f : (q1 < q2 ? 0.f : gm);
+        }
+        if (E.net[NET_Q1].out_act != ACT_ID) {
+          if (q_lo == 0) g1 = act_bwd(E.net[NET_Q1].out_act, outP1[tid * ldo], g1);
+          if (q_hi == 2) g2 = act_bwd(E.net[NET_Q2].out_act, outP2[tid * ldo], g2);
+        }
+        for (int n = 0; n < 32; ++n) {
+          g1B[tid * ldo + n] = n == 0 ? g1 : 0.f;
+          g2B[tid * ldo + n] = n == 0 ? g2 : 0.f;
+        }
+      }
+      if (!ROLES) {
+        term = wave_sum(term);
+        if (tid == 0) GP(float, E.lossp)[rbi * 4 + 2] = term;
+      }
+    }
     __syncthreads();
-    for (int i = tid; i < R * A; i += SAC_THREADS) gaB[i] += Gx[(i / A) * ld + O + i % A];
-    __syncthreads();
-    STAMP(38 + qi);
+
+    // ---- d a~ through the critics: dX of layer 0, action columns
+    for (int qi = q_lo; qi < q_hi; ++qi) {
+      const NetDev& q = E.net[NET_Q1 + qi];
+      lf* G0 = mlp_backward<T, R>(q, qi ? g2B : g1B, ldo, Xb, Yb, ld, qi ? E.o_P2 : E.o_P1, qi ? E.ldp2 : E.ldp1,
+                                  lds, false, Bp, r0, nvalid, pf, gw_bwd(q.l[0]));
+      lf* Gx = (G0 == Xb) ? Yb : Xb;
+      layer_bwd<T, R>(G0, ld, q.l[0], nullptr, 0, -1, Gx, ld, pf,
+                      qi ? gw_bwd(pi.l[pi.L - 1]) : gw_bwd(E.net[NET_Q2].l[E.net[NET_Q2].L - 1]));
+      __syncthreads();
+      if (ROLES) {
+        AS_G float* h = hand_data(E, HK_C1 + qi, rbi);
+        for (int i = tid; i < R * A; i += SAC_THREADS) st_sc1(h + i, Gx[(i / A) * ld + O + i % A]);
+        if (tid < R) st_sc1(h + R * A + tid, (qi ? out2 : out1)[tid * ldo]);
+        hand_publish(E, HK_C1 + qi, rbi, ep);
+      } else {
+        for (int i = tid; i < R * A; i += SAC_THREADS) gaB[i] += Gx[(i / A) * ld + O + i % A];
+        __syncthreads();
+      }
+      STAMP(38 + qi);
+    }
   }
+  if (!do_pi) return;
 
   // ---- squashed-Gaussian head backward + pi backward (agent.py:255-257)
   for (int l = 0; l < pi.L - 1; ++l) {
@@ -826,6 +956,33 @@ __global__ void __launch_bounds__(SAC_THREADS) sac_actor(const EngineDev* __rest
     lf* P = lds + E.o_P1[l];
     const AS_G float* ps = GPC(float, Ly.pstash) + (size_t)r0 * Ly.Np;
     for (int i = tid; i < R * Ly.Np; i += SAC_THREADS) P[(i / Ly.Np) * ldp + i % Ly.Np] = ps[i];
+  }
+  if (ROLES) {  // combine the critics' unit-seed gradients with the min-Q weights
+    hand_wait(E, HK_C1, rbi, ep);
+    hand_wait(E, HK_C2, rbi, ep);
+    const AS_G float* h1 = hand_data(E, HK_C1, rbi);
+    const AS_G float* h2 = hand_data(E, HK_C2, rbi);
+    if (tid < 64) {
+      float term = 0.f;
+      if (tid < R) {
+        const bool v = tid < nvalid;
+        const float q1 = ld_sc1(h1 + R * A + tid), q2 = ld_sc1(h2 + R * A + tid);
+        const float m = fmin_nan(q1, q2);
+        term = v ? alpha32 * lpB[tid] - m : 0.f;
+        const float gm = v ? -1.0f / (float)B : 0.f;
+        g1B[tid] = (q1 == q2) ? gm * 0.5f : (q1 > q2 ? 0.f : gm);
+        g2B[tid] = (q1 == q2) ? gm * 0.5f : (q1 < q2 ? 0.f : gm);
+      }
+      term = wave_sum(term);
+      if (tid == 0) GP(float, E.lossp)[rbi * 4 + 2] = term;
+    }
+    __syncthreads();
+    for (int i = tid; i < R * A; i += SAC_THREADS) {
+      const int r = i / A;
+      gaB[i] = (gaB[i] + g1B[r] * ld_sc1(h1 + i)) + g2B[r] * ld_sc1(h2 + i);
+    }
+    __syncthreads();
+    STAMP(39);
   }
   for (int i = tid; i < R * A; i += SAC_THREADS) {  // one lane per (row, action dim)
     const int r = i / A, j = i % A, b = r0 + r;
@@ -1043,6 +1200,7 @@ __device__ __forceinline__ void alpha_and_losses(const EngineDev& E) {
       stats[3] = __builtin_nanf("");
     }
     *GP(uint64_t, E.rng_step) += 1;
+    *GP(uint32_t, E.sync) += 1u;  // next launch epoch of the role hand-offs
   }
 }
 

@@ -128,6 +128,8 @@ class SacEngine:
         E.check(self.lib.sac_engine_create(ctypes.byref(cfg), ctypes.byref(bufs), self._stream(), ctypes.byref(h)))
         self.handle = h
         self.steps_done = 0
+        self.lib.sac_engine_uses_roles.argtypes = [ctypes.c_void_p]
+        self.roles = bool(self.lib.sac_engine_uses_roles(h))
 
     # ------------------------------------------------------------------ plumbing
     def _stream(self):
@@ -218,6 +220,10 @@ class SacEngine:
         return list(out)
 
     # ------------------------------------------------------------------ readback (syncs)
+    def check(self) -> None:
+        """Raise EngineError if an in-launch hand-off of the phase kernels timed out."""
+        E.check(self.lib.sac_engine_check(self.handle, self._stream()))
+
     def losses(self) -> List[float]:
         """[L_Q1, L_Q2, L_pi, L_alpha] of the last step (NaN L_alpha when fixed)."""
         return self.stats[:4].double().cpu().tolist()

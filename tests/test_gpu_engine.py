@@ -140,6 +140,7 @@ def test_graph_replay_equals_direct_launches(precision):
     for k, v in eng.state_tensors().items():
         assert torch.equal(v, a[k]), k
     assert int(eng.rng_step.item()) == 40
+    eng.check()
     assert eng.opt_steps.cpu().tolist()[:3] == [40.0, 40.0, 40.0]
 
 
@@ -151,6 +152,7 @@ def test_c2_full_size_many_steps_properties():
     q1t0 = eng.flat["q1t"].clone()
     eng.train_graph(rb, 300, chunk=50)
     torch.cuda.synchronize()
+    eng.check()
     losses = eng.losses()
     assert all(np.isfinite(losses)), losses
     assert int(eng.rng_step.item()) == 300
@@ -220,3 +222,32 @@ def test_save_load_roundtrip_continues_identically(tmp_path):
     other.engine.train(other.replay_buffer, 1, indices=idx, eps=e)
     assert torch.equal(agent.engine.flat["pi"], other.engine.flat["pi"])
     assert torch.equal(agent.engine.stats[:4], other.engine.stats[:4])
+
+
+# ---------------------------------------------------------------- role-split vs fused phase kernels
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_role_split_equals_fused(precision, monkeypatch):
+    """Phases A/C split into per-network workgroups with in-launch hand-offs give
+    the same bits as the one-workgroup-per-row-tile kernels (power-of-two batch:
+    the min-Q weights are applied after a unit-seed backward, exactly)."""
+    out = {}
+    for roles in ("1", "0"):
+        monkeypatch.setenv("SAC_ROLES", roles)
+        eng, rb, c = _engine("c2", precision, capacity=5000)
+        assert bool(eng.roles) == (roles == "1")
+        eng.train(rb, 4)
+        eng.train_graph(rb, 6, chunk=3)
+        eng.check()
+        out[roles] = {k: v.clone() for k, v in eng.state_tensors().items()}
+        out[roles]["stats"] = eng.stats.clone()
+    for k in out["1"]:
+        assert torch.equal(out["1"][k], out["0"][k]), k
+
+
+def test_large_batch_uses_fused_kernels_and_runs():
+    """C3 (B=4096): 256 row tiles do not fit the role split; the fused kernels run."""
+    eng, rb, c = _engine("c3", "bf16", capacity=20_000)
+    assert not eng.roles
+    eng.train_graph(rb, 20, chunk=10)
+    eng.check()
+    assert all(np.isfinite(eng.losses()))

@@ -22,7 +22,7 @@ eng, rb, c = bench.build_engine(cfg, prec, 0, dev)
 lib = E.load_library()
 lib.sac_engine_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
 assert lib.sac_engine_debug_stamped() == 1, "not the stamps build"
-nblk = (c["batch"] + 15) // 16
+nblk = 8 * ((c["batch"] + 15) // 16)  # covers xs-spread and role-split grids
 buf = torch.zeros(nblk * 64, dtype=torch.int64, device=dev)
 E.check(lib.sac_engine_debug_stamps(eng.handle, E.ptr(buf), eng._stream()))
 eng.train(rb, 20)
@@ -38,12 +38,14 @@ names = {0: "A start", 1: "gather+eps", 2: "pi L0", 3: "pi L1", 4: "pi L2", 5: "
          7: "Qt1", 8: "Qt2", 10: "Q1 fwd", 11: "Q1 bwd", 12: "Q2 fwd", 13: "Q2 bwd",
          32: "C start", 36: "Q1 fwd", 37: "Q2 fwd", 38: "Q1 bwd->da", 39: "Q2 bwd->da", 35: "pi bwd"}
 for base, last in ((0, 13), (32, 39)):
-    idx = [i for i in range(base, last + 1) if i in names and st[:, i].min() > 0]
-    idx.sort(key=lambda i: np.median(st[:, i]))
+    live = st[:, base] > 0  # blocks that ran this phase
+    idx = [i for i in range(base, last + 1) if i in names and (st[live, i] > 0).any()]
+    idx.sort(key=lambda i: np.median(st[live & (st[:, i] > 0), i] - st[live & (st[:, i] > 0), base]))
     prev = None
     print(f"--- phase {'A' if base == 0 else 'C'} (cycles, median over blocks)")
     for i in idx:
-        t = np.median(st[:, i] - st[:, idx[0]])
+        m = live & (st[:, i] > 0)
+        t = np.median(st[m, i] - st[m, base])
         if prev is not None:
             print(f"  {names[i]:12s} +{t - prev:9.0f}   (cum {t:9.0f})")
         prev = t
