@@ -308,8 +308,8 @@ static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
       while (xs < 8 && nrt * xs * 2 <= 256) xs *= 2;
       if (const char* v = getenv("SAC_XS")) xs = std::max(1, atoi(v));
       h.xs = xs;
-      // role split of phases A/C: 5 * nrt workgroups must be co-resident (one per CU)
-      int roles = 5 * nrt <= 256 && SAC_ROWS * (A + 1) <= SAC_HAND_STRIDE;
+      // role split of phases A/C: 6 * nrt workgroups must be co-resident (one per CU)
+      int roles = 6 * nrt <= 256 && SAC_ROWS * (A + 1) <= SAC_HAND_STRIDE;
       if (const char* v = getenv("SAC_ROLES")) roles = roles && atoi(v) != 0;
       h.roles = roles;
     }
@@ -407,7 +407,7 @@ static void launch_phase(sac_engine* e, int phase, const sac_replay* rb, const i
   switch (phase) {
     case 0:
       if (e->h.roles)
-        sac_target_critic<T, true><<<e->nrt * 5, SAC_THREADS, e->lds_bytes, s>>>(e->d, *rb, idx, eps);
+        sac_target_critic<T, true><<<e->nrt * 6, SAC_THREADS, e->lds_bytes, s>>>(e->d, *rb, idx, eps);
       else
         sac_target_critic<T, false><<<e->nrt * e->h.xs, SAC_THREADS, e->lds_bytes, s>>>(e->d, *rb, idx, eps);
       break;

@@ -1,6 +1,8 @@
 // sac_phases.h — device state and the four phase kernels of one SAC gradient step.
 // Included by sac_engine.hip only.  Reference cross-walk in sac_engine.hip.
 #pragma once
+#include <type_traits>
+
 #include "sac_device.h"
 
 #define SAC_DEV_LAYERS 6  // Linear layers per network supported by the kernels
@@ -509,7 +511,8 @@ __device__ __forceinline__ void hand_wait(const EngineDev& E, int kind, int rbi,
 
 // ============================================================================ phase A
 // sample + gather, pi on [s'; s], target twin-Q -> y, critics forward + backward.
-// ROLES: block = role * nrt + row tile; role 0 pi, 1/2 target critics, 3/4 critics.
+// ROLES: block = role * nrt + row tile; role 0 pi on s' (target sample), 1/2
+// target critics, 3/4 critics, 5 pi on s (actor sample, stashed for phase C).
 template <typename T, bool ROLES>
 __global__ void __launch_bounds__(SAC_THREADS) sac_target_critic(const EngineDev* __restrict__ Ep, sac_replay rb,
                                                                   const int32_t* __restrict__ inj_idx_,
@@ -529,7 +532,7 @@ __global__ void __launch_bounds__(SAC_THREADS) sac_target_critic(const EngineDev
     rbi = blockIdx.x / E.xs;
     role = -1;
   }
-  const bool do_pi = !ROLES || role == 0;
+  const bool do_pi = !ROLES || role == 0 || role == 5;
   STAMP(0);
   const int B = E.B, Bp = E.Bp, O = E.O, A = E.A, ld = E.ld, ldo = E.ldo;
   const int r0 = rbi * R;
@@ -566,7 +569,7 @@ __global__ void __launch_bounds__(SAC_THREADS) sac_target_critic(const EngineDev
 
   // optimizer step counters and this step's Adam bias-correction scalars
   // (torch adam.py: step_size = lr / (1 - beta1^t), bias_correction2_sqrt), once per step
-  if (do_pi && rbi == 0 && tid < 4 && (tid < 3 || E.auto_entropy)) {
+  if ((!ROLES || role == 0) && rbi == 0 && tid < 4 && (tid < 3 || E.auto_entropy)) {
     const double t = GP(double, E.opt_steps)[tid] + 1.0;
     GP(double, E.opt_steps)[tid] = t;
     if (tid < 3) {
@@ -611,10 +614,11 @@ __global__ void __launch_bounds__(SAC_THREADS) sac_target_critic(const EngineDev
     rB[tid] = sl >= 0 ? rrew[sl] : 0.f;
     dB[tid] = sl >= 0 ? rdone[sl] : 0.f;
   }
-  if (do_pi) {
+  if (do_pi) {  // which = 0: target draw (role 0), 1: actor draw (role 5)
     const int NP = (A + 1) / 2;
-    for (int i = tid; i < 2 * R * NP; i += SAC_THREADS) {
-      const int which = i / (R * NP), rem = i % (R * NP), r = rem / NP, p = rem % NP;
+    const int w_lo = ROLES ? (role == 5) : 0, w_n = ROLES ? 1 : 2;
+    for (int i = tid; i < w_n * R * NP; i += SAC_THREADS) {
+      const int which = w_lo + i / (R * NP), rem = i % (R * NP), r = rem / NP, p = rem % NP;
       const int b = r0 + r;
       float n0 = 0.f, n1 = 0.f;
       if (b < B) {
@@ -633,26 +637,32 @@ __global__ void __launch_bounds__(SAC_THREADS) sac_target_critic(const EngineDev
   __syncthreads();
   STAMP(1);
 
-  // ---- pi forward on [s' ; s] (2R rows): target sample + actor sample
-  if (do_pi) {
-    for (int i = tid; i < R * O; i += SAC_THREADS) GP(float, E.s_st)[(size_t)r0 * O + i] = sB[i];
+  // ---- pi forward: fused, one pass over [s' ; s] (2R rows: target sample, then
+  // actor sample); role split, role 0 runs the s' rows (on the critical path) and
+  // role 5 the s rows (stashed for phase C).
+  auto pi_forward_head = [&](auto rows_c, bool tgt, bool act) {
+    constexpr int ROWS = decltype(rows_c)::value;
+    const int a0 = tgt ? (act ? R : ROWS) : 0;  // first actor row
+    if (act)
+      for (int i = tid; i < R * O; i += SAC_THREADS) GP(float, E.s_st)[(size_t)r0 * O + i] = sB[i];
     const int Kp0 = pi.l[0].Kp;
-    for (int i = tid; i < 2 * R * Kp0; i += SAC_THREADS) {
+    for (int i = tid; i < ROWS * Kp0; i += SAC_THREADS) {
       const int r = i / Kp0, k = i % Kp0;
-      Xb[r * ld + k] = k < O ? (r < R ? s2B[r * O + k] : sB[(r - R) * O + k]) : 0.f;
+      Xb[r * ld + k] = k < O ? (r < a0 ? s2B[r * O + k] : sB[(r - a0) * O + k]) : 0.f;
     }
     __syncthreads();
     lf* X = Xb;
     lf* Y = Yb;
     for (int l = 0; l < pi.L; ++l) {
       const LayerDev& Ly = pi.l[l];
-      store_T<T, R>(X + R * ld, ld, Ly.Kp, Ly.K, Ly.XT, Bp, r0, nvalid, nullptr);  // actor rows' input
+      if (act) store_T<T, R>(X + a0 * ld, ld, Ly.Kp, Ly.K, Ly.XT, Bp, r0, nvalid, nullptr);  // actor rows' input
+      float* stash = act ? Ly.pstash + (size_t)r0 * Ly.Np : nullptr;
       if (l == pi.L - 1)
-        layer_fwd<T, 2 * R>(X, ld, Ly, pi.P + Ly.b_off, pi.out_act, outP, ldo, outB, ldo,
-                            Ly.pstash + (size_t)r0 * Ly.Np, R, pf, gw_fwd(E.net[NET_Q1T].l[0]));
+        layer_fwd<T, ROWS>(X, ld, Ly, pi.P + Ly.b_off, pi.out_act, outP, ldo, outB, ldo, stash, a0, pf,
+                           gw_fwd(E.net[NET_Q1T].l[0]));
       else
-        layer_fwd<T, 2 * R>(X, ld, Ly, pi.P + Ly.b_off, pi.hid_act, nullptr, 0, Y, ld, Ly.pstash + (size_t)r0 * Ly.Np,
-                            R, pf, gw_fwd(pi.l[l + 1]));
+        layer_fwd<T, ROWS>(X, ld, Ly, pi.P + Ly.b_off, pi.hid_act, nullptr, 0, Y, ld, stash, a0, pf,
+                           gw_fwd(pi.l[l + 1]));
       __syncthreads();
       STAMP(2 + l);
       lf* t = X;
@@ -661,63 +671,62 @@ __global__ void __launch_bounds__(SAC_THREADS) sac_target_critic(const EngineDev
     }
     // squashed-Gaussian head (models.py:79-87): one lane per (row, action dim),
     // each row's A lanes contiguous inside one wave (AP = pow2 >= A), summed by shuffles
-    {
-      const int AP = A <= 1 ? 1 : 1 << (32 - __builtin_clz(A - 1));
-      const int rows_per_pass = SAC_THREADS / AP;
-      for (int base = 0; base < 2 * R; base += rows_per_pass) {
-        const int r = base + tid / AP, j = tid % AP;
-        const bool live = r < 2 * R && j < A;
-        float lp = 0.f, corr = 0.f;
-        if (live) {
-          const bool actor = r >= R;
-          const int rr = actor ? r - R : r;
-          const int b = r0 + rr;
-          const lf* o = outB + r * ldo;
-          const float mu = o[j], lsr = o[A + j], e = (actor ? eaB : etB)[rr * A + j];
-          const float lo = E.ls_min, hi = E.ls_max;
-          const float ls = lsr < lo ? lo : (lsr > hi ? hi : lsr);
-          const float sd = expf(ls);
-          const float z = mu + e * sd;
-          const float act = tanhf(z) * E.scale;
-          const float diff = z - mu;
-          const float var = sd * sd;
-          lp = -(diff * diff) / (2.f * var) - logf(sd) - HALF_LOG_2PI;
-          corr = 2.f * ((LOG2F - z) - softplus20(-2.f * z));
-          if (actor) {
-            AS_G float* h = GP(float, E.head_st) + (size_t)b * 4 * A;
-            h[j] = mu;
-            h[A + j] = lsr;
-            h[2 * A + j] = z;
-            h[3 * A + j] = e;
-            GP(float, E.a_st)[(size_t)b * A + j] = act;
-          } else {
-            a2B[rr * A + j] = act;
-            if (ROLES) st_sc1(hand_data(E, HK_PI, rbi) + rr * A + j, act);
-          }
+    const int AP = A <= 1 ? 1 : 1 << (32 - __builtin_clz(A - 1));
+    const int rows_per_pass = SAC_THREADS / AP;
+    for (int base = 0; base < ROWS; base += rows_per_pass) {
+      const int r = base + tid / AP, j = tid % AP;
+      const bool live = r < ROWS && j < A;
+      const bool actor = r >= a0;
+      const int rr = actor ? r - a0 : r;
+      const int b = r0 + rr;
+      float lp = 0.f, corr = 0.f;
+      if (live) {
+        const lf* o = outB + r * ldo;
+        const float mu = o[j], lsr = o[A + j], e = (actor ? eaB : etB)[rr * A + j];
+        const float lo = E.ls_min, hi = E.ls_max;
+        const float ls = lsr < lo ? lo : (lsr > hi ? hi : lsr);
+        const float sd = expf(ls);
+        const float z = mu + e * sd;
+        const float act_v = tanhf(z) * E.scale;
+        const float diff = z - mu;
+        const float var = sd * sd;
+        lp = -(diff * diff) / (2.f * var) - logf(sd) - HALF_LOG_2PI;
+        corr = 2.f * ((LOG2F - z) - softplus20(-2.f * z));
+        if (actor) {
+          AS_G float* h = GP(float, E.head_st) + (size_t)b * 4 * A;
+          h[j] = mu;
+          h[A + j] = lsr;
+          h[2 * A + j] = z;
+          h[3 * A + j] = e;
+          GP(float, E.a_st)[(size_t)b * A + j] = act_v;
+        } else {
+          a2B[rr * A + j] = act_v;
+          if (ROLES) st_sc1(hand_data(E, HK_PI, rbi) + rr * A + j, act_v);
         }
-        for (int o = 1; o < AP; o <<= 1) {
-          lp += __shfl_xor(lp, o, 64);
-          corr += __shfl_xor(corr, o, 64);
-        }
-        if (live && j == 0) {
-          const bool actor = r >= R;
-          const int rr = actor ? r - R : r;
-          const int b = r0 + rr;
-          const float v = lp - corr;
-          if (actor) {
-            GP(float, E.lp_st)[b] = v;
-            if (b < B) stats[4 + B + b] = v;
-          } else {
-            lp2B[rr] = v;
-            if (ROLES) st_sc1(hand_data(E, HK_PI, rbi) + R * A + rr, v);
-          }
+      }
+      for (int o = 1; o < AP; o <<= 1) {
+        lp += __shfl_xor(lp, o, 64);
+        corr += __shfl_xor(corr, o, 64);
+      }
+      if (live && j == 0) {
+        const float v = lp - corr;
+        if (actor) {
+          GP(float, E.lp_st)[b] = v;
+          if (b < B) stats[4 + B + b] = v;
+        } else {
+          lp2B[rr] = v;
+          if (ROLES) st_sc1(hand_data(E, HK_PI, rbi) + R * A + rr, v);
         }
       }
     }
-    if (ROLES) hand_publish(E, HK_PI, rbi, ep);  // a~' and log pi' -> target critics and critics
+    if (ROLES && tgt) hand_publish(E, HK_PI, rbi, ep);  // a~' and log pi' -> target critics and critics
     __syncthreads();
     STAMP(6);
-  }
+  };
+  if (!ROLES)
+    pi_forward_head(std::integral_constant<int, 2 * R>(), true, true);
+  else if (role == 0 || role == 5)
+    pi_forward_head(std::integral_constant<int, R>(), role == 0, role == 5);
 
   // ---- target twin-Q (agent.py:195-211)
   const float alpha32 = (float)*GPC(double, E.alpha_state + 1);
@@ -760,7 +769,7 @@ __global__ void __launch_bounds__(SAC_THREADS) sac_target_critic(const EngineDev
   if (!ROLES) compute_y(true);
 
   // ---- critics: forward, MSE, backward (agent.py:213-236)
-  if (!ROLES || role >= 3) {
+  if (!ROLES || role == 3 || role == 4) {
     for (int qi = ROLES ? role - 3 : 0; qi < (ROLES ? role - 2 : 2); ++qi) {
       const NetDev& q = E.net[NET_Q1 + qi];
       const int Kp0 = q.l[0].Kp;
