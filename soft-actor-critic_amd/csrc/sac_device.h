@@ -18,6 +18,10 @@
 // lgkmcnt, so one flat LDS read waits for every outstanding weight load.
 #define AS_G __attribute__((address_space(1)))
 #define AS_L __attribute__((address_space(3)))
+// Constant address space: the engine descriptor is read-only for a kernel's
+// lifetime; loads through AS_C with uniform addresses become scalar (s_load)
+// loads through the scalar cache instead of vector loads + vmcnt waits.
+#define AS_C __attribute__((address_space(4)))
 typedef AS_L float lf;
 #define GP(T, p) ((AS_G T*)(p))
 #define GPC(T, p) ((const AS_G T*)(p))

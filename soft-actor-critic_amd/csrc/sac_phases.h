@@ -122,8 +122,8 @@ struct GemmW {
   int cols;       // reduction length (multiple of SAC_PAD)
   int NT;         // 16-row tiles of the packed matrix = output tiles of the step
 };
-__device__ __forceinline__ GemmW gw_fwd(const LayerDev& L) { return GemmW{L.Wc, L.Kp, L.Np >> 4}; }
-__device__ __forceinline__ GemmW gw_bwd(const LayerDev& L) { return GemmW{L.WTc, L.Np, L.Kp >> 4}; }
+__device__ __forceinline__ GemmW gw_fwd(const AS_C LayerDev& L) { return GemmW{L.Wc, L.Kp, L.Np >> 4}; }
+__device__ __forceinline__ GemmW gw_bwd(const AS_C LayerDev& L) { return GemmW{L.WTc, L.Np, L.Kp >> 4}; }
 __device__ __forceinline__ GemmW gw_none() { return GemmW{nullptr, 0, 0}; }
 
 #ifndef SAC_PF
@@ -308,7 +308,7 @@ __device__ __forceinline__ void act_pass_bwd(lf* G, int ldg, const lf* P, int ld
 // Forward: Y[r][n] = act(sum_k X[r][k] W[n][k] + b[n]) for n < Np (padded -> 0).
 // P (optional) keeps the pre-activation; Pg (optional) stashes rows >= pg_row0.
 template <typename T, int ROWS>
-__device__ __forceinline__ void layer_fwd(const lf* X, int ldx, const LayerDev& L, const float* bias_, int act, lf* P,
+__device__ __forceinline__ void layer_fwd(const lf* X, int ldx, const AS_C LayerDev& L, const float* bias_, int act, lf* P,
                                           int ldp, lf* Y, int ldy, float* Pg_, int pg_row0, Pf<T>& pf,
                                           const GemmW& next) {
   const AS_G float* bias = GPC(float, bias_);
@@ -339,7 +339,7 @@ __device__ __forceinline__ void layer_fwd(const lf* X, int ldx, const LayerDev& 
 
 // dX: Gout[r][k] = act'(Pprev[r][k]) * sum_n G[r][n] W[n][k]   (act_prev < 0: no act')
 template <typename T, int ROWS>
-__device__ __forceinline__ void layer_bwd(const lf* G, int ldg, const LayerDev& L, const lf* Pprev, int ldp,
+__device__ __forceinline__ void layer_bwd(const lf* G, int ldg, const AS_C LayerDev& L, const lf* Pprev, int ldp,
                                           int act_prev, lf* Gout, int ldo, Pf<T>& pf, const GemmW& next) {
   const int g = (threadIdx.x & 63) >> 4;
   const int K = L.K;
@@ -359,11 +359,13 @@ __device__ __forceinline__ void layer_bwd(const lf* G, int ldg, const LayerDev& 
     act_pass_bwd<ROWS>(Gout, ldo, Pprev, ldp, L.Kp >> 4, K, act_prev);
 }
 
-// dst[k][col0 + r] = src[r][k] (0 for k >= K or r >= nvalid), k < Kp; with
-// dbp != null also dbp[col0 / SAC_ROWS][k] = sum_{r<nvalid} src[r][k] (k < K).
+// dst[k][col0 + r] = x[r][k] (0 for k >= K or r >= nvalid), k < Kp, where
+// x[r][k] = src[r][k] * rowscale[r] (rowscale == null: 1); with dbp != null also
+// dbp[col0 / SAC_ROWS][k] = sum_{r<nvalid} x[r][k] (k < K).
 template <typename T, int ROWS>
 __device__ __forceinline__ void store_T(const lf* __restrict__ src, int lds_ld, int Kp, int K, void* dst_,
-                                                 int Bp, int col0, int nvalid, float* dbp_) {
+                                                 int Bp, int col0, int nvalid, float* dbp_,
+                                                 const lf* __restrict__ rowscale = nullptr) {
   AS_G T* dst = GP(T, dst_);
   AS_G float* dbp = GP(float, dbp_);
   constexpr int CH = ROWS / 8;
@@ -376,7 +378,8 @@ __device__ __forceinline__ void store_T(const lf* __restrict__ src, int lds_ld, 
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
       const int r = ch * 8 + q;
-      const float x = (live && r < nvalid && k < K) ? src[r * lds_ld + k] : 0.f;
+      float x = (live && r < nvalid && k < K) ? src[r * lds_ld + k] : 0.f;
+      if (rowscale) x = rowscale[r] * x;
       s += x;
       v[q] = MM<T>::cvt(x);
     }
@@ -402,13 +405,13 @@ __device__ __forceinline__ void store_T(const lf* __restrict__ src, int lds_ld, 
 // pre-activations into lds[o_P[l]] (stride ldp[l]).  storeXT: each layer's input
 // transposed into L.XT (ROWS must be SAC_ROWS).  after: the GEMM step that follows.
 template <typename T, int ROWS>
-__device__ __forceinline__ void mlp_forward(const NetDev& net, lf* Xb, lf* Yb, int ld, lf* Pout, lf* Yout, int ldo,
-                                            const int* o_P, const int* ldp, lf* lds, bool keepP, bool storeXT, int Bp,
+__device__ __forceinline__ void mlp_forward(const AS_C NetDev& net, lf* Xb, lf* Yb, int ld, lf* Pout, lf* Yout, int ldo,
+                                            const AS_C int* o_P, const AS_C int* ldp, lf* lds, bool keepP, bool storeXT, int Bp,
                                             int col0, int nvalid, Pf<T>& pf, const GemmW& after) {
   lf* X = Xb;
   lf* Y = Yb;
   for (int l = 0; l < net.L; ++l) {
-    const LayerDev& Ly = net.l[l];
+    const AS_C LayerDev& Ly = net.l[l];
     const bool out = l == net.L - 1;
     const GemmW next = out ? after : gw_fwd(net.l[l + 1]);
     if (storeXT) {
@@ -430,11 +433,11 @@ __device__ __forceinline__ void mlp_forward(const NetDev& net, lf* Xb, lf* Yb, i
 // pre-activation gradient.  storeGT: each layer's dY^T + bias partial sums.
 // Returns the buffer (stride ld) holding d(pre-act of layer 0).
 template <typename T, int ROWS>
-__device__ __forceinline__ lf* mlp_backward(const NetDev& net, const lf* Gout, int ldo, lf* Xb, lf* Yb, int ld,
-                                            const int* o_P, const int* ldp, lf* lds, bool storeGT, int Bp, int col0,
+__device__ __forceinline__ lf* mlp_backward(const AS_C NetDev& net, const lf* Gout, int ldo, lf* Xb, lf* Yb, int ld,
+                                            const AS_C int* o_P, const AS_C int* ldp, lf* lds, bool storeGT, int Bp, int col0,
                                             int nvalid, Pf<T>& pf, const GemmW& after) {
   const int Lh = net.L - 1;
-  const LayerDev& Lo = net.l[Lh];
+  const AS_C LayerDev& Lo = net.l[Lh];
   if (storeGT) store_T<T, ROWS>(Gout, ldo, Lo.Np, Lo.N, Lo.GT, Bp, col0, nvalid, Lo.dbp);
   layer_bwd<T, ROWS>(Gout, ldo, Lo, lds + o_P[Lh - 1], ldp[Lh - 1], net.hid_act, Yb, ld, pf,
                      Lh - 1 >= 1 ? gw_bwd(net.l[Lh - 1]) : after);
@@ -442,7 +445,7 @@ __device__ __forceinline__ lf* mlp_backward(const NetDev& net, const lf* Gout, i
   lf* G = Yb;
   lf* Gn = Xb;
   for (int l = Lh - 1; l >= 0; --l) {
-    const LayerDev& Ly = net.l[l];
+    const AS_C LayerDev& Ly = net.l[l];
     if (storeGT) store_T<T, ROWS>(G, ld, Ly.Np, Ly.N, Ly.GT, Bp, col0, nvalid, Ly.dbp);
     if (l == 0) break;
     layer_bwd<T, ROWS>(G, ld, Ly, lds + o_P[l - 1], ldp[l - 1], net.hid_act, Gn, ld, pf,
@@ -461,6 +464,24 @@ __device__ __forceinline__ lf* mlp_backward(const NetDev& net, const lf* Gout, i
 
 __device__ __forceinline__ float fmin_nan(float a, float b) { return (a != a) ? a : (a < b ? a : b); }
 
+// Unit-seed backward of a critic (phase A): Gout [R][ldo] holds d(out pre-act)
+// for a seed of 1 per row; writes U_l = d(pre-act of hidden layer l) for every
+// hidden layer into lds + E.o_P2[l] (stride E.ldp2[l]).  Pre-activations are in
+// the E.o_P1 buffers (critic forward with keepP).
+template <typename T, int ROWS>
+__device__ __forceinline__ void critic_unit_backward(const AS_C EngineDev& E, const AS_C NetDev& net, const lf* Gout, int ldo,
+                                                     lf* lds, Pf<T>& pf) {
+  const int Lh = net.L - 1;
+  layer_bwd<T, ROWS>(Gout, ldo, net.l[Lh], lds + E.o_P1[Lh - 1], E.ldp1[Lh - 1], net.hid_act, lds + E.o_P2[Lh - 1],
+                     E.ldp2[Lh - 1], pf, Lh - 1 >= 1 ? gw_bwd(net.l[Lh - 1]) : gw_none());
+  __syncthreads();
+  for (int l = Lh - 1; l >= 1; --l) {
+    layer_bwd<T, ROWS>(lds + E.o_P2[l], E.ldp2[l], net.l[l], lds + E.o_P1[l - 1], E.ldp1[l - 1], net.hid_act,
+                       lds + E.o_P2[l - 1], E.ldp2[l - 1], pf, l - 1 >= 1 ? gw_bwd(net.l[l - 1]) : gw_none());
+    __syncthreads();
+  }
+}
+
 // ============================================================================ role hand-offs
 // With E.roles, phases A and C run as several workgroups per row tile, one per
 // network ("role"), that hand small per-row results to each other inside the
@@ -475,10 +496,10 @@ __device__ __forceinline__ float fmin_nan(float a, float b) { return (a != a) ? 
 enum HandKind { HK_PI = 0, HK_T1 = 1, HK_T2 = 2, HK_C1 = 3, HK_C2 = 4, HK_COUNT = 5 };
 #define SAC_HAND_STRIDE 576  // floats per (kind, row tile) payload: >= SAC_ROWS * (act_dim + 1)
 
-__device__ __forceinline__ AS_G uint32_t* hand_flag(const EngineDev& E, int kind, int rbi) {
+__device__ __forceinline__ AS_G uint32_t* hand_flag(const AS_C EngineDev& E, int kind, int rbi) {
   return GP(uint32_t, E.sync) + 64 + (kind * E.nrt + rbi) * 16;  // one 64-B line per flag
 }
-__device__ __forceinline__ AS_G float* hand_data(const EngineDev& E, int kind, int rbi) {
+__device__ __forceinline__ AS_G float* hand_data(const AS_C EngineDev& E, int kind, int rbi) {
   return GP(float, E.hand) + (size_t)(kind * E.nrt + rbi) * SAC_HAND_STRIDE;
 }
 __device__ __forceinline__ void st_sc1(AS_G float* p, float v) {
@@ -488,18 +509,37 @@ __device__ __forceinline__ float ld_sc1(const AS_G float* p) {
   return __hip_atomic_load((float*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 // all threads: after this workgroup's sc1 payload stores
-__device__ __forceinline__ void hand_publish(const EngineDev& E, int kind, int rbi, uint32_t ep) {
+__device__ __forceinline__ void hand_publish(const AS_C EngineDev& E, int kind, int rbi, uint32_t ep) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) __hip_atomic_store((uint32_t*)hand_flag(E, kind, rbi), ep, __ATOMIC_RELAXED,
                                            __HIP_MEMORY_SCOPE_AGENT);
 }
 // all threads: returns once flag(kind, rbi) == ep (or the spin gave up)
-__device__ __forceinline__ void hand_wait(const EngineDev& E, int kind, int rbi, uint32_t ep) {
+__device__ __forceinline__ void hand_wait(const AS_C EngineDev& E, int kind, int rbi, uint32_t ep) {
   if (threadIdx.x == 0) {
     uint32_t* f = (uint32_t*)hand_flag(E, kind, rbi);
     for (int it = 0; __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != ep; ++it) {
       if (it > (1 << 22)) {  // ~0.3 s: a producer never ran; flag the error, do not hang the GPU
+        __hip_atomic_store((uint32_t*)GP(uint32_t, E.sync) + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+  }
+  __syncthreads();
+}
+
+// all threads: returns once both flags == ep (one polling lane, one barrier)
+__device__ __forceinline__ void hand_wait2(const AS_C EngineDev& E, int k1, int k2, int rbi, uint32_t ep) {
+  if (threadIdx.x == 0) {
+    uint32_t* f1 = (uint32_t*)hand_flag(E, k1, rbi);
+    uint32_t* f2 = (uint32_t*)hand_flag(E, k2, rbi);
+    for (int it = 0;; ++it) {
+      const uint32_t a = __hip_atomic_load(f1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const uint32_t b = __hip_atomic_load(f2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (a == ep && b == ep) break;
+      if (it > (1 << 22)) {
         __hip_atomic_store((uint32_t*)GP(uint32_t, E.sync) + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         break;
       }
@@ -518,7 +558,7 @@ __global__ void __launch_bounds__(SAC_THREADS) sac_target_critic(const EngineDev
                                                                   const int32_t* __restrict__ inj_idx_,
                                                                   const float* __restrict__ inj_eps_) {
   PREFETCH_ARG(Ep);
-  const EngineDev& E = *Ep;
+  const AS_C EngineDev& E = *(const AS_C EngineDev*)Ep;
   extern __shared__ float lds_raw[];
   lf* lds = (lf*)lds_raw;
   constexpr int R = SAC_ROWS;
@@ -557,7 +597,7 @@ __global__ void __launch_bounds__(SAC_THREADS) sac_target_critic(const EngineDev
   lf* yB = lds + E.o_y;
   lf* gqB = lds + E.o_gout;
   AS_L int64_t* slotB = (AS_L int64_t*)(lds + E.o_slot);
-  const NetDev& pi = E.net[NET_PI];
+  const AS_C NetDev& pi = E.net[NET_PI];
   Pf<T> pf;
   pf_issue<T>(pf, gw_fwd(pi.l[0]));
   const AS_G float* obs = GPC(float, rb.obs);
@@ -654,7 +694,7 @@ __global__ void __launch_bounds__(SAC_THREADS) sac_target_critic(const EngineDev
     lf* X = Xb;
     lf* Y = Yb;
     for (int l = 0; l < pi.L; ++l) {
-      const LayerDev& Ly = pi.l[l];
+      const AS_C LayerDev& Ly = pi.l[l];
       if (act) store_T<T, R>(X + a0 * ld, ld, Ly.Kp, Ly.K, Ly.XT, Bp, r0, nvalid, nullptr);  // actor rows' input
       float* stash = act ? Ly.pstash + (size_t)r0 * Ly.Np : nullptr;
       if (l == pi.L - 1)
@@ -738,7 +778,7 @@ __global__ void __launch_bounds__(SAC_THREADS) sac_target_critic(const EngineDev
       __syncthreads();
     }
     for (int t = ROLES ? role - 1 : 0; t < (ROLES ? role : 2); ++t) {
-      const NetDev& q = E.net[NET_Q1T + t];
+      const AS_C NetDev& q = E.net[NET_Q1T + t];
       const int Kp0 = q.l[0].Kp;
       for (int i = tid; i < R * Kp0; i += SAC_THREADS) {
         const int r = i / Kp0, k = i % Kp0;
@@ -755,23 +795,23 @@ __global__ void __launch_bounds__(SAC_THREADS) sac_target_critic(const EngineDev
       STAMP(7 + t);
     }
     if (ROLES) hand_publish(E, HK_T1 + role - 1, rbi, ep);
+    STAMP(9);
   }
-  auto compute_y = [&](bool write_stats) {
+  if (!ROLES) {
     if (tid < R) {
       const int b = r0 + tid;
       const float mq = fmin_nan(qtB[tid], qtB[R + tid]);
       const float y = rB[tid] + (E.gamma * (1.f - dB[tid])) * (mq - alpha32 * lp2B[tid]);
       yB[tid] = y;
-      if (write_stats && b < B) stats[4 + b] = y;
+      if (b < B) stats[4 + b] = y;
     }
     __syncthreads();
-  };
-  if (!ROLES) compute_y(true);
+  }
 
   // ---- critics: forward, MSE, backward (agent.py:213-236)
   if (!ROLES || role == 3 || role == 4) {
     for (int qi = ROLES ? role - 3 : 0; qi < (ROLES ? role - 2 : 2); ++qi) {
-      const NetDev& q = E.net[NET_Q1 + qi];
+      const AS_C NetDev& q = E.net[NET_Q1 + qi];
       const int Kp0 = q.l[0].Kp;
       for (int i = tid; i < R * Kp0; i += SAC_THREADS) {
         const int r = i / Kp0, k = i % Kp0;
@@ -783,7 +823,7 @@ __global__ void __launch_bounds__(SAC_THREADS) sac_target_critic(const EngineDev
       lf* X = Xb;
       lf* Y = Yb;
       for (int l = 0; l < q.L; ++l) {
-        const LayerDev& Ly = q.l[l];
+        const AS_C LayerDev& Ly = q.l[l];
         if (l > 0) store_T<T, R>(X, ld, Ly.Kp, Ly.K, Ly.XT, Bp, r0, nvalid, nullptr);
         if (l == q.L - 1)
           layer_fwd<T, R>(X, ld, Ly, q.P + Ly.b_off, q.out_act, outP, ldo, outB, ldo, nullptr, 0, pf, gw_bwd(Ly));
@@ -796,34 +836,55 @@ __global__ void __launch_bounds__(SAC_THREADS) sac_target_critic(const EngineDev
         Y = t;
       }
       STAMP(10 + 2 * qi);
-      if (ROLES) {  // y needs both target critics and log pi' (the forward above did not)
-        hand_wait(E, HK_T1, rbi, ep);
-        hand_wait(E, HK_T2, rbi, ep);
-        hand_wait(E, HK_PI, rbi, ep);
-        if (tid < R) {
-          qtB[tid] = ld_sc1(hand_data(E, HK_T1, rbi) + tid);
-          qtB[R + tid] = ld_sc1(hand_data(E, HK_T2, rbi) + tid);
-          lp2B[tid] = ld_sc1(hand_data(E, HK_PI, rbi) + R * A + tid);
-        }
-        __syncthreads();
-        compute_y(qi == 0);
+      // Backward with a UNIT seed per row first: every layer's dY is linear in
+      // the row's seed 2(q - y)/B, so U_l = dY_l / seed does not need y and runs
+      // while the target critics finish (role split); U_l stays in LDS (the Q2
+      // pre-activation buffers, unused here) and is scaled once y is known.
+      if (tid < R) {
+        float u = tid < nvalid ? 1.f : 0.f;
+        if (q.out_act != ACT_ID) u = act_bwd(q.out_act, outP[tid * ldo], u);
+        for (int n = 0; n < 32; ++n) gqB[tid * ldo + n] = n == 0 ? u : 0.f;
       }
-      if (tid < 64) {  // wave 0: loss partial + dL/dq (mse_loss backward: 2(q-y)/B)
+      __syncthreads();
+      critic_unit_backward<T, R>(E, q, gqB, ldo, lds, pf);
+      STAMP(16);
+      // y needs both target critics and log pi'.  The target critics published
+      // only after seeing pi's flag, so their flags also order pi's payload.
+      if (ROLES) hand_wait2(E, HK_T1, HK_T2, rbi, ep);
+      STAMP(14);
+      if (tid < 64) {  // wave 0: y, loss partial, seed dL/dq (mse_loss backward: 2(q-y)/B)
         float sq = 0.f;
         if (tid < R) {
+          const int b = r0 + tid;
           const bool v = tid < nvalid;
-          const float d = outB[tid * ldo] - yB[tid];
+          float y;
+          if (ROLES) {
+            const float q1t = ld_sc1(hand_data(E, HK_T1, rbi) + tid);
+            const float q2t = ld_sc1(hand_data(E, HK_T2, rbi) + tid);
+            const float lp2 = ld_sc1(hand_data(E, HK_PI, rbi) + R * A + tid);
+            y = rB[tid] + (E.gamma * (1.f - dB[tid])) * (fmin_nan(q1t, q2t) - alpha32 * lp2);
+            if (qi == 0 && b < B) stats[4 + b] = y;
+          } else {
+            y = yB[tid];
+          }
+          const float d = outB[tid * ldo] - y;
           sq = v ? d * d : 0.f;
-          float g = v ? (2.0f / (float)B) * d : 0.f;
-          if (q.out_act != ACT_ID) g = act_bwd(q.out_act, outP[tid * ldo], g);
-          for (int n = 0; n < 32; ++n) gqB[tid * ldo + n] = n == 0 ? g : 0.f;
+          qtB[tid] = v ? (2.0f / (float)B) * d : 0.f;  // the row's seed
         }
         sq = wave_sum(sq);
         if (tid == 0) GP(float, E.lossp)[rbi * 4 + qi] = sq;
       }
       __syncthreads();
-      mlp_backward<T, R>(q, gqB, ldo, Xb, Yb, ld, E.o_P1, E.ldp1, lds, true, Bp, r0, nvalid, pf,
-                         qi == 0 ? gw_fwd(E.net[NET_Q2].l[0]) : gw_none());
+      STAMP(15);
+      {  // dY of every layer = seed * U, stored as dY^T + bias partials for phase B
+        const AS_C LayerDev& Lo = q.l[q.L - 1];
+        store_T<T, R>(gqB, ldo, Lo.Np, Lo.N, Lo.GT, Bp, r0, nvalid, Lo.dbp, qtB);
+        for (int l = q.L - 2; l >= 0; --l) {
+          const AS_C LayerDev& Ly = q.l[l];
+          store_T<T, R>(lds + E.o_P2[l], E.ldp2[l], Ly.Np, Ly.N, Ly.GT, Bp, r0, nvalid, Ly.dbp, qtB);
+        }
+        __syncthreads();
+      }
       STAMP(11 + 2 * qi);
     }
   }
@@ -838,7 +899,7 @@ __global__ void __launch_bounds__(SAC_THREADS) sac_target_critic(const EngineDev
 template <typename T, bool ROLES>
 __global__ void __launch_bounds__(SAC_THREADS) sac_actor(const EngineDev* __restrict__ Ep) {
   PREFETCH_ARG(Ep);
-  const EngineDev& E = *Ep;
+  const AS_C EngineDev& E = *(const AS_C EngineDev*)Ep;
   extern __shared__ float lds_raw[];
   lf* lds = (lf*)lds_raw;
   constexpr int R = SAC_ROWS;
@@ -871,7 +932,7 @@ __global__ void __launch_bounds__(SAC_THREADS) sac_actor(const EngineDev* __rest
   lf* outP1 = lds + E.o_outp;
   lf* out2 = lds + E.o_out2;
   lf* outP2 = lds + E.o_outp2;
-  const NetDev& pi = E.net[NET_PI];
+  const AS_C NetDev& pi = E.net[NET_PI];
   const float alpha32 = (float)*GPC(double, E.alpha_state + 1);
   Pf<T> pf;
   pf_issue<T>(pf, gw_fwd(E.net[NET_Q1].l[0]));
@@ -890,7 +951,7 @@ __global__ void __launch_bounds__(SAC_THREADS) sac_actor(const EngineDev* __rest
     const int q_lo = ROLES ? role - 1 : 0, q_hi = ROLES ? role : 2;
     // ---- Q1, Q2 on (s, a~) with the updated critics (agent.py:244-248)
     for (int qi = q_lo; qi < q_hi; ++qi) {
-      const NetDev& q = E.net[NET_Q1 + qi];
+      const AS_C NetDev& q = E.net[NET_Q1 + qi];
       const int Kp0 = q.l[0].Kp;
       for (int i = tid; i < R * Kp0; i += SAC_THREADS) {
         const int r = i / Kp0, k = i % Kp0;
@@ -937,7 +998,7 @@ __global__ void __launch_bounds__(SAC_THREADS) sac_actor(const EngineDev* __rest
 
     // ---- d a~ through the critics: dX of layer 0, action columns
     for (int qi = q_lo; qi < q_hi; ++qi) {
-      const NetDev& q = E.net[NET_Q1 + qi];
+      const AS_C NetDev& q = E.net[NET_Q1 + qi];
       lf* G0 = mlp_backward<T, R>(q, qi ? g2B : g1B, ldo, Xb, Yb, ld, qi ? E.o_P2 : E.o_P1, qi ? E.ldp2 : E.ldp1,
                                   lds, false, Bp, r0, nvalid, pf, gw_bwd(q.l[0]));
       lf* Gx = (G0 == Xb) ? Yb : Xb;
@@ -960,7 +1021,7 @@ __global__ void __launch_bounds__(SAC_THREADS) sac_actor(const EngineDev* __rest
 
   // ---- squashed-Gaussian head backward + pi backward (agent.py:255-257)
   for (int l = 0; l < pi.L - 1; ++l) {
-    const LayerDev& Ly = pi.l[l];
+    const AS_C LayerDev& Ly = pi.l[l];
     const int ldp = E.ldp1[l];
     lf* P = lds + E.o_P1[l];
     const AS_G float* ps = GPC(float, Ly.pstash) + (size_t)r0 * Ly.Np;
@@ -1019,7 +1080,7 @@ __global__ void __launch_bounds__(SAC_THREADS) sac_actor(const EngineDev* __rest
     const bool in_range = (lsr >= lo) && (lsr <= hi);
     float gm = v ? g_mu : 0.f, gs = (v && in_range) ? g_ls : 0.f;
     if (pi.out_act != ACT_ID) {
-      const LayerDev& Lo = pi.l[pi.L - 1];
+      const AS_C LayerDev& Lo = pi.l[pi.L - 1];
       const AS_G float* ps = GPC(float, Lo.pstash) + (size_t)b * Lo.Np;
       gm = act_bwd(pi.out_act, ps[j], gm);
       gs = act_bwd(pi.out_act, ps[A + j], gs);
@@ -1051,7 +1112,7 @@ __device__ __forceinline__ float adam_elem(float& p, float& m, float& v, float g
 }
 
 template <typename T>
-__device__ __forceinline__ void dw_adam_tile(const EngineDev& E, const TileDesc* tdp, bool polyak) {
+__device__ __forceinline__ void dw_adam_tile(const AS_C EngineDev& E, const TileDesc* tdp, bool polyak) {
   constexpr int KC = MM<T>::KC, KL = MM<T>::KL;
   __shared__ float red[32][9];
   const TileDesc td = *tdp;
@@ -1151,11 +1212,11 @@ __device__ __forceinline__ void dw_adam_tile(const EngineDev& E, const TileDesc*
 template <typename T>
 __global__ void __launch_bounds__(256) sac_critic_update(const EngineDev* __restrict__ Ep,
                                                          const TileDesc* __restrict__ tiles) {
-  const EngineDev& E = *Ep;
+  const AS_C EngineDev& E = *(const AS_C EngineDev*)Ep;
   dw_adam_tile<T>(E, tiles + blockIdx.x, true);
 }
 
-__device__ __forceinline__ void alpha_and_losses(const EngineDev& E) {
+__device__ __forceinline__ void alpha_and_losses(const AS_C EngineDev& E) {
   __shared__ float red[5][256];
   const int tid = threadIdx.x, B = E.B;
   const float H = E.target_entropy;
@@ -1216,7 +1277,7 @@ __device__ __forceinline__ void alpha_and_losses(const EngineDev& E) {
 template <typename T>
 __global__ void __launch_bounds__(256) sac_actor_update(const EngineDev* __restrict__ Ep, const TileDesc* __restrict__ tiles,
                                                         int ntiles) {
-  const EngineDev& E = *Ep;
+  const AS_C EngineDev& E = *(const AS_C EngineDev*)Ep;
   if ((int)blockIdx.x < ntiles)
     dw_adam_tile<T>(E, tiles + blockIdx.x, false);
   else
@@ -1229,7 +1290,7 @@ __global__ void __launch_bounds__(SAC_THREADS) sac_policy_act_kernel(const Engin
                                                              const float* __restrict__ eps_, float* __restrict__ action_,
                                                              float* __restrict__ log_pi_) {
   PREFETCH_ARG(Ep);
-  const EngineDev& E = *Ep;
+  const AS_C EngineDev& E = *(const AS_C EngineDev*)Ep;
   extern __shared__ float lds_raw[];
   lf* lds = (lf*)lds_raw;
   constexpr int R = SAC_ROWS;
@@ -1244,7 +1305,7 @@ __global__ void __launch_bounds__(SAC_THREADS) sac_policy_act_kernel(const Engin
   lf* Yb = lds + E.o_Y;
   lf* outB = lds + E.o_out;
   lf* outP = lds + E.o_outp;
-  const NetDev& pi = E.net[NET_PI];
+  const AS_C NetDev& pi = E.net[NET_PI];
   const int Kp0 = pi.l[0].Kp;
   for (int i = tid; i < R * Kp0; i += SAC_THREADS) {
     const int r = i / Kp0, k = i % Kp0;

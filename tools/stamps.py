@@ -35,9 +35,10 @@ for it in range(10):
     rows.append(buf.view(nblk, 64).cpu().numpy())
 st = np.median(np.stack(rows), axis=0)  # [blk][64]
 names = {0: "A start", 1: "gather+eps", 2: "pi L0", 3: "pi L1", 4: "pi L2", 5: "pi L3", 6: "head",
-         7: "Qt1", 8: "Qt2", 10: "Q1 fwd", 11: "Q1 bwd", 12: "Q2 fwd", 13: "Q2 bwd",
+         7: "Qt1", 8: "Qt2", 9: "Qt published", 10: "Q1 fwd", 11: "Q1 bwd", 12: "Q2 fwd", 13: "Q2 bwd",
+         14: "y inputs in", 15: "seed", 16: "unit bwd",
          32: "C start", 36: "Q1 fwd", 37: "Q2 fwd", 38: "Q1 bwd->da", 39: "Q2 bwd->da", 35: "pi bwd"}
-for base, last in ((0, 13), (32, 39)):
+for base, last in ((0, 16), (32, 39)):
     live = st[:, base] > 0  # blocks that ran this phase
     idx = [i for i in range(base, last + 1) if i in names and (st[live, i] > 0).any()]
     idx.sort(key=lambda i: np.median(st[live & (st[:, i] > 0), i] - st[live & (st[:, i] > 0), base]))
