@@ -374,12 +374,21 @@ __device__ __forceinline__ void store_T(const lf* __restrict__ src, int lds_ld, 
     const bool live = i < Kp * CH;
     const int k = i / CH, ch = i % CH;
     T v[8];
-    float s = 0.f;
+    float s = 0.f, xv[8];
+    // all reads issued before any use (a branch or wait per read would serialise them)
+#pragma unroll
+    for (int q = 0; q < 8; ++q) xv[q] = src[(ch * 8 + q) * lds_ld + (live ? k : 0)];
+    if (rowscale) {
+      float sc[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) sc[q] = rowscale[ch * 8 + q];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) xv[q] = sc[q] * xv[q];
+    }
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
       const int r = ch * 8 + q;
-      float x = (live && r < nvalid && k < K) ? src[r * lds_ld + k] : 0.f;
-      if (rowscale) x = rowscale[r] * x;
+      const float x = (live && r < nvalid && k < K) ? xv[q] : 0.f;
       s += x;
       v[q] = MM<T>::cvt(x);
     }
@@ -622,37 +631,40 @@ __global__ void __launch_bounds__(SAC_THREADS) sac_target_critic(const EngineDev
   // ---- sample (replay_buffer.py:32-39) + gather (agent.py:166-193); every role
   // draws the same indices from (seed, step), so no role waits for another's gather
   const uint64_t step = *GPC(uint64_t, E.rng_step);
+  const int64_t rb_size = GPC(int64_t, rb.state)[0], rb_pos = GPC(int64_t, rb.state)[1];
   if (tid < R) {
     int64_t slot = -1;
     const int b = r0 + tid;
     if (b < B) {
-      const int64_t size = GPC(int64_t, rb.state)[0], pos = GPC(int64_t, rb.state)[1];
       int64_t li;
       if (inj_idx) {
         li = inj_idx[b];
       } else {
-        const Feistel f = feistel_make(E.seed, step, size);
-        li = feistel_sample(f, b, size);
+        const Feistel f = feistel_make(E.seed, step, rb_size);
+        li = feistel_sample(f, b, rb_size);
       }
-      slot = size < rb.capacity ? li : (pos + li) % rb.capacity;
+      slot = rb_size < rb.capacity ? li : (rb_pos + li) % rb.capacity;
     }
     slotB[tid] = slot;
   }
   __syncthreads();
-  for (int i = tid; i < R * O; i += SAC_THREADS) {
-    const int r = i / O, j = i % O;
-    const int64_t sl = slotB[r];
-    sB[i] = sl >= 0 ? obs[sl * O + j] : 0.f;
-    s2B[i] = sl >= 0 ? nobs[sl * O + j] : 0.f;
-  }
-  for (int i = tid; i < R * A; i += SAC_THREADS) {
-    const int64_t sl = slotB[i / A];
-    aB[i] = sl >= 0 ? ract[sl * A + i % A] : 0.f;
-  }
-  if (tid < R) {
-    const int64_t sl = slotB[tid];
-    rB[tid] = sl >= 0 ? rrew[sl] : 0.f;
-    dB[tid] = sl >= 0 ? rdone[sl] : 0.f;
+  {  // one pass, every load unconditional (clamped row 0 for padding rows): one round trip
+    const int nI = R * (O > A ? O : A);
+    for (int i = tid; i < nI; i += SAC_THREADS) {
+      const int io = i < R * O ? i : R * O - 1, ia = i < R * A ? i : R * A - 1, ir = i < R ? i : R - 1;
+      const int64_t so = slotB[io / O], sa = slotB[ia / A], sr = slotB[ir];
+      const int64_t po = (so < 0 ? 0 : so) * O + io % O, pa = (sa < 0 ? 0 : sa) * A + ia % A, pr = sr < 0 ? 0 : sr;
+      const float vo = obs[po], vn = nobs[po], va = ract[pa], vr = rrew[pr], vd = rdone[pr];
+      if (i < R * O) {
+        sB[i] = so >= 0 ? vo : 0.f;
+        s2B[i] = so >= 0 ? vn : 0.f;
+      }
+      if (i < R * A) aB[i] = sa >= 0 ? va : 0.f;
+      if (i < R) {
+        rB[i] = sr >= 0 ? vr : 0.f;
+        dB[i] = sr >= 0 ? vd : 0.f;
+      }
+    }
   }
   if (do_pi) {  // which = 0: target draw (role 0), 1: actor draw (role 5)
     const int NP = (A + 1) / 2;
