@@ -1123,106 +1123,124 @@ __device__ __forceinline__ float adam_elem(float& p, float& m, float& v, float g
   return pn;
 }
 
+// One 32x32 weight tile of an update phase, 16 waves:
+//   1. all threads stage the tile's 32 dY^T rows and 32 X^T rows (the dW GEMM's
+//      operands, K = batch) into LDS and fetch their own element's master weight,
+//      Adam moments, target weight and bias state, all in one round trip;
+//   2. waves 0-3 run the dW MFMAs (one 16x16 sub-tile each, batch chunks in
+//      order: the same summation order as before the staging);
+//   3. every thread updates ONE element: Adam (torch single-tensor op order),
+//      Polyak, master + packed compute copies.
+#define SAC_UPD_THREADS 1024
+#define SAC_UPD_BCH (512 / (int)sizeof(T))  // batch columns staged per chunk (512 B per row)
 template <typename T>
-__device__ __forceinline__ void dw_adam_tile(const AS_C EngineDev& E, const TileDesc* tdp, bool polyak) {
+__device__ __forceinline__ void dw_adam_tile(const AS_C EngineDev& E, const TileDesc* tdp_, bool polyak) {
   constexpr int KC = MM<T>::KC, KL = MM<T>::KL;
+  constexpr int EPR = 16 / sizeof(T);  // elements per 16-B piece
   __shared__ float red[32][9];
-  const TileDesc td = *tdp;
+  __shared__ float accs[32][33];
+  extern __shared__ float stage_raw[];  // [64 rows][Bp + pad] of T: rows 0-31 dY^T, 32-63 X^T
+  const AS_C TileDesc& td = *(const AS_C TileDesc*)tdp_;  // scalar loads
+  STAMP(polyak ? 48 : 52);
+  const int tid = threadIdx.x;
   const int Bp = E.Bp;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int c = lane & 15, g = lane >> 4;
-  const int ns = (wave >> 1) * 16, ks = (wave & 1) * 16;
-  const int n0 = td.n0 + ns, k0 = td.k0 + ks;
+  const int lds_row = SAC_UPD_BCH + 16 / (int)sizeof(T);  // +16 B per row: rows start on different banks
+  AS_L T* stage = (AS_L T*)stage_raw;
+  // this step's Adam scalars (written by phase A)
+  const float neg_step = GPC(float, E.adam_sc)[td.opt * 2];
+  const float bc2s = GPC(float, E.adam_sc)[td.opt * 2 + 1];
+  // ---- 1. loads: element state + bias state + staged operands
   AS_G float* W = GP(float, td.W);
   AS_G float* Wm = GP(float, td.Wm);
   AS_G float* Wv = GP(float, td.Wv);
   AS_G float* tW = GP(float, td.tW);
-  // this lane's master / moment elements, fetched before the dW GEMM
-  const int k = k0 + c;
-  float p[4], m[4], v[4], tp[4];
-  bool ok[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int n = n0 + g * 4 + i;
-    ok[i] = n < td.N && k < td.K;
-    const size_t idx = ok[i] ? (size_t)n * td.K + k : 0;
-    p[i] = W[idx];
-    m[i] = Wm[idx];
-    v[i] = Wv[idx];
-    tp[i] = polyak ? tW[idx] : 0.f;
-  }
-  // bias gradient: 32 rows x 8 slices of the row-tile partial sums
+  const int en = tid >> 5, ek = tid & 31;  // this thread's element (n0 + en, k0 + ek)
+  const int n = td.n0 + en, k = td.k0 + ek;
+  const bool ok = n < td.N && k < td.K;
+  const size_t idx = ok ? (size_t)n * td.K + k : 0;
+  float p = W[idx], m = Wm[idx], v = Wv[idx];
+  const float tp = polyak ? tW[idx] : 0.f;
   const bool do_bias = td.k0 == 0;
+  float pb = 0.f, mb = 0.f, vb = 0.f, tbv = 0.f;
+  if (do_bias && tid < 32 && td.n0 + tid < td.N) {
+    pb = GPC(float, td.b)[td.n0 + tid];
+    mb = GPC(float, td.bm)[td.n0 + tid];
+    vb = GPC(float, td.bv)[td.n0 + tid];
+    if (polyak) tbv = GPC(float, td.tb)[td.n0 + tid];
+  }
   float bsum = 0.f;
-  const int bn = threadIdx.x >> 3, bs = threadIdx.x & 7;
-  if (do_bias && td.n0 + bn < td.N)
+  const int bn = tid >> 3, bs = tid & 7;
+  if (do_bias && tid < 256 && td.n0 + bn < td.N)
     for (int rt = bs; rt < td.nrt; rt += 8) bsum += GPC(float, td.dbp)[(size_t)rt * td.N + td.n0 + bn];
-
-  const AS_G T* arow = GPC(T, td.GT) + (size_t)(ns + c) * Bp + g * KL;
-  const AS_G T* brow = GPC(T, td.XT) + (size_t)(ks + c) * Bp + g * KL;
-  const int nch = Bp / KC;
+  // ---- 2. dW = dY^T X over the batch, staged through LDS in 512-B row chunks;
+  // waves 0-3 run one 16x16 sub-tile each, chunks in batch order
+  const int lane = tid & 63, wave = tid >> 6;
+  const int c = lane & 15, g = lane >> 4;
+  const int ns = (wave >> 1) * 16, ks = (wave & 1) * 16;
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-  int ch = 0;
-  for (; ch + 8 <= nch; ch += 8) {
-    typename MM<T>::Frag a[8], b[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      a[u] = MM<T>::ld(arow + (ch + u) * KC);
-      b[u] = MM<T>::ld(brow + (ch + u) * KC);
+  for (int b0 = 0; b0 < Bp; b0 += SAC_UPD_BCH) {
+    const int bch = Bp - b0 < SAC_UPD_BCH ? Bp - b0 : SAC_UPD_BCH;
+    const int per_row = bch / EPR;  // 16-B pieces per operand row of this chunk
+    for (int i = tid; i < 64 * per_row; i += SAC_UPD_THREADS) {
+      const int row = i / per_row, pc = i % per_row;
+      const AS_G T* src = row < 32 ? GPC(T, td.GT) + (size_t)row * Bp : GPC(T, td.XT) + (size_t)(row - 32) * Bp;
+      *(AS_L u32x4*)(stage + row * lds_row + pc * EPR) = *(const AS_G u32x4*)(src + b0 + pc * EPR);
     }
-#pragma unroll
-    for (int u = 0; u < 8; ++u) MM<T>::mma(acc, a[u], b[u]);
-  }
-  for (; ch < nch; ++ch) MM<T>::mma(acc, MM<T>::ld(arow + ch * KC), MM<T>::ld(brow + ch * KC));
-
-  const float neg_step = GPC(float, E.adam_sc)[td.opt * 2];
-  const float bc2s = GPC(float, E.adam_sc)[td.opt * 2 + 1];
-  const float w1 = (float)(1.0 - (double)E.beta1), b2 = E.beta2, w2 = (float)(1.0 - (double)E.beta2);
-  const float eps = E.adam_eps, tau = E.tau, omt = (float)(1.0 - (double)E.tau);
-  AS_G T* Wc = GP(T, td.Wc);
-  AS_G T* WTc = GP(T, td.WTc);
-  AS_G T* tWc = GP(T, td.tWc);
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    if (!ok[i]) continue;
-    const int n = n0 + g * 4 + i;
-    const size_t idx = (size_t)n * td.K + k;
-    const float pn = adam_elem(p[i], m[i], v[i], acc[i], w1, b2, w2, bc2s, eps, neg_step);
-    W[idx] = p[i];
-    Wm[idx] = m[i];
-    Wv[idx] = v[i];
-    Wc[packed_off<T>(n, k, td.Kp)] = MM<T>::cvt(pn);
-    WTc[packed_off<T>(k, n, td.Np)] = MM<T>::cvt(pn);
-    if (polyak) {
-      const float tn = tau * pn + omt * tp[i];
-      tW[idx] = tn;
-      tWc[packed_off<T>(n, k, td.Kp)] = MM<T>::cvt(tn);
-    }
-  }
-  if (do_bias) {
-    red[bn][bs] = bsum;
     __syncthreads();
-    if (threadIdx.x < 32) {
-      const int n = td.n0 + threadIdx.x;
-      if (n < td.N) {
-        float gb = 0.f;
-        for (int s = 0; s < 8; ++s) gb += red[threadIdx.x][s];
-        AS_G float* bp = GP(float, td.b);
-        AS_G float* bm = GP(float, td.bm);
-        AS_G float* bv = GP(float, td.bv);
-        float pb = bp[n], mb = bm[n], vb = bv[n];
-        const float pn = adam_elem(pb, mb, vb, gb, w1, b2, w2, bc2s, eps, neg_step);
-        bp[n] = pb;
-        bm[n] = mb;
-        bv[n] = vb;
-        if (polyak) GP(float, td.tb)[n] = tau * pn + omt * GP(float, td.tb)[n];
+    if (wave < 4) {
+      const AS_L T* arow = stage + (ns + c) * lds_row + g * KL;
+      const AS_L T* brow = stage + (32 + ks + c) * lds_row + g * KL;
+      for (int ch = 0; ch < bch / KC; ++ch) {
+        typename MM<T>::Frag a, b;
+        if constexpr (sizeof(T) == 2) {
+          a = *(const AS_L bf16x8*)(arow + ch * KC);
+          b = *(const AS_L bf16x8*)(brow + ch * KC);
+        } else {
+          a = *(const AS_L f32x4*)(arow + ch * KC);
+          b = *(const AS_L f32x4*)(brow + ch * KC);
+        }
+        MM<T>::mma(acc, a, b);
       }
     }
+    __syncthreads();  // the stage is refilled by the next chunk
+  }
+  STAMP(polyak ? 49 : 53);
+  if (wave < 4) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) accs[ns + g * 4 + i][ks + c] = acc[i];
+  }
+  if (do_bias && tid < 256) red[bn][bs] = bsum;
+  __syncthreads();
+  STAMP(polyak ? 50 : 54);
+  // ---- 3. one element per thread
+  const float w1 = (float)(1.0 - (double)E.beta1), b2 = E.beta2, w2 = (float)(1.0 - (double)E.beta2);
+  const float eps = E.adam_eps, tau = E.tau, omt = (float)(1.0 - (double)E.tau);
+  if (ok) {
+    const float pn = adam_elem(p, m, v, accs[en][ek], w1, b2, w2, bc2s, eps, neg_step);
+    W[idx] = p;
+    Wm[idx] = m;
+    Wv[idx] = v;
+    GP(T, td.Wc)[packed_off<T>(n, k, td.Kp)] = MM<T>::cvt(pn);
+    GP(T, td.WTc)[packed_off<T>(k, n, td.Np)] = MM<T>::cvt(pn);
+    if (polyak) {
+      const float tn = tau * pn + omt * tp;
+      tW[idx] = tn;
+      GP(T, td.tWc)[packed_off<T>(n, k, td.Kp)] = MM<T>::cvt(tn);
+    }
+  }
+  if (do_bias && tid < 32 && td.n0 + tid < td.N) {
+    float gb = 0.f;
+    for (int q = 0; q < 8; ++q) gb += red[tid][q];
+    const float pn = adam_elem(pb, mb, vb, gb, w1, b2, w2, bc2s, eps, neg_step);
+    GP(float, td.b)[td.n0 + tid] = pb;
+    GP(float, td.bm)[td.n0 + tid] = mb;
+    GP(float, td.bv)[td.n0 + tid] = vb;
+    if (polyak) GP(float, td.tb)[td.n0 + tid] = tau * pn + omt * tbv;
   }
 }
 
 template <typename T>
-__global__ void __launch_bounds__(256) sac_critic_update(const EngineDev* __restrict__ Ep,
+__global__ void __launch_bounds__(SAC_UPD_THREADS) sac_critic_update(const EngineDev* __restrict__ Ep,
                                                          const TileDesc* __restrict__ tiles) {
   const AS_C EngineDev& E = *(const AS_C EngineDev*)Ep;
   dw_adam_tile<T>(E, tiles + blockIdx.x, true);
@@ -1231,6 +1249,7 @@ __global__ void __launch_bounds__(256) sac_critic_update(const EngineDev* __rest
 __device__ __forceinline__ void alpha_and_losses(const AS_C EngineDev& E) {
   __shared__ float red[5][256];
   const int tid = threadIdx.x, B = E.B;
+  if (tid >= 256) return;  // whole waves leave: the barriers below count waves 0-3
   const float H = E.target_entropy;
   AS_G double* st = GP(double, E.alpha_state);
   const float la32 = (float)st[0];
@@ -1238,12 +1257,12 @@ __device__ __forceinline__ void alpha_and_losses(const AS_C EngineDev& E) {
   const AS_G float* lp = GPC(float, E.lp_st);
   const AS_G float* lossp = GPC(float, E.lossp);
   float sg = 0.f, sl = 0.f, l0 = 0.f, l1 = 0.f, l2 = 0.f;
-  for (int b = tid; b < B; b += blockDim.x) {
+  for (int b = tid; b < B; b += 256) {
     const float term = lp[b] + H;
     sg += mB * term;
     sl += la32 * term;
   }
-  for (int rt = tid; rt < E.nrt; rt += blockDim.x) {
+  for (int rt = tid; rt < E.nrt; rt += 256) {
     l0 += lossp[rt * 4 + 0];
     l1 += lossp[rt * 4 + 1];
     l2 += lossp[rt * 4 + 2];
@@ -1287,7 +1306,7 @@ __device__ __forceinline__ void alpha_and_losses(const AS_C EngineDev& E) {
 }
 
 template <typename T>
-__global__ void __launch_bounds__(256) sac_actor_update(const EngineDev* __restrict__ Ep, const TileDesc* __restrict__ tiles,
+__global__ void __launch_bounds__(SAC_UPD_THREADS) sac_actor_update(const EngineDev* __restrict__ Ep, const TileDesc* __restrict__ tiles,
                                                         int ntiles) {
   const AS_C EngineDev& E = *(const AS_C EngineDev*)Ep;
   if ((int)blockIdx.x < ntiles)

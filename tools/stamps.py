@@ -38,15 +38,27 @@ names = {0: "A start", 1: "gather+eps", 2: "pi L0", 3: "pi L1", 4: "pi L2", 5: "
          7: "Qt1", 8: "Qt2", 9: "Qt published", 10: "Q1 fwd", 11: "Q1 bwd", 12: "Q2 fwd", 13: "Q2 bwd",
          14: "y inputs in", 15: "seed", 16: "unit bwd",
          32: "C start", 36: "Q1 fwd", 37: "Q2 fwd", 38: "Q1 bwd->da", 39: "Q2 bwd->da", 35: "pi bwd"}
-for base, last in ((0, 16), (32, 39)):
+names.update({48: "B start", 49: "B dW done", 50: "B adam issued", 52: "D start", 53: "D dW done",
+              54: "D adam issued"})
+for base, last in ((0, 16), (32, 39), (48, 50), (52, 54)):
     live = st[:, base] > 0  # blocks that ran this phase
     idx = [i for i in range(base, last + 1) if i in names and (st[live, i] > 0).any()]
     idx.sort(key=lambda i: np.median(st[live & (st[:, i] > 0), i] - st[live & (st[:, i] > 0), base]))
     prev = None
-    print(f"--- phase {'A' if base == 0 else 'C'} (cycles, median over blocks)")
+    print(f"--- phase {dict([(0, 'A'), (32, 'C'), (48, 'B'), (52, 'D')])[base]} (cycles, median over blocks)")
     for i in idx:
         m = live & (st[:, i] > 0)
         t = np.median(st[m, i] - st[m, base])
         if prev is not None:
             print(f"  {names[i]:12s} +{t - prev:9.0f}   (cum {t:9.0f})")
         prev = t
+
+# whole-grid view: first start -> last stamp of each phase (dispatch skew + slowest block)
+for base, last, nm in ((0, 16, "A"), (32, 39, "C"), (48, 50, "B"), (52, 54, "D")):
+    live = st[:, base] > 0
+    if not live.any():
+        continue
+    t0 = st[live, base].min()
+    ends = st[live, base:last + 1].max(axis=1)
+    print(f"--- phase {nm}: blocks {live.sum()}, start skew {st[live, base].max() - t0:.0f}, "
+          f"span first-start -> last-stamp {ends.max() - t0:.0f} cycles")
