@@ -22,7 +22,7 @@ eng, rb, c = bench.build_engine(cfg, prec, 0, dev)
 lib = E.load_library()
 lib.sac_engine_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
 assert lib.sac_engine_debug_stamped() == 1, "not the stamps build"
-nblk = 8 * ((c["batch"] + 15) // 16)  # covers xs-spread and role-split grids
+nblk = 2048  # rows for every block index any phase grid can have (B/D tile grids included)
 buf = torch.zeros(nblk * 64, dtype=torch.int64, device=dev)
 E.check(lib.sac_engine_debug_stamps(eng.handle, E.ptr(buf), eng._stream()))
 eng.train(rb, 20)
