@@ -334,6 +334,7 @@ static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
       h.net[ni].P = parts[ni];
       h.net[ni].M = ni < 3 ? ms[ni] : nullptr;
       h.net[ni].V = ni < 3 ? vs[ni] : nullptr;
+      for (int l = 0; l < h.net[ni].L; ++l) h.net[ni].l[l].bias = parts[ni] + h.net[ni].l[l].b_off;
     }
     h.alpha_state = e->buf.alpha_state;
     h.opt_steps = e->buf.opt_steps;

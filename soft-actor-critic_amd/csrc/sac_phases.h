@@ -17,6 +17,7 @@ struct LayerDev {
   void* GT;       // [Np][Bp] d(pre-activation), transposed
   float* dbp;     // [nrt][N] bias-gradient partial sums per row tile
   float* pstash;  // pi only: pre-activations of the actor rows [Br][Np]
+  const float* bias;  // = net P + b_off (fp32 master bias [N])
 };
 
 struct NetDev {
@@ -118,21 +119,28 @@ __device__ __forceinline__ void prefetch_engine(const void* p) {
 // so the load latency overlaps the epilogue, the barrier and whatever non-GEMM
 // work sits between the two steps.
 struct GemmW {
-  const void* p;  // packed B matrix
-  int cols;       // reduction length (multiple of SAC_PAD)
-  int NT;         // 16-row tiles of the packed matrix = output tiles of the step
+  const void* p;      // packed B matrix
+  int cols;           // reduction length (multiple of SAC_PAD)
+  int NT;             // 16-row tiles of the packed matrix = output tiles of the step
+  const float* bias;  // forward steps: bias [N], prefetched with the weights
+  int N;
 };
-__device__ __forceinline__ GemmW gw_fwd(const AS_C LayerDev& L) { return GemmW{L.Wc, L.Kp, L.Np >> 4}; }
-__device__ __forceinline__ GemmW gw_bwd(const AS_C LayerDev& L) { return GemmW{L.WTc, L.Np, L.Kp >> 4}; }
-__device__ __forceinline__ GemmW gw_none() { return GemmW{nullptr, 0, 0}; }
+__device__ __forceinline__ GemmW gw_fwd(const AS_C LayerDev& L) { return GemmW{L.Wc, L.Kp, L.Np >> 4, L.bias, L.N}; }
+__device__ __forceinline__ GemmW gw_bwd(const AS_C LayerDev& L) { return GemmW{L.WTc, L.Np, L.Kp >> 4, nullptr, 0}; }
+__device__ __forceinline__ GemmW gw_none() { return GemmW{nullptr, 0, 0, nullptr, 0}; }
 
 #ifndef SAC_PF
-#define SAC_PF 0  // cross-step register prefetch of the weight stream (see gemm_step)
+// Cross-step register prefetch of the weight stream: chunks per tile of the
+// NEXT GEMM step each wave keeps in flight, plus its first bias values (see
+// gemm_step).  Measured on C2: 1 chunk (8 VGPRs) 17.3K steps/s vs 17.8K without;
+// 8 chunks spill at 8 waves.  Off by default.
+#define SAC_PF 0
 #endif
 template <typename T>
 struct Pf {
 #if SAC_PF
-  typename MM<T>::Frag f0[8], f1[8];
+  typename MM<T>::Frag f0[SAC_PF], f1[SAC_PF];
+  float b0, b1;  // bias of the lane's column in the first tile pair (forward steps)
 #endif
   const void* tag;  // which B matrix the registers hold (wave-uniform)
 };
@@ -149,8 +157,13 @@ __device__ __forceinline__ void pf_issue(Pf<T>& pf, const GemmW& w) {
   const int nt1 = wave + SAC_NW < w.NT ? wave + SAC_NW : wave;
   const AS_G T* b0 = GPC(T, w.p) + packed_lane<T>(wave, w.cols, lane);
   const AS_G T* b1 = GPC(T, w.p) + packed_lane<T>(nt1, w.cols, lane);
+  if (w.bias) {  // same columns as layer_fwd's first pair: n0 = 16 wave + c, n1 = n0 + 16 SAC_NW
+    const int n0 = wave * 16 + (lane & 15), n1 = n0 + 16 * SAC_NW;
+    pf.b0 = GPC(float, w.bias)[n0 < w.N ? n0 : w.N - 1];
+    pf.b1 = GPC(float, w.bias)[n1 < w.N ? n1 : w.N - 1];
+  }
 #pragma unroll
-  for (int u = 0; u < 8; ++u) {
+  for (int u = 0; u < SAC_PF; ++u) {
     const int cu = u < last ? u : last;
     pf.f0[u] = MM<T>::ld(b0 + cu * FS);
     pf.f1[u] = MM<T>::ld(b1 + cu * FS);
@@ -158,54 +171,44 @@ __device__ __forceinline__ void pf_issue(Pf<T>& pf, const GemmW& w) {
 #endif
 }
 
-// acc{0,1} += A x B over chunks [ch0, nch) loaded here (batches of 8 / 2 / 1:
-// every load of a batch issued before its first MFMA).
+// acc{0,1} += A x B over chunks [ch0, nch) loaded here, in batches of BM chunks
+// whose loads are all issued before the batch's first MFMA.  A short last batch
+// loads its last chunk again for the missing slots (unconditional, so the loads
+// stay back to back) and skips their MFMAs.
 template <typename T, int RT, int BM>
 __device__ __forceinline__ void mma_pair_from(const lf* __restrict__ arow, int lda, const AS_G T* b0, const AS_G T* b1,
                                               bool has1, int ch0, int nch, f32x4 (&acc0)[RT], f32x4 (&acc1)[RT]) {
   constexpr int KC = MM<T>::KC;
   constexpr int FS = 64 * MM<T>::KL;
   typedef typename MM<T>::Frag F;
-  int ch = ch0;
-  for (; ch + BM <= nch; ch += BM) {
+  for (int ch = ch0; ch < nch; ch += BM) {
+    const int rem = nch - ch < BM ? nch - ch : BM;
     F f0[BM], f1[BM];
 #pragma unroll
     for (int u = 0; u < BM; ++u) {
-      f0[u] = MM<T>::ld(b0 + (ch + u) * FS);
-      f1[u] = MM<T>::ld(b1 + (ch + u) * FS);
+      const int cu = ch + (u < rem ? u : rem - 1);
+      f0[u] = MM<T>::ld(b0 + cu * FS);
+      f1[u] = MM<T>::ld(b1 + cu * FS);
     }
+    if (rem == BM) {  // full batch: straight-line, LDS reads free to be hoisted
 #pragma unroll
-    for (int u = 0; u < BM; ++u)
+      for (int u = 0; u < BM; ++u)
 #pragma unroll
-      for (int rt = 0; rt < RT; ++rt) {
-        const F a = MM<T>::from_lds(arow + rt * 16 * lda + (ch + u) * KC);
-        MM<T>::mma(acc0[rt], a, f0[u]);
-        if (has1) MM<T>::mma(acc1[rt], a, f1[u]);
-      }
-  }
-  for (; ch + 2 <= nch; ch += 2) {
-    F f0[2], f1[2];
+        for (int rt = 0; rt < RT; ++rt) {
+          const F a = MM<T>::from_lds(arow + rt * 16 * lda + (ch + u) * KC);
+          MM<T>::mma(acc0[rt], a, f0[u]);
+          if (has1) MM<T>::mma(acc1[rt], a, f1[u]);
+        }
+    } else {
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      f0[u] = MM<T>::ld(b0 + (ch + u) * FS);
-      f1[u] = MM<T>::ld(b1 + (ch + u) * FS);
-    }
+      for (int u = 0; u < BM; ++u)
+        if (u < rem)
 #pragma unroll
-    for (int u = 0; u < 2; ++u)
-#pragma unroll
-      for (int rt = 0; rt < RT; ++rt) {
-        const F a = MM<T>::from_lds(arow + rt * 16 * lda + (ch + u) * KC);
-        MM<T>::mma(acc0[rt], a, f0[u]);
-        if (has1) MM<T>::mma(acc1[rt], a, f1[u]);
-      }
-  }
-  if (ch < nch) {
-    const F f0 = MM<T>::ld(b0 + ch * FS), f1 = MM<T>::ld(b1 + ch * FS);
-#pragma unroll
-    for (int rt = 0; rt < RT; ++rt) {
-      const F a = MM<T>::from_lds(arow + rt * 16 * lda + ch * KC);
-      MM<T>::mma(acc0[rt], a, f0);
-      if (has1) MM<T>::mma(acc1[rt], a, f1);
+          for (int rt = 0; rt < RT; ++rt) {
+            const F a = MM<T>::from_lds(arow + rt * 16 * lda + (ch + u) * KC);
+            MM<T>::mma(acc0[rt], a, f0[u]);
+            if (has1) MM<T>::mma(acc1[rt], a, f1[u]);
+          }
     }
   }
 }
@@ -236,9 +239,9 @@ __device__ __forceinline__ void gemm_step(const lf* __restrict__ A, int lda, con
 #if SAC_PF
     int ch0 = 0;
     if (first) {
-      ch0 = nch < 8 ? nch : 8;
+      ch0 = nch < SAC_PF ? nch : SAC_PF;
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
+      for (int u = 0; u < SAC_PF; ++u) {
         if (u < ch0)
 #pragma unroll
           for (int rt = 0; rt < RT; ++rt) {
@@ -253,7 +256,7 @@ __device__ __forceinline__ void gemm_step(const lf* __restrict__ A, int lda, con
       pf_issue<T>(pf, next);
       __builtin_amdgcn_sched_barrier(0);
     }
-    mma_pair_from<T, RT, 4>(arow, lda, b0, b1, has1, ch0, nch, acc0, acc1);
+    mma_pair_from<T, RT, 8>(arow, lda, b0, b1, has1, ch0, nch, acc0, acc1);
 #else
     (void)first;
     mma_pair_from<T, RT, 8>(arow, lda, b0, b1, has1, 0, nch, acc0, acc1);
@@ -319,8 +322,14 @@ __device__ __forceinline__ void layer_fwd(const lf* X, int ldx, const AS_C Layer
   // The first pair's bias is loaded before the step: a load issued after the
   // next step's prefetch would wait for all of it (vmcnt retires in order).
   const int n0 = wave * 16 + (lane & 15), n1 = n0 + 16 * SAC_NW;
+  const GemmW w = gw_fwd(L);
+#if SAC_PF
+  if (pf.tag != w.p) pf_issue<T>(pf, w);  // bias arrives with the prefetched weights
+  const float bpre0 = pf.b0, bpre1 = pf.b1;
+#else
   const float bpre0 = bias[n0 < N ? n0 : N - 1], bpre1 = bias[n1 < N ? n1 : N - 1];
-  gemm_step<T, ROWS>(X, ldx, gw_fwd(L), pf, next, [&](int h, int n, const f32x4* acc) {
+#endif
+  gemm_step<T, ROWS>(X, ldx, w, pf, next, [&](int h, int n, const f32x4* acc) {
     const bool nv = n < N;
     const float bn = n == n0 ? bpre0 : n == n1 ? bpre1 : bias[nv ? n : N - 1];
 #pragma unroll
@@ -607,8 +616,9 @@ __global__ void __launch_bounds__(SAC_THREADS) sac_target_critic(const EngineDev
   lf* gqB = lds + E.o_gout;
   AS_L int64_t* slotB = (AS_L int64_t*)(lds + E.o_slot);
   const AS_C NetDev& pi = E.net[NET_PI];
-  Pf<T> pf;
-  pf_issue<T>(pf, gw_fwd(pi.l[0]));
+  Pf<T> pf;  // this role's first GEMM streams in under the sample / gather
+  pf_issue<T>(pf, !ROLES || do_pi ? gw_fwd(pi.l[0])
+                  : gw_fwd(E.net[role <= 2 ? NET_Q1T + role - 1 : NET_Q1 + role - 3].l[0]));
   const AS_G float* obs = GPC(float, rb.obs);
   const AS_G float* nobs = GPC(float, rb.next_obs);
   const AS_G float* ract = GPC(float, rb.act);
@@ -703,11 +713,13 @@ __global__ void __launch_bounds__(SAC_THREADS) sac_target_critic(const EngineDev
       Xb[r * ld + k] = k < O ? (r < a0 ? s2B[r * O + k] : sB[(r - a0) * O + k]) : 0.f;
     }
     __syncthreads();
+    STAMP(56);
     lf* X = Xb;
     lf* Y = Yb;
     for (int l = 0; l < pi.L; ++l) {
       const AS_C LayerDev& Ly = pi.l[l];
       if (act) store_T<T, R>(X + a0 * ld, ld, Ly.Kp, Ly.K, Ly.XT, Bp, r0, nvalid, nullptr);  // actor rows' input
+      if (l == 0) STAMP(57);
       float* stash = act ? Ly.pstash + (size_t)r0 * Ly.Np : nullptr;
       if (l == pi.L - 1)
         layer_fwd<T, ROWS>(X, ld, Ly, pi.P + Ly.b_off, pi.out_act, outP, ldo, outB, ldo, stash, a0, pf,
@@ -946,8 +958,9 @@ __global__ void __launch_bounds__(SAC_THREADS) sac_actor(const EngineDev* __rest
   lf* outP2 = lds + E.o_outp2;
   const AS_C NetDev& pi = E.net[NET_PI];
   const float alpha32 = (float)*GPC(double, E.alpha_state + 1);
-  Pf<T> pf;
-  pf_issue<T>(pf, gw_fwd(E.net[NET_Q1].l[0]));
+  Pf<T> pf;  // this role's first GEMM streams in under the loads / the wait
+  pf_issue<T>(pf, !ROLES ? gw_fwd(E.net[NET_Q1].l[0])
+                  : role == 0 ? gw_bwd(pi.l[pi.L - 1]) : gw_fwd(E.net[NET_Q1 + role - 1].l[0]));
 
   if (!ROLES || role >= 1) {
     for (int i = tid; i < R * O; i += SAC_THREADS) sB[i] = GPC(float, E.s_st)[(size_t)r0 * O + i];
@@ -972,7 +985,8 @@ __global__ void __launch_bounds__(SAC_THREADS) sac_actor(const EngineDev* __rest
       __syncthreads();
       mlp_forward<T, R>(q, Xb, Yb, ld, qi ? outP2 : outP1, qi ? out2 : out1, ldo, qi ? E.o_P2 : E.o_P1,
                         qi ? E.ldp2 : E.ldp1, lds, true, false, Bp, r0, nvalid, pf,
-                        qi ? gw_bwd(E.net[NET_Q1].l[E.net[NET_Q1].L - 1]) : gw_fwd(E.net[NET_Q2].l[0]));
+                        ROLES ? gw_bwd(q.l[q.L - 1])
+                        : qi ? gw_bwd(E.net[NET_Q1].l[E.net[NET_Q1].L - 1]) : gw_fwd(E.net[NET_Q2].l[0]));
       STAMP(36 + qi);
     }
     // ---- backward seeds.  L_pi = mean(alpha logpi - min Q) (agent.py:251-252); min

@@ -1,6 +1,7 @@
 """Where does a phase kernel spend its time?  Runs the C2 engine from the
--DSAC_STAMPS build (make -C soft-actor-critic_amd/csrc stamps) and prints the
-s_memtime deltas between the STAMP(i) points, median over row-tile blocks."""
+-DSAC_STAMPS build (make -C soft-actor-critic_amd/csrc stamps) and prints, per
+phase and per workgroup role, the s_memtime deltas between STAMP(i) points
+(median over row tiles and over 10 steps)."""
 import ctypes
 import os
 import sys
@@ -23,42 +24,46 @@ lib = E.load_library()
 lib.sac_engine_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
 assert lib.sac_engine_debug_stamped() == 1, "not the stamps build"
 nblk = 2048  # rows for every block index any phase grid can have (B/D tile grids included)
+nrt = (c["batch"] + 15) // 16
 buf = torch.zeros(nblk * 64, dtype=torch.int64, device=dev)
 E.check(lib.sac_engine_debug_stamps(eng.handle, E.ptr(buf), eng._stream()))
 eng.train(rb, 20)
 torch.cuda.synchronize()
-rows = []
+runs = []
 for it in range(10):
     buf.zero_()
     eng.train(rb, 1)
     torch.cuda.synchronize()
-    rows.append(buf.view(nblk, 64).cpu().numpy())
-st = np.median(np.stack(rows), axis=0)  # [blk][64]
-names = {0: "A start", 1: "gather+eps", 2: "pi L0", 3: "pi L1", 4: "pi L2", 5: "pi L3", 6: "head",
-         7: "Qt1", 8: "Qt2", 9: "Qt published", 10: "Q1 fwd", 11: "Q1 bwd", 12: "Q2 fwd", 13: "Q2 bwd",
-         14: "y inputs in", 15: "seed", 16: "unit bwd",
-         32: "C start", 36: "Q1 fwd", 37: "Q2 fwd", 38: "Q1 bwd->da", 39: "Q2 bwd->da", 35: "pi bwd"}
-names.update({48: "B start", 49: "B dW done", 50: "B adam issued", 52: "D start", 53: "D dW done",
-              54: "D adam issued"})
-for base, last in ((0, 16), (32, 39), (48, 50), (52, 54)):
-    live = st[:, base] > 0  # blocks that ran this phase
-    idx = [i for i in range(base, last + 1) if i in names and (st[live, i] > 0).any()]
-    idx.sort(key=lambda i: np.median(st[live & (st[:, i] > 0), i] - st[live & (st[:, i] > 0), base]))
-    prev = None
-    print(f"--- phase {dict([(0, 'A'), (32, 'C'), (48, 'B'), (52, 'D')])[base]} (cycles, median over blocks)")
-    for i in idx:
-        m = live & (st[:, i] > 0)
-        t = np.median(st[m, i] - st[m, base])
-        if prev is not None:
-            print(f"  {names[i]:12s} +{t - prev:9.0f}   (cum {t:9.0f})")
-        prev = t
-
-# whole-grid view: first start -> last stamp of each phase (dispatch skew + slowest block)
-for base, last, nm in ((0, 16, "A"), (32, 39, "C"), (48, 50, "B"), (52, 54, "D")):
-    live = st[:, base] > 0
-    if not live.any():
+    runs.append(buf.view(nblk, 64).cpu().numpy().copy())
+names = {0: "start", 1: "gather+eps", 56: "pi X built", 57: "pi L0 issued", 2: "pi L0", 3: "pi L1", 4: "pi L2",
+         5: "pi L3", 6: "head+publish", 7: "Qt1", 8: "Qt2", 9: "Qt published", 10: "Q1 fwd", 12: "Q2 fwd",
+         16: "unit bwd", 14: "y inputs in", 15: "seed", 11: "Q1 GT stored", 13: "Q2 GT stored",
+         32: "start", 36: "Q1 fwd", 37: "Q2 fwd", 38: "Q1 bwd->da", 39: "Q2 bwd->da / combined", 35: "pi bwd",
+         48: "start", 49: "dW", 50: "adam", 52: "start", 53: "dW", 54: "adam"}
+PH = {"A": list(range(0, 17)) + [56, 57], "C": list(range(32, 40)), "B": [48, 49, 50], "D": [52, 53, 54]}
+ROLES = {"A": ["pi(s')", "Qt1", "Qt2", "Q1", "Q2", "pi(s)"], "C": ["pi", "Q1", "Q2"]}
+for ph, ids in PH.items():
+    base = ids[0]
+    rows = np.concatenate([r[r[:, base] > 0] for r in runs])
+    blk = np.concatenate([np.nonzero(r[:, base] > 0)[0] for r in runs])
+    if rows.size == 0:
         continue
-    t0 = st[live, base].min()
-    ends = st[live, base:last + 1].max(axis=1)
-    print(f"--- phase {nm}: blocks {live.sum()}, start skew {st[live, base].max() - t0:.0f}, "
-          f"span first-start -> last-stamp {ends.max() - t0:.0f} cycles")
+    groups = {"all": np.ones(len(blk), bool)}
+    if ph in ROLES and eng.roles:
+        groups = {nm: (blk // nrt) == k for k, nm in enumerate(ROLES[ph])}
+    t_first = np.array([r[r[:, base] > 0, base].min() for r in runs])
+    print(f"=== phase {ph}")
+    for g, m in groups.items():
+        if not m.any():
+            continue
+        sel = rows[m]
+        seq = [(i, np.median(sel[sel[:, i] > 0, i] - sel[sel[:, i] > 0, base])) for i in ids
+               if i != base and (sel[:, i] > 0).any()]
+        seq.sort(key=lambda x: x[1])
+        line, prev = [], 0.0
+        for i, t in seq:
+            line.append(f"{names.get(i, i)} +{t - prev:.0f}")
+            prev = t
+        print(f"  [{g:6s}] " + " | ".join(line) + f"   (total {prev:.0f})")
+    spans = [r[r[:, base] > 0][:, ids].max() - r[r[:, base] > 0, base].min() for r in runs]
+    print(f"  first start -> last stamp of the grid: median {np.median(spans):.0f} cycles")
