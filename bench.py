@@ -125,6 +125,23 @@ def gather_sweep(rb, device, sizes=(256, 4096, 65536, 1_048_576), reps=20):
     return out
 
 
+def pmc_traffic(kernel):
+    """HBM-side bytes per launch of `kernel` from the newest committed PMC
+    summary (profiles/<round>_pmc.json, written by tools/pmc_summary.py from
+    separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this bench)."""
+    import glob
+
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc.json")))
+    if not files:
+        return None, None
+    with open(files[-1]) as f:
+        d = json.load(f)
+    k = d.get("kernels", {}).get(kernel)
+    if not k:
+        return None, None
+    return k["hbm_bytes_per_launch"], os.path.relpath(files[-1], ROOT)
+
+
 def cpu_baseline(cfgname, seconds=12.0):
     """Oracle (numpy restatement of the reference step incl. its deque +
     random.sample replay) on the host, single BLAS thread, bounded sample."""
@@ -217,6 +234,7 @@ def main():
     from sac import _engine as E
 
     kname = E.load_library().sac_phase_kernel_name(dom).decode()
+    traffic, traffic_src = pmc_traffic(kname) if args.config == "c2" and args.precision == "bf16" else (None, None)
     achieved = flops[dom] / (phase_ms[dom] * 1e-3) / 1e12
     peak = PEAK_TFLOPS[args.precision]
 
@@ -246,8 +264,10 @@ def main():
             "phase_ms": [round(x, 5) for x in phase_ms],
             "step_gemm_flops_survey": f_total,
             "roofline": {"bound": "mfma", "kernel": kname, "achieved": round(achieved, 3), "peak": peak,
-                         "unit": "TFLOP/s", "frac": round(achieved / peak, 5), "traffic": None,
-                         "flops_per_launch": flops[dom], "avg_launch_ms": round(phase_ms[dom], 5)},
+                         "unit": "TFLOP/s", "frac": round(achieved / peak, 5), "traffic": traffic,
+                         "traffic_source": traffic_src, "flops_per_launch": flops[dom],
+                         "avg_launch_ms": round(phase_ms[dom], 5),
+                         "timing": "hipEvents around the kernel on its launch stream, 100 steps"},
             "losses_last": [round(x, 6) for x in losses],
         }
         if world == 1 and not args.no_cpu_baseline:
