@@ -189,7 +189,7 @@ static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
   const int B = c->batch, Bp = rup(B, 32), nrt = (B + SAC_ROWS - 1) / SAC_ROWS, Br = nrt * SAC_ROWS;
   const int O = c->obs_dim, A = c->act_dim;
   Layout lay;
-  const size_t o_E = lay.take(3072);  // EngineDev, padded for prefetch_engine()
+  const size_t o_E = lay.take(4096);  // EngineDev, padded for prefetch_engine()
   EngineDev h;
   memset(&h, 0, sizeof(h));
   auto P = [&](size_t o) -> void* { return base ? (void*)(base + o) : nullptr; };
@@ -224,9 +224,12 @@ static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
         if (ni == NET_Q2 && l == 0) {
           ly.XT = P(xt_q0);
         } else {
-          const size_t o = lay.take((size_t)ly.Kp * Bp * esz);
+          // pi: two copies by step parity (phase D of step k reads one while
+          // phase A of step k + 1 writes the other when they share a launch)
+          const size_t o = lay.take((size_t)ly.Kp * Bp * esz * (is_pi ? 2 : 1));
           if (ni == NET_Q1 && l == 0) xt_q0 = o;
           ly.XT = P(o);
+          ly.xt_par = is_pi ? (long)ly.Kp * Bp : 0;
         }
         ly.GT = P(lay.take((size_t)ly.Np * Bp * esz));
         ly.dbp = (float*)P(lay.take((size_t)nrt * ly.N * 4));
@@ -236,11 +239,12 @@ static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
   }
   h.s_st = (float*)P(lay.take((size_t)Br * O * 4));
   h.a_st = (float*)P(lay.take((size_t)Br * A * 4));
-  h.lp_st = (float*)P(lay.take((size_t)Br * 4));
+  h.lp_st = (float*)P(lay.take((size_t)2 * Br * 4));
   h.head_st = (float*)P(lay.take((size_t)Br * 4 * A * 4));
-  h.lossp = (float*)P(lay.take((size_t)nrt * 4 * 4));
-  h.adam_sc = (float*)P(lay.take(6 * 4));
-  h.sync = (uint32_t*)P(lay.take((size_t)(64 + HK_COUNT * nrt * 16) * 4));
+  h.lossp = (float*)P(lay.take((size_t)2 * nrt * 4 * 4));
+  h.adam_sc = (float*)P(lay.take(2 * 6 * 4));
+  h.alpha_sc = (double*)P(lay.take(2 * 2 * 8));
+  h.sync = (uint32_t*)P(lay.take((size_t)(SYNC_FLAGS + HK_COUNT * nrt * 16) * 4));
   h.hand = (float*)P(lay.take((size_t)HK_COUNT * nrt * SAC_HAND_STRIDE * 4));
   int nB = 0, nD = 0;
   for (int ni = NET_PI; ni <= NET_Q2; ++ni)
@@ -377,6 +381,7 @@ static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
               t.tWc = tn.l[l].Wc;
             }
             t.dbp = ly.dbp;
+            t.xt_par = ly.xt_par;
             t.K = ly.K;
             t.N = ly.N;
             t.Kp = ly.Kp;

@@ -18,6 +18,7 @@ struct LayerDev {
   float* dbp;     // [nrt][N] bias-gradient partial sums per row tile
   float* pstash;  // pi only: pre-activations of the actor rows [Br][Np]
   const float* bias;  // = net P + b_off (fp32 master bias [N])
+  long xt_par;        // pi only: element offset of the second (odd-step) X^T copy
 };
 
 struct NetDev {
@@ -44,14 +45,19 @@ struct EngineDev {
   NetDev net[5];
   float* s_st;     // [Br][O]   states of the batch (phase A -> C)
   float* a_st;     // [Br][A]   actor sample a~
-  float* lp_st;    // [Br]      log pi(a~|s)
+  float* lp_st;    // [2][Br]   log pi(a~|s), by step parity
   float* head_st;  // [Br][4][A]: mu, log_std (raw), z, eps
-  float* lossp;    // [nrt][4]
+  float* lossp;    // [2][nrt][4] per-row-tile loss partials, by step parity
   double* alpha_state;
   double* opt_steps;
-  float* adam_sc;     // [3][2]: -lr/bias_correction1, sqrt(bias_correction2) of this step (pi, q1, q2)
+  // Per-step scalars are double-buffered by step parity (rng_step & 1) so an
+  // update phase of step k may run beside phase A of step k + 1.
+  float* adam_sc;      // [2][3][2]: -lr/bias_correction1, sqrt(bias_correction2) (pi, q1, q2)
+  double* alpha_sc;    // [2][2]: bias_correction1, bias_correction2 of the alpha optimizer
   uint64_t* rng_step;
-  uint32_t* sync;  // [0] launch epoch (phase D advances it), [1] hand-off timeout flag, [64 + 16 k] flags
+  // [0] launch epoch, [1] hand-off timeout flag, [SYNC_*] counters (one 64-B
+  // line each), [SYNC_FLAGS + 16 k] hand-off flags
+  uint32_t* sync;
   float* hand;     // hand-off payloads [HK_COUNT][nrt][SAC_HAND_STRIDE]
   float* stats;
   long long* stamps;  // optional in-kernel timestamps (SAC_STAMPS builds)
@@ -78,6 +84,7 @@ struct TileDesc {
   float* tb;
   void* tWc;
   const float* dbp;
+  long xt_par;     // element offset of the odd-step X^T copy (pi tiles), else 0
   int K, N, Kp, Np, n0, k0, opt, nrt;
 };
 
@@ -104,9 +111,9 @@ struct TileDesc {
 // per-load statement would let the compiler reuse the register while the load
 // is still in flight (it corrupted addresses: illegal-address fault).
 __device__ __forceinline__ void prefetch_engine(const void* p) {
-  static_assert(sizeof(EngineDev) <= 3072, "extend prefetch_engine");
+  static_assert(sizeof(EngineDev) <= 4096, "extend prefetch_engine");
   const uint64_t base = (uint64_t)(uintptr_t)p;  // kernel-argument pointer: already uniform (SGPRs)
-  asm volatile("s_load_dword s95, %0, 0\n\t" "s_load_dword s95, %0, 64\n\t" "s_load_dword s95, %0, 128\n\t" "s_load_dword s95, %0, 192\n\t" "s_load_dword s95, %0, 256\n\t" "s_load_dword s95, %0, 320\n\t" "s_load_dword s95, %0, 384\n\t" "s_load_dword s95, %0, 448\n\t" "s_load_dword s95, %0, 512\n\t" "s_load_dword s95, %0, 576\n\t" "s_load_dword s95, %0, 640\n\t" "s_load_dword s95, %0, 704\n\t" "s_load_dword s95, %0, 768\n\t" "s_load_dword s95, %0, 832\n\t" "s_load_dword s95, %0, 896\n\t" "s_load_dword s95, %0, 960\n\t" "s_load_dword s95, %0, 1024\n\t" "s_load_dword s95, %0, 1088\n\t" "s_load_dword s95, %0, 1152\n\t" "s_load_dword s95, %0, 1216\n\t" "s_load_dword s95, %0, 1280\n\t" "s_load_dword s95, %0, 1344\n\t" "s_load_dword s95, %0, 1408\n\t" "s_load_dword s95, %0, 1472\n\t" "s_load_dword s95, %0, 1536\n\t" "s_load_dword s95, %0, 1600\n\t" "s_load_dword s95, %0, 1664\n\t" "s_load_dword s95, %0, 1728\n\t" "s_load_dword s95, %0, 1792\n\t" "s_load_dword s95, %0, 1856\n\t" "s_load_dword s95, %0, 1920\n\t" "s_load_dword s95, %0, 1984\n\t" "s_load_dword s95, %0, 2048\n\t" "s_load_dword s95, %0, 2112\n\t" "s_load_dword s95, %0, 2176\n\t" "s_load_dword s95, %0, 2240\n\t" "s_load_dword s95, %0, 2304\n\t" "s_load_dword s95, %0, 2368\n\t" "s_load_dword s95, %0, 2432\n\t" "s_load_dword s95, %0, 2496\n\t" "s_load_dword s95, %0, 2560\n\t" "s_load_dword s95, %0, 2624\n\t" "s_load_dword s95, %0, 2688\n\t" "s_load_dword s95, %0, 2752\n\t" "s_load_dword s95, %0, 2816\n\t" "s_load_dword s95, %0, 2880\n\t" "s_load_dword s95, %0, 2944\n\t" "s_load_dword s95, %0, 3008\n\t" "s_waitcnt lgkmcnt(0)" :: "s"(base) : "s95", "memory");
+  asm volatile("s_load_dword s95, %0, 0\n\t" "s_load_dword s95, %0, 64\n\t" "s_load_dword s95, %0, 128\n\t" "s_load_dword s95, %0, 192\n\t" "s_load_dword s95, %0, 256\n\t" "s_load_dword s95, %0, 320\n\t" "s_load_dword s95, %0, 384\n\t" "s_load_dword s95, %0, 448\n\t" "s_load_dword s95, %0, 512\n\t" "s_load_dword s95, %0, 576\n\t" "s_load_dword s95, %0, 640\n\t" "s_load_dword s95, %0, 704\n\t" "s_load_dword s95, %0, 768\n\t" "s_load_dword s95, %0, 832\n\t" "s_load_dword s95, %0, 896\n\t" "s_load_dword s95, %0, 960\n\t" "s_load_dword s95, %0, 1024\n\t" "s_load_dword s95, %0, 1088\n\t" "s_load_dword s95, %0, 1152\n\t" "s_load_dword s95, %0, 1216\n\t" "s_load_dword s95, %0, 1280\n\t" "s_load_dword s95, %0, 1344\n\t" "s_load_dword s95, %0, 1408\n\t" "s_load_dword s95, %0, 1472\n\t" "s_load_dword s95, %0, 1536\n\t" "s_load_dword s95, %0, 1600\n\t" "s_load_dword s95, %0, 1664\n\t" "s_load_dword s95, %0, 1728\n\t" "s_load_dword s95, %0, 1792\n\t" "s_load_dword s95, %0, 1856\n\t" "s_load_dword s95, %0, 1920\n\t" "s_load_dword s95, %0, 1984\n\t" "s_load_dword s95, %0, 2048\n\t" "s_load_dword s95, %0, 2112\n\t" "s_load_dword s95, %0, 2176\n\t" "s_load_dword s95, %0, 2240\n\t" "s_load_dword s95, %0, 2304\n\t" "s_load_dword s95, %0, 2368\n\t" "s_load_dword s95, %0, 2432\n\t" "s_load_dword s95, %0, 2496\n\t" "s_load_dword s95, %0, 2560\n\t" "s_load_dword s95, %0, 2624\n\t" "s_load_dword s95, %0, 2688\n\t" "s_load_dword s95, %0, 2752\n\t" "s_load_dword s95, %0, 2816\n\t" "s_load_dword s95, %0, 2880\n\t" "s_load_dword s95, %0, 2944\n\t" "s_load_dword s95, %0, 3008\n\t" "s_load_dword s95, %0, 3072\n\t" "s_load_dword s95, %0, 3136\n\t" "s_load_dword s95, %0, 3200\n\t" "s_load_dword s95, %0, 3264\n\t" "s_load_dword s95, %0, 3328\n\t" "s_load_dword s95, %0, 3392\n\t" "s_load_dword s95, %0, 3456\n\t" "s_load_dword s95, %0, 3520\n\t" "s_load_dword s95, %0, 3584\n\t" "s_load_dword s95, %0, 3648\n\t" "s_load_dword s95, %0, 3712\n\t" "s_load_dword s95, %0, 3776\n\t" "s_load_dword s95, %0, 3840\n\t" "s_load_dword s95, %0, 3904\n\t" "s_load_dword s95, %0, 3968\n\t" "s_load_dword s95, %0, 4032\n\t" "s_waitcnt lgkmcnt(0)" :: "s"(base) : "s95", "memory");
 }
 #define PREFETCH_ARG(ptr) prefetch_engine(ptr)
 
@@ -512,10 +519,11 @@ __device__ __forceinline__ void critic_unit_backward(const AS_C EngineDev& E, co
 // indices than their consumers and the grid fits one block per CU, so every
 // spin terminates; spins are still bounded and set E.sync[1] on a timeout.
 enum HandKind { HK_PI = 0, HK_T1 = 1, HK_T2 = 2, HK_C1 = 3, HK_C2 = 4, HK_COUNT = 5 };
+enum SyncWord { SYNC_EPOCH = 0, SYNC_TIMEOUT = 1, SYNC_DDONE = 16, SYNC_BDONE = 32, SYNC_CDONE = 64, SYNC_FLAGS = 128 };
 #define SAC_HAND_STRIDE 576  // floats per (kind, row tile) payload: >= SAC_ROWS * (act_dim + 1)
 
 __device__ __forceinline__ AS_G uint32_t* hand_flag(const AS_C EngineDev& E, int kind, int rbi) {
-  return GP(uint32_t, E.sync) + 64 + (kind * E.nrt + rbi) * 16;  // one 64-B line per flag
+  return GP(uint32_t, E.sync) + SYNC_FLAGS + (kind * E.nrt + rbi) * 16;  // one 64-B line per flag
 }
 __device__ __forceinline__ AS_G float* hand_data(const AS_C EngineDev& E, int kind, int rbi) {
   return GP(float, E.hand) + (size_t)(kind * E.nrt + rbi) * SAC_HAND_STRIDE;
@@ -628,19 +636,23 @@ __global__ void __launch_bounds__(SAC_THREADS) sac_target_critic(const EngineDev
 
   // optimizer step counters and this step's Adam bias-correction scalars
   // (torch adam.py: step_size = lr / (1 - beta1^t), bias_correction2_sqrt), once per step
+  // ---- sample (replay_buffer.py:32-39) + gather (agent.py:166-193); every role
+  // draws the same indices from (seed, step), so no role waits for another's gather
+  const uint64_t step = *GPC(uint64_t, E.rng_step);
+  const int par = (int)(step & 1);  // step parity: selects the double-buffered per-step state
   if ((!ROLES || role == 0) && rbi == 0 && tid < 4 && (tid < 3 || E.auto_entropy)) {
     const double t = GP(double, E.opt_steps)[tid] + 1.0;
     GP(double, E.opt_steps)[tid] = t;
     if (tid < 3) {
       const double lr = tid == 0 ? E.actor_lr : E.critic_lr;
-      GP(float, E.adam_sc)[tid * 2] = (float)(-(lr / (1.0 - pow((double)E.beta1, t))));
-      GP(float, E.adam_sc)[tid * 2 + 1] = (float)sqrt(1.0 - pow((double)E.beta2, t));
+      GP(float, E.adam_sc)[par * 6 + tid * 2] = (float)(-(lr / (1.0 - pow((double)E.beta1, t))));
+      GP(float, E.adam_sc)[par * 6 + tid * 2 + 1] = (float)sqrt(1.0 - pow((double)E.beta2, t));
+    } else {
+      GP(double, E.alpha_sc)[par * 2] = 1.0 - pow((double)E.beta1, t);
+      GP(double, E.alpha_sc)[par * 2 + 1] = 1.0 - pow((double)E.beta2, t);
     }
   }
 
-  // ---- sample (replay_buffer.py:32-39) + gather (agent.py:166-193); every role
-  // draws the same indices from (seed, step), so no role waits for another's gather
-  const uint64_t step = *GPC(uint64_t, E.rng_step);
   const int64_t rb_size = GPC(int64_t, rb.state)[0], rb_pos = GPC(int64_t, rb.state)[1];
   if (tid < R) {
     int64_t slot = -1;
@@ -718,7 +730,8 @@ __global__ void __launch_bounds__(SAC_THREADS) sac_target_critic(const EngineDev
     lf* Y = Yb;
     for (int l = 0; l < pi.L; ++l) {
       const AS_C LayerDev& Ly = pi.l[l];
-      if (act) store_T<T, R>(X + a0 * ld, ld, Ly.Kp, Ly.K, Ly.XT, Bp, r0, nvalid, nullptr);  // actor rows' input
+      if (act)  // actor rows' input, into this step's parity copy
+        store_T<T, R>(X + a0 * ld, ld, Ly.Kp, Ly.K, (T*)Ly.XT + par * Ly.xt_par, Bp, r0, nvalid, nullptr);
       if (l == 0) STAMP(57);
       float* stash = act ? Ly.pstash + (size_t)r0 * Ly.Np : nullptr;
       if (l == pi.L - 1)
@@ -775,7 +788,7 @@ __global__ void __launch_bounds__(SAC_THREADS) sac_target_critic(const EngineDev
       if (live && j == 0) {
         const float v = lp - corr;
         if (actor) {
-          GP(float, E.lp_st)[b] = v;
+          GP(float, E.lp_st)[par * E.Br + b] = v;
           if (b < B) stats[4 + B + b] = v;
         } else {
           lp2B[rr] = v;
@@ -896,7 +909,7 @@ __global__ void __launch_bounds__(SAC_THREADS) sac_target_critic(const EngineDev
           qtB[tid] = v ? (2.0f / (float)B) * d : 0.f;  // the row's seed
         }
         sq = wave_sum(sq);
-        if (tid == 0) GP(float, E.lossp)[rbi * 4 + qi] = sq;
+        if (tid == 0) GP(float, E.lossp)[(par * E.nrt + rbi) * 4 + qi] = sq;
       }
       __syncthreads();
       STAMP(15);
@@ -921,7 +934,7 @@ __global__ void __launch_bounds__(SAC_THREADS) sac_target_critic(const EngineDev
 // dQ_i/da~) to the pi role, which applies the min-Q weights -1/B, -1/2B or 0
 // (powers of two for power-of-two batches: bit-identical to seeding them).
 template <typename T, bool ROLES>
-__global__ void __launch_bounds__(SAC_THREADS) sac_actor(const EngineDev* __restrict__ Ep) {
+__device__ __forceinline__ void actor_body(const EngineDev* __restrict__ Ep) {
   PREFETCH_ARG(Ep);
   const AS_C EngineDev& E = *(const AS_C EngineDev*)Ep;
   extern __shared__ float lds_raw[];
@@ -943,6 +956,7 @@ __global__ void __launch_bounds__(SAC_THREADS) sac_actor(const EngineDev* __rest
   const int r0 = rbi * R;
   const int nvalid = min(R, B - r0);
   const uint32_t ep = ROLES ? *GPC(uint32_t, E.sync) + 1u : 0u;
+  const int par = (int)(*GPC(uint64_t, E.rng_step) & 1);  // advanced by the last block of this phase
   lf* Xb = lds + E.o_X;
   lf* Yb = lds + E.o_Y;
   lf* sB = lds + E.o_s;
@@ -968,7 +982,7 @@ __global__ void __launch_bounds__(SAC_THREADS) sac_actor(const EngineDev* __rest
   }
   if (do_pi) {
     for (int i = tid; i < R * A; i += SAC_THREADS) gaB[i] = 0.f;
-    if (tid < R) lpB[tid] = GPC(float, E.lp_st)[r0 + tid];
+    if (tid < R) lpB[tid] = GPC(float, E.lp_st)[par * E.Br + r0 + tid];
   }
   __syncthreads();
 
@@ -1017,7 +1031,7 @@ __global__ void __launch_bounds__(SAC_THREADS) sac_actor(const EngineDev* __rest
       }
       if (!ROLES) {
         term = wave_sum(term);
-        if (tid == 0) GP(float, E.lossp)[rbi * 4 + 2] = term;
+        if (tid == 0) GP(float, E.lossp)[(par * E.nrt + rbi) * 4 + 2] = term;
       }
     }
     __syncthreads();
@@ -1070,7 +1084,7 @@ __global__ void __launch_bounds__(SAC_THREADS) sac_actor(const EngineDev* __rest
         g2B[tid] = (q1 == q2) ? gm * 0.5f : (q1 < q2 ? 0.f : gm);
       }
       term = wave_sum(term);
-      if (tid == 0) GP(float, E.lossp)[rbi * 4 + 2] = term;
+      if (tid == 0) GP(float, E.lossp)[(par * E.nrt + rbi) * 4 + 2] = term;
     }
     __syncthreads();
     for (int i = tid; i < R * A; i += SAC_THREADS) {
@@ -1123,6 +1137,27 @@ __global__ void __launch_bounds__(SAC_THREADS) sac_actor(const EngineDev* __rest
   STAMP(35);
 }
 
+// The last block of phase C to finish advances the step: RNG step, hand-off
+// epoch, and resets the completion counters (every reader of those words ran
+// earlier in this launch or runs in a later one).
+__device__ __forceinline__ void phase_c_done(const AS_C EngineDev& E) {
+  if (threadIdx.x != 0) return;
+  uint32_t* sync = (uint32_t*)E.sync;
+  const uint32_t old = __hip_atomic_fetch_add(sync + SYNC_CDONE, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (old == gridDim.x - 1) {
+    *GP(uint64_t, E.rng_step) += 1;
+    sync[SYNC_EPOCH] += 1u;
+    sync[SYNC_CDONE] = 0u;
+    sync[SYNC_DDONE] = 0u;
+  }
+}
+
+template <typename T, bool ROLES>
+__global__ void __launch_bounds__(SAC_THREADS) sac_actor(const EngineDev* __restrict__ Ep) {
+  actor_body<T, ROLES>(Ep);
+  phase_c_done(*(const AS_C EngineDev*)Ep);
+}
+
 // ============================================================================ phases B / D
 __device__ __forceinline__ float adam_elem(float& p, float& m, float& v, float g, float w1, float b2, float w2,
                                            float bc2s, float eps, float neg_step) {
@@ -1148,7 +1183,7 @@ __device__ __forceinline__ float adam_elem(float& p, float& m, float& v, float g
 #define SAC_UPD_THREADS 1024
 #define SAC_UPD_BCH (512 / (int)sizeof(T))  // batch columns staged per chunk (512 B per row)
 template <typename T>
-__device__ __forceinline__ void dw_adam_tile(const AS_C EngineDev& E, const TileDesc* tdp_, bool polyak) {
+__device__ __forceinline__ void dw_adam_tile(const AS_C EngineDev& E, const TileDesc* tdp_, bool polyak, int par) {
   constexpr int KC = MM<T>::KC, KL = MM<T>::KL;
   constexpr int EPR = 16 / sizeof(T);  // elements per 16-B piece
   __shared__ float red[32][9];
@@ -1161,8 +1196,8 @@ __device__ __forceinline__ void dw_adam_tile(const AS_C EngineDev& E, const Tile
   const int lds_row = SAC_UPD_BCH + 16 / (int)sizeof(T);  // +16 B per row: rows start on different banks
   AS_L T* stage = (AS_L T*)stage_raw;
   // this step's Adam scalars (written by phase A)
-  const float neg_step = GPC(float, E.adam_sc)[td.opt * 2];
-  const float bc2s = GPC(float, E.adam_sc)[td.opt * 2 + 1];
+  const float neg_step = GPC(float, E.adam_sc)[par * 6 + td.opt * 2];
+  const float bc2s = GPC(float, E.adam_sc)[par * 6 + td.opt * 2 + 1];
   // ---- 1. loads: element state + bias state + staged operands
   AS_G float* W = GP(float, td.W);
   AS_G float* Wm = GP(float, td.Wm);
@@ -1197,7 +1232,8 @@ __device__ __forceinline__ void dw_adam_tile(const AS_C EngineDev& E, const Tile
     const int per_row = bch / EPR;  // 16-B pieces per operand row of this chunk
     for (int i = tid; i < 64 * per_row; i += SAC_UPD_THREADS) {
       const int row = i / per_row, pc = i % per_row;
-      const AS_G T* src = row < 32 ? GPC(T, td.GT) + (size_t)row * Bp : GPC(T, td.XT) + (size_t)(row - 32) * Bp;
+      const AS_G T* src = row < 32 ? GPC(T, td.GT) + (size_t)row * Bp
+                                   : GPC(T, td.XT) + par * td.xt_par + (size_t)(row - 32) * Bp;
       *(AS_L u32x4*)(stage + row * lds_row + pc * EPR) = *(const AS_G u32x4*)(src + b0 + pc * EPR);
     }
     __syncthreads();
@@ -1257,10 +1293,10 @@ template <typename T>
 __global__ void __launch_bounds__(SAC_UPD_THREADS) sac_critic_update(const EngineDev* __restrict__ Ep,
                                                          const TileDesc* __restrict__ tiles) {
   const AS_C EngineDev& E = *(const AS_C EngineDev*)Ep;
-  dw_adam_tile<T>(E, tiles + blockIdx.x, true);
+  dw_adam_tile<T>(E, tiles + blockIdx.x, true, (int)(*GPC(uint64_t, E.rng_step) & 1));
 }
 
-__device__ __forceinline__ void alpha_and_losses(const AS_C EngineDev& E) {
+__device__ __forceinline__ void alpha_and_losses(const AS_C EngineDev& E, int par) {
   __shared__ float red[5][256];
   const int tid = threadIdx.x, B = E.B;
   if (tid >= 256) return;  // whole waves leave: the barriers below count waves 0-3
@@ -1268,8 +1304,8 @@ __device__ __forceinline__ void alpha_and_losses(const AS_C EngineDev& E) {
   AS_G double* st = GP(double, E.alpha_state);
   const float la32 = (float)st[0];
   const float mB = -1.0f / (float)B;
-  const AS_G float* lp = GPC(float, E.lp_st);
-  const AS_G float* lossp = GPC(float, E.lossp);
+  const AS_G float* lp = GPC(float, E.lp_st) + par * E.Br;
+  const AS_G float* lossp = GPC(float, E.lossp) + par * E.nrt * 4;
   float sg = 0.f, sl = 0.f, l0 = 0.f, l1 = 0.f, l2 = 0.f;
   for (int b = tid; b < B; b += 256) {
     const float term = lp[b] + H;
@@ -1303,8 +1339,7 @@ __device__ __forceinline__ void alpha_and_losses(const AS_C EngineDev& E) {
       const double b1 = (double)E.beta1, b2 = (double)E.beta2;
       const double m = st[2] + (1.0 - b1) * (gr - st[2]);
       const double v = st[3] * b2 + (1.0 - b2) * gr * gr;
-      const double t = GPC(double, E.opt_steps)[3];
-      const double bc1 = 1.0 - pow(b1, t), bc2 = 1.0 - pow(b2, t);
+      const double bc1 = GPC(double, E.alpha_sc)[par * 2], bc2 = GPC(double, E.alpha_sc)[par * 2 + 1];
       const double denom = sqrt(v) / sqrt(bc2) + (double)E.adam_eps;
       const double la = st[0] + (-(E.alpha_lr / bc1)) * m / denom;
       st[0] = la;
@@ -1314,8 +1349,6 @@ __device__ __forceinline__ void alpha_and_losses(const AS_C EngineDev& E) {
     } else {
       stats[3] = __builtin_nanf("");
     }
-    *GP(uint64_t, E.rng_step) += 1;
-    *GP(uint32_t, E.sync) += 1u;  // next launch epoch of the role hand-offs
   }
 }
 
@@ -1323,10 +1356,11 @@ template <typename T>
 __global__ void __launch_bounds__(SAC_UPD_THREADS) sac_actor_update(const EngineDev* __restrict__ Ep, const TileDesc* __restrict__ tiles,
                                                         int ntiles) {
   const AS_C EngineDev& E = *(const AS_C EngineDev*)Ep;
+  const int par = (int)((*GPC(uint64_t, E.rng_step) - 1) & 1);  // phase C already advanced the step
   if ((int)blockIdx.x < ntiles)
-    dw_adam_tile<T>(E, tiles + blockIdx.x, false);
+    dw_adam_tile<T>(E, tiles + blockIdx.x, false, par);
   else
-    alpha_and_losses(E);
+    alpha_and_losses(E, par);
 }
 
 // ============================================================================ policy
