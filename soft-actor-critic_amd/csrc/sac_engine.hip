@@ -418,7 +418,7 @@ static void launch_phase(sac_engine* e, int phase, const sac_replay* rb, const i
         sac_target_critic<T, false><<<e->nrt * e->h.xs, SAC_THREADS, e->lds_bytes, s>>>(e->d, *rb, idx, eps);
       break;
     case 1:
-      sac_critic_update<T><<<e->nB, SAC_UPD_THREADS, 64 * (512 + 16), s>>>(e->d, e->tilesB);
+      sac_critic_update<T><<<e->nB, SAC_UPD_THREADS, SAC_UPD_LDS, s>>>(e->d, e->tilesB);
       break;
     case 2:
       if (e->h.roles)
@@ -427,7 +427,7 @@ static void launch_phase(sac_engine* e, int phase, const sac_replay* rb, const i
         sac_actor<T, false><<<e->nrt * e->h.xs, SAC_THREADS, e->lds_bytes, s>>>(e->d);
       break;
     case 3:
-      sac_actor_update<T><<<e->nD + 1, SAC_UPD_THREADS, 64 * (512 + 16), s>>>(e->d, e->tilesD, e->nD);
+      sac_actor_update<T><<<e->nD + 1, SAC_UPD_THREADS, SAC_UPD_LDS, s>>>(e->d, e->tilesD, e->nD);
       break;
   }
 }

@@ -1172,29 +1172,62 @@ __device__ __forceinline__ float adam_elem(float& p, float& m, float& v, float g
   return pn;
 }
 
-// One 32x32 weight tile of an update phase, 16 waves:
+// Coherent (sc1) 16-B accesses: what a workgroup of the SAME launch on any XCD
+// reads after a counter / flag hand-off (MI355X_MICROARCH.md §visibility: every
+// store of the handed-off bytes sc1 + drained, every load of them sc1).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t coh_rsrc(const void* base, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ void coh_store16(const void* base, uint32_t byte_off, u32x4 v) {
+  // uniform descriptor (base only): a per-lane bound would force a waterfall loop
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, v),
+                                         coh_rsrc(base, 0xFFFFFFF0u), (int)byte_off, 0, 16);
+}
+__device__ __forceinline__ float coh_load(const float* p) {
+  return __hip_atomic_load((float*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void coh_storef(float* p, float v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// all threads: drain this workgroup's stores, then one lane counts the block done
+__device__ __forceinline__ void count_done(uint32_t* counter) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// One 32x32 weight tile of an update phase, UT threads:
 //   1. all threads stage the tile's 32 dY^T rows and 32 X^T rows (the dW GEMM's
-//      operands, K = batch) into LDS and fetch their own element's master weight,
+//      operands, K = batch) into LDS and fetch their elements' master weight,
 //      Adam moments, target weight and bias state, all in one round trip;
 //   2. waves 0-3 run the dW MFMAs (one 16x16 sub-tile each, batch chunks in
 //      order: the same summation order as before the staging);
-//   3. every thread updates ONE element: Adam (torch single-tensor op order),
-//      Polyak, master + packed compute copies.
+//   3. every thread updates 1024 / UT elements: Adam (torch single-tensor op
+//      order), Polyak, master weights; the packed compute copies are written
+//      from LDS as whole 16-B fragment pieces with sc1 stores, so a phase that
+//      shares the launch can read them after the completion counter.
 #define SAC_UPD_THREADS 1024
 #define SAC_UPD_BCH (512 / (int)sizeof(T))  // batch columns staged per chunk (512 B per row)
-template <typename T>
-__device__ __forceinline__ void dw_adam_tile(const AS_C EngineDev& E, const TileDesc* tdp_, bool polyak, int par) {
+// dynamic LDS of an update tile: stage 64 x 528 B | 2 x [32][33] f32 | [32][9] f32
+// (>= the alpha block's 5 x 1024 floats)
+#define SAC_UPD_LDS (64 * 528 + 2 * 32 * 33 * 4 + 32 * 9 * 4)
+template <typename T, int UT>
+__device__ __forceinline__ void dw_adam_tile(const AS_C EngineDev& E, const TileDesc* tdp_, bool polyak, int par,
+                                             lf* lds) {
   constexpr int KC = MM<T>::KC, KL = MM<T>::KL;
-  constexpr int EPR = 16 / sizeof(T);  // elements per 16-B piece
-  __shared__ float red[32][9];
-  __shared__ float accs[32][33];
-  extern __shared__ float stage_raw[];  // [64 rows][Bp + pad] of T: rows 0-31 dY^T, 32-63 X^T
+  constexpr int EPR = 16 / sizeof(T);  // elements per 16-B piece (= KL)
+  constexpr int EPT = 1024 / UT;       // elements per thread
+  static_assert(EPR == KL, "a piece is one lane's fragment slice");
   const AS_C TileDesc& td = *(const AS_C TileDesc*)tdp_;  // scalar loads
   STAMP(polyak ? 48 : 52);
   const int tid = threadIdx.x;
   const int Bp = E.Bp;
+  // LDS: stage [64][SAC_UPD_BCH + pad] of T | acc / new params [32][33] f32 | targets [32][33] | bias reduce [32][9]
   const int lds_row = SAC_UPD_BCH + 16 / (int)sizeof(T);  // +16 B per row: rows start on different banks
-  AS_L T* stage = (AS_L T*)stage_raw;
+  AS_L T* stage = (AS_L T*)lds;
+  lf* accs = lds + (64 * lds_row * (int)sizeof(T) + 15) / 16 * 4;
+  lf* tgts = accs + 32 * 33;
+  lf* red = tgts + 32 * 33;
   // this step's Adam scalars (written by phase A)
   const float neg_step = GPC(float, E.adam_sc)[par * 6 + td.opt * 2];
   const float bc2s = GPC(float, E.adam_sc)[par * 6 + td.opt * 2 + 1];
@@ -1203,12 +1236,20 @@ __device__ __forceinline__ void dw_adam_tile(const AS_C EngineDev& E, const Tile
   AS_G float* Wm = GP(float, td.Wm);
   AS_G float* Wv = GP(float, td.Wv);
   AS_G float* tW = GP(float, td.tW);
-  const int en = tid >> 5, ek = tid & 31;  // this thread's element (n0 + en, k0 + ek)
-  const int n = td.n0 + en, k = td.k0 + ek;
-  const bool ok = n < td.N && k < td.K;
-  const size_t idx = ok ? (size_t)n * td.K + k : 0;
-  float p = W[idx], m = Wm[idx], v = Wv[idx];
-  const float tp = polyak ? tW[idx] : 0.f;
+  float p[EPT], m[EPT], v[EPT], tp[EPT];
+  size_t idx[EPT];
+  bool ok[EPT];
+#pragma unroll
+  for (int e = 0; e < EPT; ++e) {
+    const int el = tid + e * UT, en = el >> 5, ek = el & 31;  // element (n0 + en, k0 + ek)
+    const int n = td.n0 + en, k = td.k0 + ek;
+    ok[e] = n < td.N && k < td.K;
+    idx[e] = ok[e] ? (size_t)n * td.K + k : 0;
+    p[e] = W[idx[e]];
+    m[e] = Wm[idx[e]];
+    v[e] = Wv[idx[e]];
+    tp[e] = polyak ? tW[idx[e]] : 0.f;
+  }
   const bool do_bias = td.k0 == 0;
   float pb = 0.f, mb = 0.f, vb = 0.f, tbv = 0.f;
   if (do_bias && tid < 32 && td.n0 + tid < td.N) {
@@ -1230,7 +1271,7 @@ __device__ __forceinline__ void dw_adam_tile(const AS_C EngineDev& E, const Tile
   for (int b0 = 0; b0 < Bp; b0 += SAC_UPD_BCH) {
     const int bch = Bp - b0 < SAC_UPD_BCH ? Bp - b0 : SAC_UPD_BCH;
     const int per_row = bch / EPR;  // 16-B pieces per operand row of this chunk
-    for (int i = tid; i < 64 * per_row; i += SAC_UPD_THREADS) {
+    for (int i = tid; i < 64 * per_row; i += UT) {
       const int row = i / per_row, pc = i % per_row;
       const AS_G T* src = row < 32 ? GPC(T, td.GT) + (size_t)row * Bp
                                    : GPC(T, td.XT) + par * td.xt_par + (size_t)(row - 32) * Bp;
@@ -1257,35 +1298,68 @@ __device__ __forceinline__ void dw_adam_tile(const AS_C EngineDev& E, const Tile
   STAMP(polyak ? 49 : 53);
   if (wave < 4) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) accs[ns + g * 4 + i][ks + c] = acc[i];
+    for (int i = 0; i < 4; ++i) accs[(ns + g * 4 + i) * 33 + ks + c] = acc[i];
   }
-  if (do_bias && tid < 256) red[bn][bs] = bsum;
+  if (do_bias && tid < 256) red[bn * 9 + bs] = bsum;
   __syncthreads();
   STAMP(polyak ? 50 : 54);
-  // ---- 3. one element per thread
+  // ---- 3. elements: Adam + Polyak on the masters; new values -> LDS
   const float w1 = (float)(1.0 - (double)E.beta1), b2 = E.beta2, w2 = (float)(1.0 - (double)E.beta2);
   const float eps = E.adam_eps, tau = E.tau, omt = (float)(1.0 - (double)E.tau);
-  if (ok) {
-    const float pn = adam_elem(p, m, v, accs[en][ek], w1, b2, w2, bc2s, eps, neg_step);
-    W[idx] = p;
-    Wm[idx] = m;
-    Wv[idx] = v;
-    GP(T, td.Wc)[packed_off<T>(n, k, td.Kp)] = MM<T>::cvt(pn);
-    GP(T, td.WTc)[packed_off<T>(k, n, td.Np)] = MM<T>::cvt(pn);
-    if (polyak) {
-      const float tn = tau * pn + omt * tp;
-      tW[idx] = tn;
-      GP(T, td.tWc)[packed_off<T>(n, k, td.Kp)] = MM<T>::cvt(tn);
+  float pn[EPT], tn[EPT];
+#pragma unroll
+  for (int e = 0; e < EPT; ++e) {
+    const int el = tid + e * UT;
+    pn[e] = 0.f;
+    tn[e] = 0.f;
+    if (ok[e]) {
+      pn[e] = adam_elem(p[e], m[e], v[e], accs[(el >> 5) * 33 + (el & 31)], w1, b2, w2, bc2s, eps, neg_step);
+      W[idx[e]] = p[e];
+      Wm[idx[e]] = m[e];
+      Wv[idx[e]] = v[e];
+      if (polyak) {
+        tn[e] = tau * pn[e] + omt * tp[e];
+        tW[idx[e]] = tn[e];
+      }
     }
+  }
+  __syncthreads();  // every read of accs done
+#pragma unroll
+  for (int e = 0; e < EPT; ++e) {
+    const int el = tid + e * UT;
+    accs[(el >> 5) * 33 + (el & 31)] = pn[e];  // padding elements: 0, as packed
+    if (polyak) tgts[(el >> 5) * 33 + (el & 31)] = tn[e];
   }
   if (do_bias && tid < 32 && td.n0 + tid < td.N) {
     float gb = 0.f;
-    for (int q = 0; q < 8; ++q) gb += red[tid][q];
-    const float pn = adam_elem(pb, mb, vb, gb, w1, b2, w2, bc2s, eps, neg_step);
-    GP(float, td.b)[td.n0 + tid] = pb;
+    for (int q = 0; q < 8; ++q) gb += red[tid * 9 + q];
+    const float pbn = adam_elem(pb, mb, vb, gb, w1, b2, w2, bc2s, eps, neg_step);
+    coh_storef((float*)td.b + td.n0 + tid, pb);
     GP(float, td.bm)[td.n0 + tid] = mb;
     GP(float, td.bv)[td.n0 + tid] = vb;
-    if (polyak) GP(float, td.tb)[td.n0 + tid] = tau * pn + omt * tbv;
+    if (polyak) GP(float, td.tb)[td.n0 + tid] = tau * pbn + omt * tbv;
+  }
+  __syncthreads();
+  // ---- packed copies as 16-B pieces: Wc / tWc rows n (EPR consecutive k), WTc rows k
+  constexpr int PPR = 32 / EPR;  // pieces per 32-element tile row
+  for (int mat = 0; mat < (polyak ? 3 : 2); ++mat) {  // uniform: one buffer descriptor per matrix
+    const void* base = mat == 0 ? td.Wc : mat == 1 ? td.WTc : td.tWc;
+    for (int i = tid; i < 32 * PPR; i += UT) {
+      const int row = i / PPR, pc = i % PPR;
+      T vv[EPR];
+      size_t off;
+      if (mat == 1) {  // W^T: row k = k0 + row, columns n = n0 + pc * EPR + j
+#pragma unroll
+        for (int j = 0; j < EPR; ++j) vv[j] = MM<T>::cvt(accs[(pc * EPR + j) * 33 + row]);
+        off = packed_off<T>(td.k0 + row, td.n0 + pc * EPR, td.Np);
+      } else {  // W or target W: row n = n0 + row, columns k = k0 + pc * EPR + j
+        const lf* srcm = mat == 0 ? accs : tgts;
+#pragma unroll
+        for (int j = 0; j < EPR; ++j) vv[j] = MM<T>::cvt(srcm[row * 33 + pc * EPR + j]);
+        off = packed_off<T>(td.n0 + row, td.k0 + pc * EPR, td.Kp);
+      }
+      coh_store16(base, (uint32_t)(off * sizeof(T)), *(const u32x4*)vv);
+    }
   }
 }
 
@@ -1293,13 +1367,19 @@ template <typename T>
 __global__ void __launch_bounds__(SAC_UPD_THREADS) sac_critic_update(const EngineDev* __restrict__ Ep,
                                                          const TileDesc* __restrict__ tiles) {
   const AS_C EngineDev& E = *(const AS_C EngineDev*)Ep;
-  dw_adam_tile<T>(E, tiles + blockIdx.x, true, (int)(*GPC(uint64_t, E.rng_step) & 1));
+  extern __shared__ float upd_lds[];
+  dw_adam_tile<T, SAC_UPD_THREADS>(E, tiles + blockIdx.x, true, (int)(*GPC(uint64_t, E.rng_step) & 1),
+                                   (lf*)upd_lds);
+  count_done((uint32_t*)E.sync + SYNC_BDONE + 16 * (tiles[blockIdx.x].opt - 1));
 }
 
-__device__ __forceinline__ void alpha_and_losses(const AS_C EngineDev& E, int par) {
-  __shared__ float red[5][256];
-  const int tid = threadIdx.x, B = E.B;
-  if (tid >= 256) return;  // whole waves leave: the barriers below count waves 0-3
+// One block: reduces the step's loss partials into stats[0..3] and runs the
+// float64 alpha Adam step (agent.py:263-280).  All blockDim.x threads take part
+// (no early exit: the caller's completion barrier follows).  alpha_state is
+// stored sc1: the critics of a phase A sharing the launch read alpha after the
+// completion counter.
+__device__ __forceinline__ void alpha_and_losses(const AS_C EngineDev& E, int par, lf* red) {
+  const int tid = threadIdx.x, NT = blockDim.x, B = E.B;
   const float H = E.target_entropy;
   AS_G double* st = GP(double, E.alpha_state);
   const float la32 = (float)st[0];
@@ -1307,45 +1387,46 @@ __device__ __forceinline__ void alpha_and_losses(const AS_C EngineDev& E, int pa
   const AS_G float* lp = GPC(float, E.lp_st) + par * E.Br;
   const AS_G float* lossp = GPC(float, E.lossp) + par * E.nrt * 4;
   float sg = 0.f, sl = 0.f, l0 = 0.f, l1 = 0.f, l2 = 0.f;
-  for (int b = tid; b < B; b += 256) {
+  for (int b = tid; b < B; b += NT) {
     const float term = lp[b] + H;
     sg += mB * term;
     sl += la32 * term;
   }
-  for (int rt = tid; rt < E.nrt; rt += 256) {
+  for (int rt = tid; rt < E.nrt; rt += NT) {
     l0 += lossp[rt * 4 + 0];
     l1 += lossp[rt * 4 + 1];
     l2 += lossp[rt * 4 + 2];
   }
-  red[0][tid] = sg;
-  red[1][tid] = sl;
-  red[2][tid] = l0;
-  red[3][tid] = l1;
-  red[4][tid] = l2;
+  red[0 * NT + tid] = sg;
+  red[1 * NT + tid] = sl;
+  red[2 * NT + tid] = l0;
+  red[3 * NT + tid] = l1;
+  red[4 * NT + tid] = l2;
   __syncthreads();
-  for (int s = 128; s > 0; s >>= 1) {
+  for (int s = NT / 2; s > 0; s >>= 1) {
     if (tid < s)
-      for (int j = 0; j < 5; ++j) red[j][tid] += red[j][tid + s];
+      for (int j = 0; j < 5; ++j) red[j * NT + tid] += red[j * NT + tid + s];
     __syncthreads();
   }
   if (tid == 0) {
     AS_G float* stats = GP(float, E.stats);
-    stats[0] = red[2][0] / (float)B;
-    stats[1] = red[3][0] / (float)B;
-    stats[2] = red[4][0] / (float)B;
+    stats[0] = red[2 * NT] / (float)B;
+    stats[1] = red[3 * NT] / (float)B;
+    stats[2] = red[4 * NT] / (float)B;
     if (E.auto_entropy) {
-      stats[3] = -(red[1][0] / (float)B);
-      const double gr = (double)red[0][0];
+      stats[3] = -(red[1 * NT] / (float)B);
+      const double gr = (double)red[0];
       const double b1 = (double)E.beta1, b2 = (double)E.beta2;
       const double m = st[2] + (1.0 - b1) * (gr - st[2]);
       const double v = st[3] * b2 + (1.0 - b2) * gr * gr;
       const double bc1 = GPC(double, E.alpha_sc)[par * 2], bc2 = GPC(double, E.alpha_sc)[par * 2 + 1];
       const double denom = sqrt(v) / sqrt(bc2) + (double)E.adam_eps;
       const double la = st[0] + (-(E.alpha_lr / bc1)) * m / denom;
-      st[0] = la;
-      st[1] = exp(la);
-      st[2] = m;
-      st[3] = v;
+      double* sd = (double*)E.alpha_state;
+      __hip_atomic_store(sd + 0, la, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(sd + 1, exp(la), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(sd + 2, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(sd + 3, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     } else {
       stats[3] = __builtin_nanf("");
     }
@@ -1357,10 +1438,12 @@ __global__ void __launch_bounds__(SAC_UPD_THREADS) sac_actor_update(const Engine
                                                         int ntiles) {
   const AS_C EngineDev& E = *(const AS_C EngineDev*)Ep;
   const int par = (int)((*GPC(uint64_t, E.rng_step) - 1) & 1);  // phase C already advanced the step
+  extern __shared__ float upd_lds[];
   if ((int)blockIdx.x < ntiles)
-    dw_adam_tile<T>(E, tiles + blockIdx.x, false, par);
+    dw_adam_tile<T, SAC_UPD_THREADS>(E, tiles + blockIdx.x, false, par, (lf*)upd_lds);
   else
-    alpha_and_losses(E, par);
+    alpha_and_losses(E, par, (lf*)upd_lds);
+  count_done((uint32_t*)E.sync + SYNC_DDONE);
 }
 
 // ============================================================================ policy
