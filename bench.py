@@ -230,6 +230,10 @@ def main():
     # per-phase device time (hipEvents on the launch stream), then roofline of the dominant kernel
     phase_ms = eng.time_phases(rb, 100)
     flops, f_total, _, _ = gemm_flops(c["obs"], c["act"], c["hidden"], c["batch"])
+    if eng.fused:  # D inside the next A launch (and with layout 2, B inside the C launch)
+        flops = [flops[0] + flops[3], flops[1], flops[2], 0]
+        if eng.fused == 2:
+            flops = [flops[0], 0, flops[2] + flops[1], 0]
     dom = int(np.argmax(phase_ms))
     from sac import _engine as E
 

@@ -163,9 +163,11 @@ int sac_replay_gather(const sac_replay *rb, const int32_t *logical_idx, int32_t 
 int sac_replay_sample_indices(const sac_replay *rb, int32_t batch, uint64_t seed,
                               uint64_t step, int32_t *out, void *stream);
 
-/* Profiling: runs n_steps with hipEvents around each phase kernel and returns
- * the mean device time per phase in ms: [0]=A target+critic-backward,
- * [1]=B critic dW+Adam+Polyak, [2]=C actor, [3]=D actor dW+Adam+alpha.
+/* Profiling: runs n_steps with hipEvents after each launch and returns the
+ * mean device time per phase launch in ms: [0]=A target+critic-backward,
+ * [1]=B critic dW+Adam+Polyak, [2]=C actor, [3]=D actor dW+Adam+alpha.  Fused
+ * layouts (sac_engine_phase_layout()): 1 = D shares the next step's A launch
+ * ([0] is that launch, [3] = 0); 2 = also B shares C's launch ([1] = 0).
  * Synchronises the stream. */
 int sac_engine_time_phases(sac_engine *e, const sac_replay *rb, int32_t n_steps,
                            float *ms_host, void *stream);
@@ -174,6 +176,11 @@ int sac_engine_time_phases(sac_engine *e, const sac_replay *rb, int32_t n_steps,
  * workgroup hand-off of the role-split phase kernels gave up waiting (the
  * affected steps are invalid), else 0.  Replaces: nothing (diagnostic). */
 int sac_engine_check(sac_engine *e, void *stream);
+
+/* Launch layout of a step: 0 = four launches (A B C D); 1 = phase D of step
+ * k runs inside phase A's launch of step k + 1 (three launches); 2 = also phase
+ * B inside phase C's launch (two launches). */
+int sac_engine_phase_layout(const sac_engine *e);
 
 /* Phase kernel names as they appear in rocprofv3 kernel traces. */
 const char *sac_phase_kernel_name(int32_t phase);

@@ -142,6 +142,7 @@ struct sac_engine {
   int nB = 0, nD = 0;
   size_t lds_bytes = 0;
   int nrt = 0;
+  int fused = 0;  // 0: A B C D per step; 1: D inside the next A's launch; 2: also B inside C's
   // graph cache
   hipGraphExec_t gexec = nullptr;
   hipGraph_t graph = nullptr;
@@ -350,6 +351,10 @@ static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
     e->tilesD = (TileDesc*)(base + o_tD);
     e->nB = nB;
     e->nD = nD;
+    e->h.tilesB = e->tilesB;
+    e->h.tilesD = e->tilesD;
+    e->h.nB = nB;
+    e->h.nD = nD;
     e->lds_bytes = (size_t)lo * 4;
     e->nrt = nrt;
     // self-contained update tiles (phase B: critics + Polyak, phase D: policy)
@@ -394,51 +399,106 @@ static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
           }
       }
     }
+    e->h.nBq[0] = e->h.nBq[1] = 0;
+    for (const TileDesc& t : e->hostB) ++e->h.nBq[t.opt - 1];
+    {
+      // Fused layouts are exact (tests/test_gpu_engine.py) but measured no faster
+      // on C2: four launches stay the default; SAC_FUSE=1|2 opts in.
+      int fuse = 0;
+      if (const char* v = getenv("SAC_FUSE")) fuse = std::max(0, std::min(2, atoi(v)));
+      if (!e->h.roles || nD + 1 + 6 * nrt > 256) fuse = 0;
+      if (fuse == 2 && nB + 3 * nrt > 256) fuse = 1;
+      e->fused = fuse;
+    }
   }
   return total + 256;
 }
 
 template <typename T>
 static void set_lds_attrs(size_t bytes) {
-  (void)hipFuncSetAttribute((const void*)sac_target_critic<T, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
-  (void)hipFuncSetAttribute((const void*)sac_target_critic<T, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
-  (void)hipFuncSetAttribute((const void*)sac_actor<T, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
-  (void)hipFuncSetAttribute((const void*)sac_actor<T, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
-  (void)hipFuncSetAttribute((const void*)sac_policy_act_kernel<T>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+  const int b = (int)std::max(bytes, (size_t)SAC_UPD_LDS);
+  (void)hipFuncSetAttribute((const void*)sac_target_critic<T, false, false>, hipFuncAttributeMaxDynamicSharedMemorySize, b);
+  (void)hipFuncSetAttribute((const void*)sac_target_critic<T, true, false>, hipFuncAttributeMaxDynamicSharedMemorySize, b);
+  (void)hipFuncSetAttribute((const void*)sac_target_critic<T, true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, b);
+  (void)hipFuncSetAttribute((const void*)sac_actor<T, false, false>, hipFuncAttributeMaxDynamicSharedMemorySize, b);
+  (void)hipFuncSetAttribute((const void*)sac_actor<T, true, false>, hipFuncAttributeMaxDynamicSharedMemorySize, b);
+  (void)hipFuncSetAttribute((const void*)sac_actor<T, true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, b);
+  (void)hipFuncSetAttribute((const void*)sac_policy_act_kernel<T>, hipFuncAttributeMaxDynamicSharedMemorySize, b);
 }
+
+// Launch kinds of a step sequence.  Unfused: A B C D per step.  Fused (role
+// split with every block co-resident): A, then per step BC, and DA for the next
+// step, closed by a D: D(k) shares a launch with A(k + 1), B(k) with C(k).
+enum LaunchKind { L_A = 0, L_B = 1, L_C = 2, L_D = 3, L_DA = 4, L_BC = 5 };
 
 template <typename T>
-static void launch_phase(sac_engine* e, int phase, const sac_replay* rb, const int32_t* idx, const float* eps,
-                         hipStream_t s) {
-  switch (phase) {
-    case 0:
+static void launch_kind(sac_engine* e, int kind, const sac_replay* rb, const int32_t* idx, const float* eps,
+                        hipStream_t s) {
+  const size_t lf = std::max(e->lds_bytes, (size_t)SAC_UPD_LDS);
+  switch (kind) {
+    case L_A:
       if (e->h.roles)
-        sac_target_critic<T, true><<<e->nrt * 6, SAC_THREADS, e->lds_bytes, s>>>(e->d, *rb, idx, eps);
+        sac_target_critic<T, true, false><<<e->nrt * 6, SAC_THREADS, lf, s>>>(e->d, *rb, idx, eps);
       else
-        sac_target_critic<T, false><<<e->nrt * e->h.xs, SAC_THREADS, e->lds_bytes, s>>>(e->d, *rb, idx, eps);
+        sac_target_critic<T, false, false><<<e->nrt * e->h.xs, SAC_THREADS, lf, s>>>(e->d, *rb, idx, eps);
       break;
-    case 1:
+    case L_B:
       sac_critic_update<T><<<e->nB, SAC_UPD_THREADS, SAC_UPD_LDS, s>>>(e->d, e->tilesB);
       break;
-    case 2:
+    case L_C:
       if (e->h.roles)
-        sac_actor<T, true><<<e->nrt * 3, SAC_THREADS, e->lds_bytes, s>>>(e->d);
+        sac_actor<T, true, false><<<e->nrt * 3, SAC_THREADS, lf, s>>>(e->d);
       else
-        sac_actor<T, false><<<e->nrt * e->h.xs, SAC_THREADS, e->lds_bytes, s>>>(e->d);
+        sac_actor<T, false, false><<<e->nrt * e->h.xs, SAC_THREADS, lf, s>>>(e->d);
       break;
-    case 3:
+    case L_D:
       sac_actor_update<T><<<e->nD + 1, SAC_UPD_THREADS, SAC_UPD_LDS, s>>>(e->d, e->tilesD, e->nD);
+      break;
+    case L_DA:
+      sac_target_critic<T, true, true><<<e->nD + 1 + e->nrt * 6, SAC_THREADS, lf, s>>>(e->d, *rb, idx, eps);
+      break;
+    case L_BC:
+      sac_actor<T, true, true><<<e->nB + e->nrt * 3, SAC_THREADS, lf, s>>>(e->d);
       break;
   }
 }
 
-static void launch_step(sac_engine* e, const sac_replay* rb, const int32_t* idx, const float* eps, hipStream_t s) {
-  for (int p = 0; p < 4; ++p) {
+// The launches of n consecutive steps (and, per launch, its kind in *kinds).
+static void launch_steps(sac_engine* e, const sac_replay* rb, int n, const int32_t* indices, const float* eps,
+                         hipStream_t s, std::vector<int>* kinds = nullptr, std::vector<hipEvent_t>* ev = nullptr) {
+  const size_t B = e->cfg.batch, A = e->cfg.act_dim;
+  auto go = [&](int kind, int step) {
+    const int32_t* ix = indices ? indices + (size_t)step * B : nullptr;
+    const float* ep = eps ? eps + (size_t)step * 2 * B * A : nullptr;
     if (e->cfg.precision == SAC_PREC_BF16)
-      launch_phase<bf16>(e, p, rb, idx, eps, s);
+      launch_kind<bf16>(e, kind, rb, ix, ep, s);
     else
-      launch_phase<float>(e, p, rb, idx, eps, s);
+      launch_kind<float>(e, kind, rb, ix, ep, s);
+    if (kinds) kinds->push_back(kind);
+    if (ev) {
+      hipEvent_t x;
+      (void)hipEventCreate(&x);
+      (void)hipEventRecord(x, s);
+      ev->push_back(x);
+    }
+  };
+  if (!e->fused) {
+    for (int i = 0; i < n; ++i)
+      for (int k = L_A; k <= L_D; ++k) go(k, i);
+    return;
   }
+  if (n < 1) return;
+  go(L_A, 0);
+  for (int i = 0; i < n; ++i) {
+    if (e->fused == 2) {
+      go(L_BC, i);
+    } else {
+      go(L_B, i);
+      go(L_C, i);
+    }
+    if (i + 1 < n) go(L_DA, i + 1);
+  }
+  go(L_D, n - 1);
 }
 
 static int check_replay(sac_engine* e, const sac_replay* rb) {
@@ -556,10 +616,7 @@ int sac_engine_train(sac_engine* e, const sac_replay* rb, int32_t n_steps, const
   if (!e) return fail(SAC_E_INVALID, "null engine");
   int rc = check_replay(e, rb);
   if (rc) return rc;
-  hipStream_t s = (hipStream_t)stream;
-  const size_t B = e->cfg.batch, A = e->cfg.act_dim;
-  for (int i = 0; i < n_steps; ++i)
-    launch_step(e, rb, indices ? indices + i * B : nullptr, eps ? eps + (size_t)i * 2 * B * A : nullptr, s);
+  launch_steps(e, rb, n_steps, indices, eps, (hipStream_t)stream);
   HIPCHK(hipGetLastError());
   return SAC_OK;
 }
@@ -578,7 +635,7 @@ int sac_engine_train_graph(sac_engine* e, const sac_replay* rb, int32_t n_steps,
     e->graph = nullptr;
     if (!e->cap) HIPCHK(hipStreamCreateWithFlags(&e->cap, hipStreamNonBlocking));
     HIPCHK(hipStreamBeginCapture(e->cap, hipStreamCaptureModeThreadLocal));
-    for (int i = 0; i < chunk; ++i) launch_step(e, rb, nullptr, nullptr, e->cap);
+    launch_steps(e, rb, chunk, nullptr, nullptr, e->cap);
     HIPCHK(hipStreamEndCapture(e->cap, &e->graph));
     HIPCHK(hipGraphInstantiate(&e->gexec, e->graph, nullptr, nullptr, 0));
     e->gchunk = chunk;
@@ -587,7 +644,7 @@ int sac_engine_train_graph(sac_engine* e, const sac_replay* rb, int32_t n_steps,
   int done = 0;
   if (e->gexec)
     for (; done + chunk <= n_steps; done += chunk) HIPCHK(hipGraphLaunch(e->gexec, s));
-  for (; done < n_steps; ++done) launch_step(e, rb, nullptr, nullptr, s);
+  if (done < n_steps) launch_steps(e, rb, n_steps - done, nullptr, nullptr, s);
   HIPCHK(hipGetLastError());
   return SAC_OK;
 }
@@ -661,6 +718,8 @@ int sac_debug_sample_indices_host(int64_t size, int32_t batch, uint64_t seed, ui
 
 int sac_engine_uses_roles(const sac_engine* e) { return e && e->h.roles ? 1 : 0; }
 
+int sac_engine_phase_layout(const sac_engine* e) { return e ? e->fused : 0; }
+
 int sac_engine_debug_stamped(void) {
 #ifdef SAC_STAMPS
   return 1;
@@ -674,26 +733,34 @@ int sac_engine_time_phases(sac_engine* e, const sac_replay* rb, int32_t n_steps,
   int rc = check_replay(e, rb);
   if (rc) return rc;
   hipStream_t s = (hipStream_t)stream;
-  std::vector<hipEvent_t> ev((size_t)n_steps * 5);
-  for (auto& x : ev) HIPCHK(hipEventCreate(&x));
-  for (int i = 0; i < n_steps; ++i) {
-    HIPCHK(hipEventRecord(ev[i * 5], s));
-    for (int p = 0; p < 4; ++p) {
-      if (e->cfg.precision == SAC_PREC_BF16)
-        launch_phase<bf16>(e, p, rb, nullptr, nullptr, s);
-      else
-        launch_phase<float>(e, p, rb, nullptr, nullptr, s);
-      HIPCHK(hipEventRecord(ev[i * 5 + p + 1], s));
-    }
-  }
+  // events after every launch of the step sequence; a launch's time = its event
+  // minus the previous one.  Fused: [0] = phase A launches with D inside (DA),
+  // [2] = phase C launches with B inside (BC), [1] = [3] = 0.
+  std::vector<int> kinds;
+  std::vector<hipEvent_t> ev;
+  hipEvent_t start;
+  HIPCHK(hipEventCreate(&start));
+  HIPCHK(hipEventRecord(start, s));
+  launch_steps(e, rb, n_steps, nullptr, nullptr, s, &kinds, &ev);
   HIPCHK(hipStreamSynchronize(s));
-  for (int p = 0; p < 4; ++p) ms_host[p] = 0.f;
-  for (int i = 0; i < n_steps; ++i)
-    for (int p = 0; p < 4; ++p) {
-      float ms = 0.f;
-      HIPCHK(hipEventElapsedTime(&ms, ev[i * 5 + p], ev[i * 5 + p + 1]));
-      ms_host[p] += ms / n_steps;
-    }
+  double sum[6] = {0, 0, 0, 0, 0, 0};
+  int cnt[6] = {0, 0, 0, 0, 0, 0};
+  for (size_t i = 0; i < ev.size(); ++i) {
+    float ms = 0.f;
+    HIPCHK(hipEventElapsedTime(&ms, i ? ev[i - 1] : start, ev[i]));
+    sum[kinds[i]] += ms;
+    ++cnt[kinds[i]];
+  }
+  auto avg = [&](int k) { return cnt[k] ? (float)(sum[k] / cnt[k]) : 0.f; };
+  if (e->fused) {
+    ms_host[0] = cnt[L_DA] ? avg(L_DA) : avg(L_A);
+    ms_host[1] = e->fused == 2 ? 0.f : avg(L_B);
+    ms_host[2] = e->fused == 2 ? avg(L_BC) : avg(L_C);
+    ms_host[3] = 0.f;
+  } else {
+    for (int p = 0; p < 4; ++p) ms_host[p] = avg(p);
+  }
+  (void)hipEventDestroy(start);
   for (auto& x : ev) (void)hipEventDestroy(x);
   return SAC_OK;
 }

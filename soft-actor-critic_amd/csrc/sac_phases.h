@@ -7,6 +7,37 @@
 
 #define SAC_DEV_LAYERS 6  // Linear layers per network supported by the kernels
 
+// Coherent (sc1) 16-B accesses: what a workgroup of the SAME launch on any XCD
+// reads after a counter / flag hand-off (MI355X_MICROARCH.md §visibility: every
+// store of the handed-off bytes sc1 + drained, every load of them sc1).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t coh_rsrc(const void* base, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, (int)bytes, 0x00020000);
+}
+template <bool COH>
+__device__ __forceinline__ void coh_store16(const void* base, uint32_t byte_off, u32x4 v) {
+  // uniform descriptor (base only): a per-lane bound would force a waterfall loop
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, v),
+                                         coh_rsrc(base, 0xFFFFFFF0u), (int)byte_off, 0, COH ? 16 : 0);
+}
+__device__ __forceinline__ float coh_load(const float* p) {
+  return __hip_atomic_load((float*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// COH ? sc1 : plain load of a float another workgroup of the launch may have written
+template <bool COH>
+__device__ __forceinline__ float ldf(const float* p) {
+  if constexpr (COH) return coh_load(p);
+  return *GPC(float, p);
+}
+__device__ __forceinline__ void coh_storef(float* p, float v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// weight-stream fragment: sc1 when the matrix was written earlier in the same launch
+template <typename T, bool COH>
+__device__ __forceinline__ typename MM<T>::Frag coh_frag(__amdgpu_buffer_rsrc_t rs, uint32_t byte_off) {
+  return __builtin_bit_cast(typename MM<T>::Frag,
+                            __builtin_amdgcn_raw_buffer_load_b128(rs, (int)byte_off, 0, COH ? 16 : 0));
+}
+
 // ============================================================================ device state
 struct LayerDev {
   int K, N, Kp, Np;
@@ -31,6 +62,8 @@ struct NetDev {
 
 enum { NET_PI = 0, NET_Q1 = 1, NET_Q2 = 2, NET_Q1T = 3, NET_Q2T = 4 };
 
+struct TileDesc;
+
 struct EngineDev {
   int B, Bp, Br, O, A, nrt, ld, ldo;
   // Row-tile workgroups of phases A and C are blocks xs*i (the others exit at
@@ -38,6 +71,11 @@ struct EngineDev {
   // tiles onto 8/xs XCDs whose L2s then share one weight stream (speed only).
   int xs;
   int roles;  // phases A / C split into per-network workgroups (see "role hand-offs")
+  // update tiles, read by the fused launches (phase D inside phase A's launch,
+  // phase B inside phase C's launch)
+  const TileDesc* tilesB;
+  const TileDesc* tilesD;
+  int nB, nD, nBq[2];
   int auto_entropy;
   float gamma, tau, ls_min, ls_max, scale, beta1, beta2, adam_eps, target_entropy;
   double actor_lr, critic_lr, alpha_lr;
@@ -93,11 +131,21 @@ struct TileDesc {
 #ifdef SAC_STAMPS
 #define STAMP(i)                                                                               \
   do {                                                                                         \
-    if (threadIdx.x == 0 && E.stamps) GP(long long, E.stamps)[blockIdx.x * 64 + (i)] = __builtin_amdgcn_s_memtime(); \
+    if (threadIdx.x == 0 && E.stamps) GP(long long, E.stamps)[blockIdx.x * 64 + (i)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+// block end with its stores drained (stamps builds only)
+#define END_STAMP(i)                                   \
+  do {                                                 \
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   \
+    __syncthreads();                                   \
+    STAMP(i);                                          \
   } while (0)
 #else
 #define STAMP(i) \
   do {           \
+  } while (0)
+#define END_STAMP(i) \
+  do {               \
   } while (0)
 #endif
 
@@ -182,20 +230,21 @@ __device__ __forceinline__ void pf_issue(Pf<T>& pf, const GemmW& w) {
 // whose loads are all issued before the batch's first MFMA.  A short last batch
 // loads its last chunk again for the missing slots (unconditional, so the loads
 // stay back to back) and skips their MFMAs.
-template <typename T, int RT, int BM>
-__device__ __forceinline__ void mma_pair_from(const lf* __restrict__ arow, int lda, const AS_G T* b0, const AS_G T* b1,
-                                              bool has1, int ch0, int nch, f32x4 (&acc0)[RT], f32x4 (&acc1)[RT]) {
+template <typename T, int RT, int BM, bool COH>
+__device__ __forceinline__ void mma_pair_from(const lf* __restrict__ arow, int lda, __amdgpu_buffer_rsrc_t rs,
+                                              uint32_t o0, uint32_t o1, bool has1, int ch0, int nch,
+                                              f32x4 (&acc0)[RT], f32x4 (&acc1)[RT]) {
   constexpr int KC = MM<T>::KC;
-  constexpr int FS = 64 * MM<T>::KL;
+  constexpr uint32_t FSB = 64 * MM<T>::KL * sizeof(T);  // bytes per fragment
   typedef typename MM<T>::Frag F;
   for (int ch = ch0; ch < nch; ch += BM) {
     const int rem = nch - ch < BM ? nch - ch : BM;
     F f0[BM], f1[BM];
 #pragma unroll
     for (int u = 0; u < BM; ++u) {
-      const int cu = ch + (u < rem ? u : rem - 1);
-      f0[u] = MM<T>::ld(b0 + cu * FS);
-      f1[u] = MM<T>::ld(b1 + cu * FS);
+      const uint32_t cu = ch + (u < rem ? u : rem - 1);
+      f0[u] = coh_frag<T, COH>(rs, o0 + cu * FSB);
+      f1[u] = coh_frag<T, COH>(rs, o1 + cu * FSB);
     }
     if (rem == BM) {  // full batch: straight-line, LDS reads free to be hoisted
 #pragma unroll
@@ -224,7 +273,7 @@ __device__ __forceinline__ void mma_pair_from(const lf* __restrict__ arow, int l
 // acc = sum_k A[r][k] B[col][k]; epi(h, col, acc[RT]) consumes each tile pair.
 // Batch 0 of the first pair comes from pf; the next step's batch 0 is issued
 // into pf right after those MFMAs.
-template <typename T, int ROWS, typename Epi>
+template <typename T, int ROWS, bool COH, typename Epi>
 __device__ __forceinline__ void gemm_step(const lf* __restrict__ A, int lda, const GemmW& w, Pf<T>& pf,
                                           const GemmW& next, Epi epi) {
   constexpr int RT = ROWS / 16;
@@ -233,13 +282,14 @@ __device__ __forceinline__ void gemm_step(const lf* __restrict__ A, int lda, con
   const int c = lane & 15, g = lane >> 4;
   const int NT = w.NT, nch = w.cols / KC;
   if (pf.tag != w.p) pf_issue<T>(pf, w);  // chain broken by the caller: reload (uniform)
-  const AS_G T* B = GPC(T, w.p);
+  // weight stream: sc1 buffer loads, coherent with an update phase sharing the launch
+  const __amdgpu_buffer_rsrc_t rs = coh_rsrc(w.p, 0xFFFFFFF0u);
   const lf* arow = A + c * lda + g * KL;
   auto pair = [&](int nt0, bool first) {
     const int nt1 = nt0 + SAC_NW;
     const bool has1 = nt1 < NT;
-    const AS_G T* b0 = B + packed_lane<T>(nt0, w.cols, lane);
-    const AS_G T* b1 = B + packed_lane<T>(has1 ? nt1 : nt0, w.cols, lane);
+    const uint32_t o0 = (uint32_t)(packed_lane<T>(nt0, w.cols, lane) * sizeof(T));
+    const uint32_t o1 = (uint32_t)(packed_lane<T>(has1 ? nt1 : nt0, w.cols, lane) * sizeof(T));
     f32x4 acc0[RT], acc1[RT];
 #pragma unroll
     for (int rt = 0; rt < RT; ++rt) acc0[rt] = acc1[rt] = (f32x4){0.f, 0.f, 0.f, 0.f};
@@ -263,10 +313,10 @@ __device__ __forceinline__ void gemm_step(const lf* __restrict__ A, int lda, con
       pf_issue<T>(pf, next);
       __builtin_amdgcn_sched_barrier(0);
     }
-    mma_pair_from<T, RT, 8>(arow, lda, b0, b1, has1, ch0, nch, acc0, acc1);
+    mma_pair_from<T, RT, 8, COH>(arow, lda, rs, o0, o1, has1, ch0, nch, acc0, acc1);
 #else
     (void)first;
-    mma_pair_from<T, RT, 8>(arow, lda, b0, b1, has1, 0, nch, acc0, acc1);
+    mma_pair_from<T, RT, 8, COH>(arow, lda, rs, o0, o1, has1, 0, nch, acc0, acc1);
 #endif
     epi(0, nt0 * 16 + c, acc0);
     if (has1) epi(1, nt1 * 16 + c, acc1);
@@ -317,7 +367,7 @@ __device__ __forceinline__ void act_pass_bwd(lf* G, int ldg, const lf* P, int ld
 
 // Forward: Y[r][n] = act(sum_k X[r][k] W[n][k] + b[n]) for n < Np (padded -> 0).
 // P (optional) keeps the pre-activation; Pg (optional) stashes rows >= pg_row0.
-template <typename T, int ROWS>
+template <typename T, int ROWS, bool COH = false>
 __device__ __forceinline__ void layer_fwd(const lf* X, int ldx, const AS_C LayerDev& L, const float* bias_, int act, lf* P,
                                           int ldp, lf* Y, int ldy, float* Pg_, int pg_row0, Pf<T>& pf,
                                           const GemmW& next) {
@@ -334,11 +384,12 @@ __device__ __forceinline__ void layer_fwd(const lf* X, int ldx, const AS_C Layer
   if (pf.tag != w.p) pf_issue<T>(pf, w);  // bias arrives with the prefetched weights
   const float bpre0 = pf.b0, bpre1 = pf.b1;
 #else
-  const float bpre0 = bias[n0 < N ? n0 : N - 1], bpre1 = bias[n1 < N ? n1 : N - 1];
+  const float bpre0 = ldf<COH>((const float*)bias + (n0 < N ? n0 : N - 1));
+  const float bpre1 = ldf<COH>((const float*)bias + (n1 < N ? n1 : N - 1));
 #endif
-  gemm_step<T, ROWS>(X, ldx, w, pf, next, [&](int h, int n, const f32x4* acc) {
+  gemm_step<T, ROWS, COH>(X, ldx, w, pf, next, [&](int h, int n, const f32x4* acc) {
     const bool nv = n < N;
-    const float bn = n == n0 ? bpre0 : n == n1 ? bpre1 : bias[nv ? n : N - 1];
+    const float bn = n == n0 ? bpre0 : n == n1 ? bpre1 : ldf<COH>((const float*)bias + (nv ? n : N - 1));
 #pragma unroll
     for (int rt = 0; rt < ROWS / 16; ++rt)
 #pragma unroll
@@ -354,12 +405,12 @@ __device__ __forceinline__ void layer_fwd(const lf* X, int ldx, const AS_C Layer
 }
 
 // dX: Gout[r][k] = act'(Pprev[r][k]) * sum_n G[r][n] W[n][k]   (act_prev < 0: no act')
-template <typename T, int ROWS>
+template <typename T, int ROWS, bool COH = false>
 __device__ __forceinline__ void layer_bwd(const lf* G, int ldg, const AS_C LayerDev& L, const lf* Pprev, int ldp,
                                           int act_prev, lf* Gout, int ldo, Pf<T>& pf, const GemmW& next) {
   const int g = (threadIdx.x & 63) >> 4;
   const int K = L.K;
-  gemm_step<T, ROWS>(G, ldg, gw_bwd(L), pf, next, [&](int, int k, const f32x4* acc) {
+  gemm_step<T, ROWS, COH>(G, ldg, gw_bwd(L), pf, next, [&](int, int k, const f32x4* acc) {
     const bool kv = k < K;
 #pragma unroll
     for (int rt = 0; rt < ROWS / 16; ++rt)
@@ -429,7 +480,7 @@ __device__ __forceinline__ void store_T(const lf* __restrict__ src, int lds_ld, 
 // output layer writes (Pout, Yout) with stride ldo.  keepP: per-layer
 // pre-activations into lds[o_P[l]] (stride ldp[l]).  storeXT: each layer's input
 // transposed into L.XT (ROWS must be SAC_ROWS).  after: the GEMM step that follows.
-template <typename T, int ROWS>
+template <typename T, int ROWS, bool COH = false>
 __device__ __forceinline__ void mlp_forward(const AS_C NetDev& net, lf* Xb, lf* Yb, int ld, lf* Pout, lf* Yout, int ldo,
                                             const AS_C int* o_P, const AS_C int* ldp, lf* lds, bool keepP, bool storeXT, int Bp,
                                             int col0, int nvalid, Pf<T>& pf, const GemmW& after) {
@@ -443,9 +494,9 @@ __device__ __forceinline__ void mlp_forward(const AS_C NetDev& net, lf* Xb, lf* 
       if constexpr (ROWS == SAC_ROWS) store_T<T, ROWS>(X, ld, Ly.Kp, Ly.K, Ly.XT, Bp, col0, nvalid, nullptr);
     }
     if (out)
-      layer_fwd<T, ROWS>(X, ld, Ly, net.P + Ly.b_off, net.out_act, Pout, ldo, Yout, ldo, nullptr, 0, pf, next);
+      layer_fwd<T, ROWS, COH>(X, ld, Ly, net.P + Ly.b_off, net.out_act, Pout, ldo, Yout, ldo, nullptr, 0, pf, next);
     else
-      layer_fwd<T, ROWS>(X, ld, Ly, net.P + Ly.b_off, net.hid_act, keepP ? lds + o_P[l] : nullptr,
+      layer_fwd<T, ROWS, COH>(X, ld, Ly, net.P + Ly.b_off, net.hid_act, keepP ? lds + o_P[l] : nullptr,
                          keepP ? ldp[l] : 0, Y, ld, nullptr, 0, pf, next);
     __syncthreads();
     lf* t = X;
@@ -457,14 +508,14 @@ __device__ __forceinline__ void mlp_forward(const AS_C NetDev& net, lf* Xb, lf* 
 // Backward from d(output pre-activation) Gout [ROWS][ldo] down to layer 0's
 // pre-activation gradient.  storeGT: each layer's dY^T + bias partial sums.
 // Returns the buffer (stride ld) holding d(pre-act of layer 0).
-template <typename T, int ROWS>
+template <typename T, int ROWS, bool COH = false>
 __device__ __forceinline__ lf* mlp_backward(const AS_C NetDev& net, const lf* Gout, int ldo, lf* Xb, lf* Yb, int ld,
                                             const AS_C int* o_P, const AS_C int* ldp, lf* lds, bool storeGT, int Bp, int col0,
                                             int nvalid, Pf<T>& pf, const GemmW& after) {
   const int Lh = net.L - 1;
   const AS_C LayerDev& Lo = net.l[Lh];
   if (storeGT) store_T<T, ROWS>(Gout, ldo, Lo.Np, Lo.N, Lo.GT, Bp, col0, nvalid, Lo.dbp);
-  layer_bwd<T, ROWS>(Gout, ldo, Lo, lds + o_P[Lh - 1], ldp[Lh - 1], net.hid_act, Yb, ld, pf,
+  layer_bwd<T, ROWS, COH>(Gout, ldo, Lo, lds + o_P[Lh - 1], ldp[Lh - 1], net.hid_act, Yb, ld, pf,
                      Lh - 1 >= 1 ? gw_bwd(net.l[Lh - 1]) : after);
   __syncthreads();
   lf* G = Yb;
@@ -473,7 +524,7 @@ __device__ __forceinline__ lf* mlp_backward(const AS_C NetDev& net, const lf* Go
     const AS_C LayerDev& Ly = net.l[l];
     if (storeGT) store_T<T, ROWS>(G, ld, Ly.Np, Ly.N, Ly.GT, Bp, col0, nvalid, Ly.dbp);
     if (l == 0) break;
-    layer_bwd<T, ROWS>(G, ld, Ly, lds + o_P[l - 1], ldp[l - 1], net.hid_act, Gn, ld, pf,
+    layer_bwd<T, ROWS, COH>(G, ld, Ly, lds + o_P[l - 1], ldp[l - 1], net.hid_act, Gn, ld, pf,
                        l - 1 >= 1 ? gw_bwd(net.l[l - 1]) : after);
     __syncthreads();
     lf* t = G;
@@ -493,669 +544,18 @@ __device__ __forceinline__ float fmin_nan(float a, float b) { return (a != a) ? 
 // for a seed of 1 per row; writes U_l = d(pre-act of hidden layer l) for every
 // hidden layer into lds + E.o_P2[l] (stride E.ldp2[l]).  Pre-activations are in
 // the E.o_P1 buffers (critic forward with keepP).
-template <typename T, int ROWS>
+template <typename T, int ROWS, bool COH = false>
 __device__ __forceinline__ void critic_unit_backward(const AS_C EngineDev& E, const AS_C NetDev& net, const lf* Gout, int ldo,
                                                      lf* lds, Pf<T>& pf) {
   const int Lh = net.L - 1;
-  layer_bwd<T, ROWS>(Gout, ldo, net.l[Lh], lds + E.o_P1[Lh - 1], E.ldp1[Lh - 1], net.hid_act, lds + E.o_P2[Lh - 1],
+  layer_bwd<T, ROWS, COH>(Gout, ldo, net.l[Lh], lds + E.o_P1[Lh - 1], E.ldp1[Lh - 1], net.hid_act, lds + E.o_P2[Lh - 1],
                      E.ldp2[Lh - 1], pf, Lh - 1 >= 1 ? gw_bwd(net.l[Lh - 1]) : gw_none());
   __syncthreads();
   for (int l = Lh - 1; l >= 1; --l) {
-    layer_bwd<T, ROWS>(lds + E.o_P2[l], E.ldp2[l], net.l[l], lds + E.o_P1[l - 1], E.ldp1[l - 1], net.hid_act,
+    layer_bwd<T, ROWS, COH>(lds + E.o_P2[l], E.ldp2[l], net.l[l], lds + E.o_P1[l - 1], E.ldp1[l - 1], net.hid_act,
                        lds + E.o_P2[l - 1], E.ldp2[l - 1], pf, l - 1 >= 1 ? gw_bwd(net.l[l - 1]) : gw_none());
     __syncthreads();
   }
-}
-
-// ============================================================================ role hand-offs
-// With E.roles, phases A and C run as several workgroups per row tile, one per
-// network ("role"), that hand small per-row results to each other inside the
-// launch (MI355X_MICROARCH.md §visibility, write-through form): every payload
-// store and load is an agent-scope (sc1) access, the storing waves drain their
-// stores (s_waitcnt vmcnt(0)) before a workgroup barrier, then one lane stores
-// the flag (sc1); the consumer polls the flag with sc1 loads from one lane and
-// joins the others at a barrier.  Flags carry a per-launch epoch (E.sync[0] + 1,
-// advanced by phase D), so they are never reset.  Producers have lower block
-// indices than their consumers and the grid fits one block per CU, so every
-// spin terminates; spins are still bounded and set E.sync[1] on a timeout.
-enum HandKind { HK_PI = 0, HK_T1 = 1, HK_T2 = 2, HK_C1 = 3, HK_C2 = 4, HK_COUNT = 5 };
-enum SyncWord { SYNC_EPOCH = 0, SYNC_TIMEOUT = 1, SYNC_DDONE = 16, SYNC_BDONE = 32, SYNC_CDONE = 64, SYNC_FLAGS = 128 };
-#define SAC_HAND_STRIDE 576  // floats per (kind, row tile) payload: >= SAC_ROWS * (act_dim + 1)
-
-__device__ __forceinline__ AS_G uint32_t* hand_flag(const AS_C EngineDev& E, int kind, int rbi) {
-  return GP(uint32_t, E.sync) + SYNC_FLAGS + (kind * E.nrt + rbi) * 16;  // one 64-B line per flag
-}
-__device__ __forceinline__ AS_G float* hand_data(const AS_C EngineDev& E, int kind, int rbi) {
-  return GP(float, E.hand) + (size_t)(kind * E.nrt + rbi) * SAC_HAND_STRIDE;
-}
-__device__ __forceinline__ void st_sc1(AS_G float* p, float v) {
-  __hip_atomic_store((float*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ float ld_sc1(const AS_G float* p) {
-  return __hip_atomic_load((float*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-// all threads: after this workgroup's sc1 payload stores
-__device__ __forceinline__ void hand_publish(const AS_C EngineDev& E, int kind, int rbi, uint32_t ep) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) __hip_atomic_store((uint32_t*)hand_flag(E, kind, rbi), ep, __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_AGENT);
-}
-// all threads: returns once flag(kind, rbi) == ep (or the spin gave up)
-__device__ __forceinline__ void hand_wait(const AS_C EngineDev& E, int kind, int rbi, uint32_t ep) {
-  if (threadIdx.x == 0) {
-    uint32_t* f = (uint32_t*)hand_flag(E, kind, rbi);
-    for (int it = 0; __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != ep; ++it) {
-      if (it > (1 << 22)) {  // ~0.3 s: a producer never ran; flag the error, do not hang the GPU
-        __hip_atomic_store((uint32_t*)GP(uint32_t, E.sync) + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        break;
-      }
-      __builtin_amdgcn_s_sleep(2);
-    }
-  }
-  __syncthreads();
-}
-
-// all threads: returns once both flags == ep (one polling lane, one barrier)
-__device__ __forceinline__ void hand_wait2(const AS_C EngineDev& E, int k1, int k2, int rbi, uint32_t ep) {
-  if (threadIdx.x == 0) {
-    uint32_t* f1 = (uint32_t*)hand_flag(E, k1, rbi);
-    uint32_t* f2 = (uint32_t*)hand_flag(E, k2, rbi);
-    for (int it = 0;; ++it) {
-      const uint32_t a = __hip_atomic_load(f1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const uint32_t b = __hip_atomic_load(f2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (a == ep && b == ep) break;
-      if (it > (1 << 22)) {
-        __hip_atomic_store((uint32_t*)GP(uint32_t, E.sync) + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        break;
-      }
-      __builtin_amdgcn_s_sleep(2);
-    }
-  }
-  __syncthreads();
-}
-
-// ============================================================================ phase A
-// sample + gather, pi on [s'; s], target twin-Q -> y, critics forward + backward.
-// ROLES: block = role * nrt + row tile; role 0 pi on s' (target sample), 1/2
-// target critics, 3/4 critics, 5 pi on s (actor sample, stashed for phase C).
-template <typename T, bool ROLES>
-__global__ void __launch_bounds__(SAC_THREADS) sac_target_critic(const EngineDev* __restrict__ Ep, sac_replay rb,
-                                                                  const int32_t* __restrict__ inj_idx_,
-                                                                  const float* __restrict__ inj_eps_) {
-  PREFETCH_ARG(Ep);
-  const AS_C EngineDev& E = *(const AS_C EngineDev*)Ep;
-  extern __shared__ float lds_raw[];
-  lf* lds = (lf*)lds_raw;
-  constexpr int R = SAC_ROWS;
-  const int tid = threadIdx.x;
-  int rbi, role;
-  if (ROLES) {
-    rbi = blockIdx.x % E.nrt;
-    role = blockIdx.x / E.nrt;
-  } else {
-    if (blockIdx.x % E.xs) return;  // XCD placement: see EngineDev::xs
-    rbi = blockIdx.x / E.xs;
-    role = -1;
-  }
-  const bool do_pi = !ROLES || role == 0 || role == 5;
-  STAMP(0);
-  const int B = E.B, Bp = E.Bp, O = E.O, A = E.A, ld = E.ld, ldo = E.ldo;
-  const int r0 = rbi * R;
-  const int nvalid = min(R, B - r0);
-  const uint32_t ep = ROLES ? *GPC(uint32_t, E.sync) + 1u : 0u;
-  const AS_G int32_t* inj_idx = GPC(int32_t, inj_idx_);
-  const AS_G float* inj_eps = GPC(float, inj_eps_);
-  lf* Xb = lds + E.o_X;
-  lf* Yb = lds + E.o_Y;
-  lf* sB = lds + E.o_s;
-  lf* s2B = lds + E.o_s2;
-  lf* aB = lds + E.o_a;
-  lf* a2B = lds + E.o_a2;
-  lf* rB = lds + E.o_r;
-  lf* dB = lds + E.o_d;
-  lf* etB = lds + E.o_et;
-  lf* eaB = lds + E.o_ea;
-  lf* outB = lds + E.o_out;
-  lf* outP = lds + E.o_outp;
-  lf* lp2B = lds + E.o_lp;
-  lf* qtB = lds + E.o_qt;
-  lf* yB = lds + E.o_y;
-  lf* gqB = lds + E.o_gout;
-  AS_L int64_t* slotB = (AS_L int64_t*)(lds + E.o_slot);
-  const AS_C NetDev& pi = E.net[NET_PI];
-  Pf<T> pf;  // this role's first GEMM streams in under the sample / gather
-  pf_issue<T>(pf, !ROLES || do_pi ? gw_fwd(pi.l[0])
-                  : gw_fwd(E.net[role <= 2 ? NET_Q1T + role - 1 : NET_Q1 + role - 3].l[0]));
-  const AS_G float* obs = GPC(float, rb.obs);
-  const AS_G float* nobs = GPC(float, rb.next_obs);
-  const AS_G float* ract = GPC(float, rb.act);
-  const AS_G float* rrew = GPC(float, rb.rew);
-  const AS_G float* rdone = GPC(float, rb.done);
-  AS_G float* stats = GP(float, E.stats);
-
-  // optimizer step counters and this step's Adam bias-correction scalars
-  // (torch adam.py: step_size = lr / (1 - beta1^t), bias_correction2_sqrt), once per step
-  // ---- sample (replay_buffer.py:32-39) + gather (agent.py:166-193); every role
-  // draws the same indices from (seed, step), so no role waits for another's gather
-  const uint64_t step = *GPC(uint64_t, E.rng_step);
-  const int par = (int)(step & 1);  // step parity: selects the double-buffered per-step state
-  if ((!ROLES || role == 0) && rbi == 0 && tid < 4 && (tid < 3 || E.auto_entropy)) {
-    const double t = GP(double, E.opt_steps)[tid] + 1.0;
-    GP(double, E.opt_steps)[tid] = t;
-    if (tid < 3) {
-      const double lr = tid == 0 ? E.actor_lr : E.critic_lr;
-      GP(float, E.adam_sc)[par * 6 + tid * 2] = (float)(-(lr / (1.0 - pow((double)E.beta1, t))));
-      GP(float, E.adam_sc)[par * 6 + tid * 2 + 1] = (float)sqrt(1.0 - pow((double)E.beta2, t));
-    } else {
-      GP(double, E.alpha_sc)[par * 2] = 1.0 - pow((double)E.beta1, t);
-      GP(double, E.alpha_sc)[par * 2 + 1] = 1.0 - pow((double)E.beta2, t);
-    }
-  }
-
-  const int64_t rb_size = GPC(int64_t, rb.state)[0], rb_pos = GPC(int64_t, rb.state)[1];
-  if (tid < R) {
-    int64_t slot = -1;
-    const int b = r0 + tid;
-    if (b < B) {
-      int64_t li;
-      if (inj_idx) {
-        li = inj_idx[b];
-      } else {
-        const Feistel f = feistel_make(E.seed, step, rb_size);
-        li = feistel_sample(f, b, rb_size);
-      }
-      slot = rb_size < rb.capacity ? li : (rb_pos + li) % rb.capacity;
-    }
-    slotB[tid] = slot;
-  }
-  __syncthreads();
-  {  // one pass, every load unconditional (clamped row 0 for padding rows): one round trip
-    const int nI = R * (O > A ? O : A);
-    for (int i = tid; i < nI; i += SAC_THREADS) {
-      const int io = i < R * O ? i : R * O - 1, ia = i < R * A ? i : R * A - 1, ir = i < R ? i : R - 1;
-      const int64_t so = slotB[io / O], sa = slotB[ia / A], sr = slotB[ir];
-      const int64_t po = (so < 0 ? 0 : so) * O + io % O, pa = (sa < 0 ? 0 : sa) * A + ia % A, pr = sr < 0 ? 0 : sr;
-      const float vo = obs[po], vn = nobs[po], va = ract[pa], vr = rrew[pr], vd = rdone[pr];
-      if (i < R * O) {
-        sB[i] = so >= 0 ? vo : 0.f;
-        s2B[i] = so >= 0 ? vn : 0.f;
-      }
-      if (i < R * A) aB[i] = sa >= 0 ? va : 0.f;
-      if (i < R) {
-        rB[i] = sr >= 0 ? vr : 0.f;
-        dB[i] = sr >= 0 ? vd : 0.f;
-      }
-    }
-  }
-  if (do_pi) {  // which = 0: target draw (role 0), 1: actor draw (role 5)
-    const int NP = (A + 1) / 2;
-    const int w_lo = ROLES ? (role == 5) : 0, w_n = ROLES ? 1 : 2;
-    for (int i = tid; i < w_n * R * NP; i += SAC_THREADS) {
-      const int which = w_lo + i / (R * NP), rem = i % (R * NP), r = rem / NP, p = rem % NP;
-      const int b = r0 + r;
-      float n0 = 0.f, n1 = 0.f;
-      if (b < B) {
-        if (inj_eps) {
-          n0 = inj_eps[((size_t)which * B + b) * A + 2 * p];
-          if (2 * p + 1 < A) n1 = inj_eps[((size_t)which * B + b) * A + 2 * p + 1];
-        } else {
-          philox_normal2(E.seed, step, (uint32_t)b, (uint32_t)which, (uint32_t)p, n0, n1);
-        }
-      }
-      lf* dst = which ? eaB : etB;
-      dst[r * A + 2 * p] = n0;
-      if (2 * p + 1 < A) dst[r * A + 2 * p + 1] = n1;
-    }
-  }
-  __syncthreads();
-  STAMP(1);
-
-  // ---- pi forward: fused, one pass over [s' ; s] (2R rows: target sample, then
-  // actor sample); role split, role 0 runs the s' rows (on the critical path) and
-  // role 5 the s rows (stashed for phase C).
-  auto pi_forward_head = [&](auto rows_c, bool tgt, bool act) {
-    constexpr int ROWS = decltype(rows_c)::value;
-    const int a0 = tgt ? (act ? R : ROWS) : 0;  // first actor row
-    if (act)
-      for (int i = tid; i < R * O; i += SAC_THREADS) GP(float, E.s_st)[(size_t)r0 * O + i] = sB[i];
-    const int Kp0 = pi.l[0].Kp;
-    for (int i = tid; i < ROWS * Kp0; i += SAC_THREADS) {
-      const int r = i / Kp0, k = i % Kp0;
-      Xb[r * ld + k] = k < O ? (r < a0 ? s2B[r * O + k] : sB[(r - a0) * O + k]) : 0.f;
-    }
-    __syncthreads();
-    STAMP(56);
-    lf* X = Xb;
-    lf* Y = Yb;
-    for (int l = 0; l < pi.L; ++l) {
-      const AS_C LayerDev& Ly = pi.l[l];
-      if (act)  // actor rows' input, into this step's parity copy
-        store_T<T, R>(X + a0 * ld, ld, Ly.Kp, Ly.K, (T*)Ly.XT + par * Ly.xt_par, Bp, r0, nvalid, nullptr);
-      if (l == 0) STAMP(57);
-      float* stash = act ? Ly.pstash + (size_t)r0 * Ly.Np : nullptr;
-      if (l == pi.L - 1)
-        layer_fwd<T, ROWS>(X, ld, Ly, pi.P + Ly.b_off, pi.out_act, outP, ldo, outB, ldo, stash, a0, pf,
-                           gw_fwd(E.net[NET_Q1T].l[0]));
-      else
-        layer_fwd<T, ROWS>(X, ld, Ly, pi.P + Ly.b_off, pi.hid_act, nullptr, 0, Y, ld, stash, a0, pf,
-                           gw_fwd(pi.l[l + 1]));
-      __syncthreads();
-      STAMP(2 + l);
-      lf* t = X;
-      X = Y;
-      Y = t;
-    }
-    // squashed-Gaussian head (models.py:79-87): one lane per (row, action dim),
-    // each row's A lanes contiguous inside one wave (AP = pow2 >= A), summed by shuffles
-    const int AP = A <= 1 ? 1 : 1 << (32 - __builtin_clz(A - 1));
-    const int rows_per_pass = SAC_THREADS / AP;
-    for (int base = 0; base < ROWS; base += rows_per_pass) {
-      const int r = base + tid / AP, j = tid % AP;
-      const bool live = r < ROWS && j < A;
-      const bool actor = r >= a0;
-      const int rr = actor ? r - a0 : r;
-      const int b = r0 + rr;
-      float lp = 0.f, corr = 0.f;
-      if (live) {
-        const lf* o = outB + r * ldo;
-        const float mu = o[j], lsr = o[A + j], e = (actor ? eaB : etB)[rr * A + j];
-        const float lo = E.ls_min, hi = E.ls_max;
-        const float ls = lsr < lo ? lo : (lsr > hi ? hi : lsr);
-        const float sd = expf(ls);
-        const float z = mu + e * sd;
-        const float act_v = tanhf(z) * E.scale;
-        const float diff = z - mu;
-        const float var = sd * sd;
-        lp = -(diff * diff) / (2.f * var) - logf(sd) - HALF_LOG_2PI;
-        corr = 2.f * ((LOG2F - z) - softplus20(-2.f * z));
-        if (actor) {
-          AS_G float* h = GP(float, E.head_st) + (size_t)b * 4 * A;
-          h[j] = mu;
-          h[A + j] = lsr;
-          h[2 * A + j] = z;
-          h[3 * A + j] = e;
-          GP(float, E.a_st)[(size_t)b * A + j] = act_v;
-        } else {
-          a2B[rr * A + j] = act_v;
-          if (ROLES) st_sc1(hand_data(E, HK_PI, rbi) + rr * A + j, act_v);
-        }
-      }
-      for (int o = 1; o < AP; o <<= 1) {
-        lp += __shfl_xor(lp, o, 64);
-        corr += __shfl_xor(corr, o, 64);
-      }
-      if (live && j == 0) {
-        const float v = lp - corr;
-        if (actor) {
-          GP(float, E.lp_st)[par * E.Br + b] = v;
-          if (b < B) stats[4 + B + b] = v;
-        } else {
-          lp2B[rr] = v;
-          if (ROLES) st_sc1(hand_data(E, HK_PI, rbi) + R * A + rr, v);
-        }
-      }
-    }
-    if (ROLES && tgt) hand_publish(E, HK_PI, rbi, ep);  // a~' and log pi' -> target critics and critics
-    __syncthreads();
-    STAMP(6);
-  };
-  if (!ROLES)
-    pi_forward_head(std::integral_constant<int, 2 * R>(), true, true);
-  else if (role == 0 || role == 5)
-    pi_forward_head(std::integral_constant<int, R>(), role == 0, role == 5);
-
-  // ---- target twin-Q (agent.py:195-211)
-  const float alpha32 = (float)*GPC(double, E.alpha_state + 1);
-  if (!ROLES || role == 1 || role == 2) {
-    if (ROLES) {
-      hand_wait(E, HK_PI, rbi, ep);
-      const AS_G float* h = hand_data(E, HK_PI, rbi);
-      for (int i = tid; i < R * A; i += SAC_THREADS) a2B[i] = ld_sc1(h + i);
-      __syncthreads();
-    }
-    for (int t = ROLES ? role - 1 : 0; t < (ROLES ? role : 2); ++t) {
-      const AS_C NetDev& q = E.net[NET_Q1T + t];
-      const int Kp0 = q.l[0].Kp;
-      for (int i = tid; i < R * Kp0; i += SAC_THREADS) {
-        const int r = i / Kp0, k = i % Kp0;
-        Xb[r * ld + k] = k < O ? s2B[r * O + k] : (k < O + A ? a2B[r * A + (k - O)] : 0.f);
-      }
-      __syncthreads();
-      mlp_forward<T, R>(q, Xb, Yb, ld, outP, outB, ldo, E.o_P1, E.ldp1, lds, false, false, Bp, r0, nvalid, pf,
-                        gw_fwd(E.net[t ? NET_Q1 : NET_Q2T].l[0]));
-      if (tid < R) {
-        qtB[t * R + tid] = outB[tid * ldo];
-        if (ROLES) st_sc1(hand_data(E, HK_T1 + t, rbi) + tid, outB[tid * ldo]);
-      }
-      __syncthreads();
-      STAMP(7 + t);
-    }
-    if (ROLES) hand_publish(E, HK_T1 + role - 1, rbi, ep);
-    STAMP(9);
-  }
-  if (!ROLES) {
-    if (tid < R) {
-      const int b = r0 + tid;
-      const float mq = fmin_nan(qtB[tid], qtB[R + tid]);
-      const float y = rB[tid] + (E.gamma * (1.f - dB[tid])) * (mq - alpha32 * lp2B[tid]);
-      yB[tid] = y;
-      if (b < B) stats[4 + b] = y;
-    }
-    __syncthreads();
-  }
-
-  // ---- critics: forward, MSE, backward (agent.py:213-236)
-  if (!ROLES || role == 3 || role == 4) {
-    for (int qi = ROLES ? role - 3 : 0; qi < (ROLES ? role - 2 : 2); ++qi) {
-      const AS_C NetDev& q = E.net[NET_Q1 + qi];
-      const int Kp0 = q.l[0].Kp;
-      for (int i = tid; i < R * Kp0; i += SAC_THREADS) {
-        const int r = i / Kp0, k = i % Kp0;
-        Xb[r * ld + k] = k < O ? sB[r * O + k] : (k < O + A ? aB[r * A + (k - O)] : 0.f);
-      }
-      __syncthreads();
-      // the layer-0 input (s, a) is shared by Q1 and Q2: its X^T is stored once
-      if (qi == 0) store_T<T, R>(Xb, ld, Kp0, q.l[0].K, q.l[0].XT, Bp, r0, nvalid, nullptr);
-      lf* X = Xb;
-      lf* Y = Yb;
-      for (int l = 0; l < q.L; ++l) {
-        const AS_C LayerDev& Ly = q.l[l];
-        if (l > 0) store_T<T, R>(X, ld, Ly.Kp, Ly.K, Ly.XT, Bp, r0, nvalid, nullptr);
-        if (l == q.L - 1)
-          layer_fwd<T, R>(X, ld, Ly, q.P + Ly.b_off, q.out_act, outP, ldo, outB, ldo, nullptr, 0, pf, gw_bwd(Ly));
-        else
-          layer_fwd<T, R>(X, ld, Ly, q.P + Ly.b_off, q.hid_act, lds + E.o_P1[l], E.ldp1[l], Y, ld, nullptr, 0, pf,
-                          gw_fwd(q.l[l + 1]));
-        __syncthreads();
-        lf* t = X;
-        X = Y;
-        Y = t;
-      }
-      STAMP(10 + 2 * qi);
-      // Backward with a UNIT seed per row first: every layer's dY is linear in
-      // the row's seed 2(q - y)/B, so U_l = dY_l / seed does not need y and runs
-      // while the target critics finish (role split); U_l stays in LDS (the Q2
-      // pre-activation buffers, unused here) and is scaled once y is known.
-      if (tid < R) {
-        float u = tid < nvalid ? 1.f : 0.f;
-        if (q.out_act != ACT_ID) u = act_bwd(q.out_act, outP[tid * ldo], u);
-        for (int n = 0; n < 32; ++n) gqB[tid * ldo + n] = n == 0 ? u : 0.f;
-      }
-      __syncthreads();
-      critic_unit_backward<T, R>(E, q, gqB, ldo, lds, pf);
-      STAMP(16);
-      // y needs both target critics and log pi'.  The target critics published
-      // only after seeing pi's flag, so their flags also order pi's payload.
-      if (ROLES) hand_wait2(E, HK_T1, HK_T2, rbi, ep);
-      STAMP(14);
-      if (tid < 64) {  // wave 0: y, loss partial, seed dL/dq (mse_loss backward: 2(q-y)/B)
-        float sq = 0.f;
-        if (tid < R) {
-          const int b = r0 + tid;
-          const bool v = tid < nvalid;
-          float y;
-          if (ROLES) {
-            const float q1t = ld_sc1(hand_data(E, HK_T1, rbi) + tid);
-            const float q2t = ld_sc1(hand_data(E, HK_T2, rbi) + tid);
-            const float lp2 = ld_sc1(hand_data(E, HK_PI, rbi) + R * A + tid);
-            y = rB[tid] + (E.gamma * (1.f - dB[tid])) * (fmin_nan(q1t, q2t) - alpha32 * lp2);
-            if (qi == 0 && b < B) stats[4 + b] = y;
-          } else {
-            y = yB[tid];
-          }
-          const float d = outB[tid * ldo] - y;
-          sq = v ? d * d : 0.f;
-          qtB[tid] = v ? (2.0f / (float)B) * d : 0.f;  // the row's seed
-        }
-        sq = wave_sum(sq);
-        if (tid == 0) GP(float, E.lossp)[(par * E.nrt + rbi) * 4 + qi] = sq;
-      }
-      __syncthreads();
-      STAMP(15);
-      {  // dY of every layer = seed * U, stored as dY^T + bias partials for phase B
-        const AS_C LayerDev& Lo = q.l[q.L - 1];
-        store_T<T, R>(gqB, ldo, Lo.Np, Lo.N, Lo.GT, Bp, r0, nvalid, Lo.dbp, qtB);
-        for (int l = q.L - 2; l >= 0; --l) {
-          const AS_C LayerDev& Ly = q.l[l];
-          store_T<T, R>(lds + E.o_P2[l], E.ldp2[l], Ly.Np, Ly.N, Ly.GT, Bp, r0, nvalid, Ly.dbp, qtB);
-        }
-        __syncthreads();
-      }
-      STAMP(11 + 2 * qi);
-    }
-  }
-}
-
-// ============================================================================ phase C
-// critics on (s, a~) with the updated weights, d a~, head backward, pi backward.
-// ROLES: block = role * nrt + row tile; role 0 pi (head + pi backward), 1/2 critics.
-// A critic role back-propagates a UNIT seed (d Q_i / d a~) and hands (q_i,
-// dQ_i/da~) to the pi role, which applies the min-Q weights -1/B, -1/2B or 0
-// (powers of two for power-of-two batches: bit-identical to seeding them).
-template <typename T, bool ROLES>
-__device__ __forceinline__ void actor_body(const EngineDev* __restrict__ Ep) {
-  PREFETCH_ARG(Ep);
-  const AS_C EngineDev& E = *(const AS_C EngineDev*)Ep;
-  extern __shared__ float lds_raw[];
-  lf* lds = (lf*)lds_raw;
-  constexpr int R = SAC_ROWS;
-  const int tid = threadIdx.x;
-  int rbi, role;
-  if (ROLES) {
-    rbi = blockIdx.x % E.nrt;
-    role = blockIdx.x / E.nrt;
-  } else {
-    if (blockIdx.x % E.xs) return;  // XCD placement: see EngineDev::xs
-    rbi = blockIdx.x / E.xs;
-    role = -1;
-  }
-  const bool do_pi = !ROLES || role == 0;
-  STAMP(32);
-  const int B = E.B, Bp = E.Bp, O = E.O, A = E.A, ld = E.ld, ldo = E.ldo;
-  const int r0 = rbi * R;
-  const int nvalid = min(R, B - r0);
-  const uint32_t ep = ROLES ? *GPC(uint32_t, E.sync) + 1u : 0u;
-  const int par = (int)(*GPC(uint64_t, E.rng_step) & 1);  // advanced by the last block of this phase
-  lf* Xb = lds + E.o_X;
-  lf* Yb = lds + E.o_Y;
-  lf* sB = lds + E.o_s;
-  lf* aB = lds + E.o_a;
-  lf* lpB = lds + E.o_lp;
-  lf* g1B = lds + E.o_g;
-  lf* g2B = lds + E.o_g2;
-  lf* gaB = lds + E.o_ga;
-  lf* goutB = lds + E.o_gout;
-  lf* out1 = lds + E.o_out;
-  lf* outP1 = lds + E.o_outp;
-  lf* out2 = lds + E.o_out2;
-  lf* outP2 = lds + E.o_outp2;
-  const AS_C NetDev& pi = E.net[NET_PI];
-  const float alpha32 = (float)*GPC(double, E.alpha_state + 1);
-  Pf<T> pf;  // this role's first GEMM streams in under the loads / the wait
-  pf_issue<T>(pf, !ROLES ? gw_fwd(E.net[NET_Q1].l[0])
-                  : role == 0 ? gw_bwd(pi.l[pi.L - 1]) : gw_fwd(E.net[NET_Q1 + role - 1].l[0]));
-
-  if (!ROLES || role >= 1) {
-    for (int i = tid; i < R * O; i += SAC_THREADS) sB[i] = GPC(float, E.s_st)[(size_t)r0 * O + i];
-    for (int i = tid; i < R * A; i += SAC_THREADS) aB[i] = GPC(float, E.a_st)[(size_t)r0 * A + i];
-  }
-  if (do_pi) {
-    for (int i = tid; i < R * A; i += SAC_THREADS) gaB[i] = 0.f;
-    if (tid < R) lpB[tid] = GPC(float, E.lp_st)[par * E.Br + r0 + tid];
-  }
-  __syncthreads();
-
-  if (!ROLES || role >= 1) {
-    const int q_lo = ROLES ? role - 1 : 0, q_hi = ROLES ? role : 2;
-    // ---- Q1, Q2 on (s, a~) with the updated critics (agent.py:244-248)
-    for (int qi = q_lo; qi < q_hi; ++qi) {
-      const AS_C NetDev& q = E.net[NET_Q1 + qi];
-      const int Kp0 = q.l[0].Kp;
-      for (int i = tid; i < R * Kp0; i += SAC_THREADS) {
-        const int r = i / Kp0, k = i % Kp0;
-        Xb[r * ld + k] = k < O ? sB[r * O + k] : (k < O + A ? aB[r * A + (k - O)] : 0.f);
-      }
-      __syncthreads();
-      mlp_forward<T, R>(q, Xb, Yb, ld, qi ? outP2 : outP1, qi ? out2 : out1, ldo, qi ? E.o_P2 : E.o_P1,
-                        qi ? E.ldp2 : E.ldp1, lds, true, false, Bp, r0, nvalid, pf,
-                        ROLES ? gw_bwd(q.l[q.L - 1])
-                        : qi ? gw_bwd(E.net[NET_Q1].l[E.net[NET_Q1].L - 1]) : gw_fwd(E.net[NET_Q2].l[0]));
-      STAMP(36 + qi);
-    }
-    // ---- backward seeds.  L_pi = mean(alpha logpi - min Q) (agent.py:251-252); min
-    // backward splits ties.  ROLES: unit seeds, the pi role applies the weights.
-    if (tid < 64) {
-      float term = 0.f;
-      if (tid < R) {
-        const bool v = tid < nvalid;
-        float g1, g2;
-        if (ROLES) {
-          g1 = g2 = v ? 1.0f : 0.f;
-        } else {
-          const float q1 = out1[tid * ldo], q2 = out2[tid * ldo];
-          const float m = fmin_nan(q1, q2);
-          term = v ? alpha32 * lpB[tid] - m : 0.f;
-          const float gm = v ? -1.0f / (float)B : 0.f;
-          g1 = (q1 == q2) ? gm * 0.5f : (q1 > q2 ? 0.f : gm);
-          g2 = (q1 == q2) ? gm * 0.5f : (q1 < q2 ? 0.f : gm);
-        }
-        if (E.net[NET_Q1].out_act != ACT_ID) {
-          if (q_lo == 0) g1 = act_bwd(E.net[NET_Q1].out_act, outP1[tid * ldo], g1);
-          if (q_hi == 2) g2 = act_bwd(E.net[NET_Q2].out_act, outP2[tid * ldo], g2);
-        }
-        for (int n = 0; n < 32; ++n) {
-          g1B[tid * ldo + n] = n == 0 ? g1 : 0.f;
-          g2B[tid * ldo + n] = n == 0 ? g2 : 0.f;
-        }
-      }
-      if (!ROLES) {
-        term = wave_sum(term);
-        if (tid == 0) GP(float, E.lossp)[(par * E.nrt + rbi) * 4 + 2] = term;
-      }
-    }
-    __syncthreads();
-
-    // ---- d a~ through the critics: dX of layer 0, action columns
-    for (int qi = q_lo; qi < q_hi; ++qi) {
-      const AS_C NetDev& q = E.net[NET_Q1 + qi];
-      lf* G0 = mlp_backward<T, R>(q, qi ? g2B : g1B, ldo, Xb, Yb, ld, qi ? E.o_P2 : E.o_P1, qi ? E.ldp2 : E.ldp1,
-                                  lds, false, Bp, r0, nvalid, pf, gw_bwd(q.l[0]));
-      lf* Gx = (G0 == Xb) ? Yb : Xb;
-      layer_bwd<T, R>(G0, ld, q.l[0], nullptr, 0, -1, Gx, ld, pf,
-                      qi ? gw_bwd(pi.l[pi.L - 1]) : gw_bwd(E.net[NET_Q2].l[E.net[NET_Q2].L - 1]));
-      __syncthreads();
-      if (ROLES) {
-        AS_G float* h = hand_data(E, HK_C1 + qi, rbi);
-        for (int i = tid; i < R * A; i += SAC_THREADS) st_sc1(h + i, Gx[(i / A) * ld + O + i % A]);
-        if (tid < R) st_sc1(h + R * A + tid, (qi ? out2 : out1)[tid * ldo]);
-        hand_publish(E, HK_C1 + qi, rbi, ep);
-      } else {
-        for (int i = tid; i < R * A; i += SAC_THREADS) gaB[i] += Gx[(i / A) * ld + O + i % A];
-        __syncthreads();
-      }
-      STAMP(38 + qi);
-    }
-  }
-  if (!do_pi) return;
-
-  // ---- squashed-Gaussian head backward + pi backward (agent.py:255-257)
-  for (int l = 0; l < pi.L - 1; ++l) {
-    const AS_C LayerDev& Ly = pi.l[l];
-    const int ldp = E.ldp1[l];
-    lf* P = lds + E.o_P1[l];
-    const AS_G float* ps = GPC(float, Ly.pstash) + (size_t)r0 * Ly.Np;
-    for (int i = tid; i < R * Ly.Np; i += SAC_THREADS) P[(i / Ly.Np) * ldp + i % Ly.Np] = ps[i];
-  }
-  if (ROLES) {  // combine the critics' unit-seed gradients with the min-Q weights
-    hand_wait(E, HK_C1, rbi, ep);
-    hand_wait(E, HK_C2, rbi, ep);
-    const AS_G float* h1 = hand_data(E, HK_C1, rbi);
-    const AS_G float* h2 = hand_data(E, HK_C2, rbi);
-    if (tid < 64) {
-      float term = 0.f;
-      if (tid < R) {
-        const bool v = tid < nvalid;
-        const float q1 = ld_sc1(h1 + R * A + tid), q2 = ld_sc1(h2 + R * A + tid);
-        const float m = fmin_nan(q1, q2);
-        term = v ? alpha32 * lpB[tid] - m : 0.f;
-        const float gm = v ? -1.0f / (float)B : 0.f;
-        g1B[tid] = (q1 == q2) ? gm * 0.5f : (q1 > q2 ? 0.f : gm);
-        g2B[tid] = (q1 == q2) ? gm * 0.5f : (q1 < q2 ? 0.f : gm);
-      }
-      term = wave_sum(term);
-      if (tid == 0) GP(float, E.lossp)[(par * E.nrt + rbi) * 4 + 2] = term;
-    }
-    __syncthreads();
-    for (int i = tid; i < R * A; i += SAC_THREADS) {
-      const int r = i / A;
-      gaB[i] = (gaB[i] + g1B[r] * ld_sc1(h1 + i)) + g2B[r] * ld_sc1(h2 + i);
-    }
-    __syncthreads();
-    STAMP(39);
-  }
-  for (int i = tid; i < R * A; i += SAC_THREADS) {  // one lane per (row, action dim)
-    const int r = i / A, j = i % A, b = r0 + r;
-    const bool v = r < nvalid;
-    const float gl = v ? alpha32 * (1.0f / (float)B) : 0.f;
-    const AS_G float* h = GPC(float, E.head_st) + (size_t)b * 4 * A;
-    const float lo = E.ls_min, hi = E.ls_max, scale = E.scale;
-    const float mu = h[j], lsr = h[A + j], z = h[2 * A + j], e = h[3 * A + j];
-    const float ls = lsr < lo ? lo : (lsr > hi ? hi : lsr);
-    const float sd = expf(ls);
-    const float t = tanhf(z);
-    const float diff = z - mu, var = sd * sd;
-    float g_z = (gaB[r * A + j] * scale) * (1.f - t * t);
-    g_z = g_z + (-gl) * 2.f * (-1.f + 2.f * softplus20_grad(-2.f * z));
-    const float two_var = 2.f * var;
-    const float g_sq = -gl / two_var;
-    const float g_twovar = gl * (diff * diff) / (two_var * two_var);
-    const float g_var = 2.f * g_twovar;
-    float g_std = 2.f * sd * g_var - gl / sd;
-    const float g_diff = 2.f * diff * g_sq;
-    g_z = g_z + g_diff;
-    const float g_mu = -g_diff + g_z;
-    g_std = g_std + g_z * e;
-    const float g_ls = g_std * sd;
-    const bool in_range = (lsr >= lo) && (lsr <= hi);
-    float gm = v ? g_mu : 0.f, gs = (v && in_range) ? g_ls : 0.f;
-    if (pi.out_act != ACT_ID) {
-      const AS_C LayerDev& Lo = pi.l[pi.L - 1];
-      const AS_G float* ps = GPC(float, Lo.pstash) + (size_t)b * Lo.Np;
-      gm = act_bwd(pi.out_act, ps[j], gm);
-      gs = act_bwd(pi.out_act, ps[A + j], gs);
-    }
-    goutB[r * ldo + j] = gm;
-    goutB[r * ldo + A + j] = gs;
-  }
-  {
-    const int NOp = 32 * ((2 * A + 31) / 32), pad = NOp - 2 * A;
-    for (int i = tid; i < R * pad; i += SAC_THREADS) goutB[(i / pad) * ldo + 2 * A + i % pad] = 0.f;
-  }
-  __syncthreads();
-  mlp_backward<T, R>(pi, goutB, ldo, Xb, Yb, ld, E.o_P1, E.ldp1, lds, true, Bp, r0, nvalid, pf, gw_none());
-  STAMP(35);
-}
-
-// The last block of phase C to finish advances the step: RNG step, hand-off
-// epoch, and resets the completion counters (every reader of those words ran
-// earlier in this launch or runs in a later one).
-__device__ __forceinline__ void phase_c_done(const AS_C EngineDev& E) {
-  if (threadIdx.x != 0) return;
-  uint32_t* sync = (uint32_t*)E.sync;
-  const uint32_t old = __hip_atomic_fetch_add(sync + SYNC_CDONE, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if (old == gridDim.x - 1) {
-    *GP(uint64_t, E.rng_step) += 1;
-    sync[SYNC_EPOCH] += 1u;
-    sync[SYNC_CDONE] = 0u;
-    sync[SYNC_DDONE] = 0u;
-  }
-}
-
-template <typename T, bool ROLES>
-__global__ void __launch_bounds__(SAC_THREADS) sac_actor(const EngineDev* __restrict__ Ep) {
-  actor_body<T, ROLES>(Ep);
-  phase_c_done(*(const AS_C EngineDev*)Ep);
 }
 
 // ============================================================================ phases B / D
@@ -1172,23 +572,6 @@ __device__ __forceinline__ float adam_elem(float& p, float& m, float& v, float g
   return pn;
 }
 
-// Coherent (sc1) 16-B accesses: what a workgroup of the SAME launch on any XCD
-// reads after a counter / flag hand-off (MI355X_MICROARCH.md §visibility: every
-// store of the handed-off bytes sc1 + drained, every load of them sc1).
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t coh_rsrc(const void* base, uint32_t bytes) {
-  return __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, (int)bytes, 0x00020000);
-}
-__device__ __forceinline__ void coh_store16(const void* base, uint32_t byte_off, u32x4 v) {
-  // uniform descriptor (base only): a per-lane bound would force a waterfall loop
-  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, v),
-                                         coh_rsrc(base, 0xFFFFFFF0u), (int)byte_off, 0, 16);
-}
-__device__ __forceinline__ float coh_load(const float* p) {
-  return __hip_atomic_load((float*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void coh_storef(float* p, float v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
 // all threads: drain this workgroup's stores, then one lane counts the block done
 __device__ __forceinline__ void count_done(uint32_t* counter) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1211,7 +594,7 @@ __device__ __forceinline__ void count_done(uint32_t* counter) {
 // dynamic LDS of an update tile: stage 64 x 528 B | 2 x [32][33] f32 | [32][9] f32
 // (>= the alpha block's 5 x 1024 floats)
 #define SAC_UPD_LDS (64 * 528 + 2 * 32 * 33 * 4 + 32 * 9 * 4)
-template <typename T, int UT>
+template <typename T, int UT, bool COH>
 __device__ __forceinline__ void dw_adam_tile(const AS_C EngineDev& E, const TileDesc* tdp_, bool polyak, int par,
                                              lf* lds) {
   constexpr int KC = MM<T>::KC, KL = MM<T>::KL;
@@ -1334,7 +717,10 @@ __device__ __forceinline__ void dw_adam_tile(const AS_C EngineDev& E, const Tile
     float gb = 0.f;
     for (int q = 0; q < 8; ++q) gb += red[tid * 9 + q];
     const float pbn = adam_elem(pb, mb, vb, gb, w1, b2, w2, bc2s, eps, neg_step);
-    coh_storef((float*)td.b + td.n0 + tid, pb);
+    if (COH)
+      coh_storef((float*)td.b + td.n0 + tid, pb);
+    else
+      GP(float, td.b)[td.n0 + tid] = pb;
     GP(float, td.bm)[td.n0 + tid] = mb;
     GP(float, td.bv)[td.n0 + tid] = vb;
     if (polyak) GP(float, td.tb)[td.n0 + tid] = tau * pbn + omt * tbv;
@@ -1358,19 +744,9 @@ __device__ __forceinline__ void dw_adam_tile(const AS_C EngineDev& E, const Tile
         for (int j = 0; j < EPR; ++j) vv[j] = MM<T>::cvt(srcm[row * 33 + pc * EPR + j]);
         off = packed_off<T>(td.n0 + row, td.k0 + pc * EPR, td.Kp);
       }
-      coh_store16(base, (uint32_t)(off * sizeof(T)), *(const u32x4*)vv);
+      coh_store16<COH>(base, (uint32_t)(off * sizeof(T)), *(const u32x4*)vv);
     }
   }
-}
-
-template <typename T>
-__global__ void __launch_bounds__(SAC_UPD_THREADS) sac_critic_update(const EngineDev* __restrict__ Ep,
-                                                         const TileDesc* __restrict__ tiles) {
-  const AS_C EngineDev& E = *(const AS_C EngineDev*)Ep;
-  extern __shared__ float upd_lds[];
-  dw_adam_tile<T, SAC_UPD_THREADS>(E, tiles + blockIdx.x, true, (int)(*GPC(uint64_t, E.rng_step) & 1),
-                                   (lf*)upd_lds);
-  count_done((uint32_t*)E.sync + SYNC_BDONE + 16 * (tiles[blockIdx.x].opt - 1));
 }
 
 // One block: reduces the step's loss partials into stats[0..3] and runs the
@@ -1433,6 +809,740 @@ __device__ __forceinline__ void alpha_and_losses(const AS_C EngineDev& E, int pa
   }
 }
 
+// ============================================================================ role hand-offs
+// With E.roles, phases A and C run as several workgroups per row tile, one per
+// network ("role"), that hand small per-row results to each other inside the
+// launch (MI355X_MICROARCH.md §visibility, write-through form): every payload
+// store and load is an agent-scope (sc1) access, the storing waves drain their
+// stores (s_waitcnt vmcnt(0)) before a workgroup barrier, then one lane stores
+// the flag (sc1); the consumer polls the flag with sc1 loads from one lane and
+// joins the others at a barrier.  Flags carry a per-launch epoch (E.sync[0] + 1,
+// advanced by phase D), so they are never reset.  Producers have lower block
+// indices than their consumers and the grid fits one block per CU, so every
+// spin terminates; spins are still bounded and set E.sync[1] on a timeout.
+enum HandKind { HK_PI = 0, HK_T1 = 1, HK_T2 = 2, HK_C1 = 3, HK_C2 = 4, HK_COUNT = 5 };
+enum SyncWord { SYNC_EPOCH = 0, SYNC_TIMEOUT = 1, SYNC_DDONE = 16, SYNC_BDONE = 32, SYNC_CDONE = 64, SYNC_FLAGS = 128 };
+#define SAC_HAND_STRIDE 576  // floats per (kind, row tile) payload: >= SAC_ROWS * (act_dim + 1)
+
+__device__ __forceinline__ AS_G uint32_t* hand_flag(const AS_C EngineDev& E, int kind, int rbi) {
+  return GP(uint32_t, E.sync) + SYNC_FLAGS + (kind * E.nrt + rbi) * 16;  // one 64-B line per flag
+}
+__device__ __forceinline__ AS_G float* hand_data(const AS_C EngineDev& E, int kind, int rbi) {
+  return GP(float, E.hand) + (size_t)(kind * E.nrt + rbi) * SAC_HAND_STRIDE;
+}
+__device__ __forceinline__ void st_sc1(AS_G float* p, float v) {
+  __hip_atomic_store((float*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float ld_sc1(const AS_G float* p) {
+  return __hip_atomic_load((float*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// all threads: after this workgroup's sc1 payload stores
+__device__ __forceinline__ void hand_publish(const AS_C EngineDev& E, int kind, int rbi, uint32_t ep) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_store((uint32_t*)hand_flag(E, kind, rbi), ep, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+}
+// all threads: returns once flag(kind, rbi) == ep (or the spin gave up)
+__device__ __forceinline__ void hand_wait(const AS_C EngineDev& E, int kind, int rbi, uint32_t ep) {
+  if (threadIdx.x == 0) {
+    uint32_t* f = (uint32_t*)hand_flag(E, kind, rbi);
+    for (int it = 0; __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != ep; ++it) {
+      if (it > (1 << 22)) {  // ~0.3 s: a producer never ran; flag the error, do not hang the GPU
+        __hip_atomic_store((uint32_t*)GP(uint32_t, E.sync) + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+  }
+  __syncthreads();
+}
+
+// all threads: returns once both flags == ep (one polling lane, one barrier)
+__device__ __forceinline__ void hand_wait2(const AS_C EngineDev& E, int k1, int k2, int rbi, uint32_t ep) {
+  if (threadIdx.x == 0) {
+    uint32_t* f1 = (uint32_t*)hand_flag(E, k1, rbi);
+    uint32_t* f2 = (uint32_t*)hand_flag(E, k2, rbi);
+    for (int it = 0;; ++it) {
+      const uint32_t a = __hip_atomic_load(f1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const uint32_t b = __hip_atomic_load(f2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (a == ep && b == ep) break;
+      if (it > (1 << 22)) {
+        __hip_atomic_store((uint32_t*)GP(uint32_t, E.sync) + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+  }
+  __syncthreads();
+}
+
+// all threads: returns once *counter >= target (one polling lane, one barrier)
+__device__ __forceinline__ void count_wait(const AS_C EngineDev& E, int word, uint32_t target) {
+  if (threadIdx.x == 0) {
+    uint32_t* c = (uint32_t*)E.sync + word;
+    for (int it = 0; __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target; ++it) {
+      if (it > (1 << 22)) {
+        __hip_atomic_store((uint32_t*)GP(uint32_t, E.sync) + SYNC_TIMEOUT, 1u, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+  }
+  __syncthreads();
+}
+
+// ============================================================================ phase A
+// sample + gather, pi on [s'; s], target twin-Q -> y, critics forward + backward.
+// ROLES: block = role * nrt + row tile; role 0 pi on s' (target sample), 1/2
+// target critics, 3/4 critics, 5 pi on s (actor sample, stashed for phase C).
+// WITH_D (role split only): blocks [0, nD] first run the PREVIOUS step's phase
+// D (pi tiles, then the alpha block) and count themselves done; the pi roles
+// wait for that count before streaming pi's weights, everything else of phase
+// A (sampling, gathers, the critics' forward) overlaps it.
+template <typename T, bool ROLES, bool WITH_D>
+__device__ __forceinline__ void target_critic_body(const EngineDev* __restrict__ Ep, const sac_replay& rb,
+                                                   const int32_t* __restrict__ inj_idx_,
+                                                   const float* __restrict__ inj_eps_) {
+  PREFETCH_ARG(Ep);
+  const AS_C EngineDev& E = *(const AS_C EngineDev*)Ep;
+  extern __shared__ float lds_raw[];
+  lf* lds = (lf*)lds_raw;
+  constexpr int R = SAC_ROWS;
+  const int tid = threadIdx.x;
+  int bid = blockIdx.x;
+  if (WITH_D) {
+    // grid order = dispatch order: pi(s') roles first (the critical path), then
+    // the phase D blocks they wait for, then the other roles
+    if (bid >= E.nrt) {
+      if (bid <= E.nrt + E.nD) {
+        const int parD = (int)((*GPC(uint64_t, E.rng_step) - 1) & 1);  // the step phase C just closed
+        if (bid < E.nrt + E.nD)
+          dw_adam_tile<T, SAC_THREADS, true>(E, E.tilesD + (bid - E.nrt), false, parD, lds);
+        else
+          alpha_and_losses(E, parD, lds);
+        count_done((uint32_t*)E.sync + SYNC_DDONE);
+        return;
+      }
+      bid -= E.nD + 1;
+    }
+  }
+  int rbi, role;
+  if (ROLES) {
+    rbi = bid % E.nrt;
+    role = bid / E.nrt;
+  } else {
+    if (blockIdx.x % E.xs) return;  // XCD placement: see EngineDev::xs
+    rbi = blockIdx.x / E.xs;
+    role = -1;
+  }
+  const bool do_pi = !ROLES || role == 0 || role == 5;
+  STAMP(0);
+  const int B = E.B, Bp = E.Bp, O = E.O, A = E.A, ld = E.ld, ldo = E.ldo;
+  const int r0 = rbi * R;
+  const int nvalid = min(R, B - r0);
+  const uint32_t ep = ROLES ? *GPC(uint32_t, E.sync) + 1u : 0u;
+  const AS_G int32_t* inj_idx = GPC(int32_t, inj_idx_);
+  const AS_G float* inj_eps = GPC(float, inj_eps_);
+  lf* Xb = lds + E.o_X;
+  lf* Yb = lds + E.o_Y;
+  lf* sB = lds + E.o_s;
+  lf* s2B = lds + E.o_s2;
+  lf* aB = lds + E.o_a;
+  lf* a2B = lds + E.o_a2;
+  lf* rB = lds + E.o_r;
+  lf* dB = lds + E.o_d;
+  lf* etB = lds + E.o_et;
+  lf* eaB = lds + E.o_ea;
+  lf* outB = lds + E.o_out;
+  lf* outP = lds + E.o_outp;
+  lf* lp2B = lds + E.o_lp;
+  lf* qtB = lds + E.o_qt;
+  lf* yB = lds + E.o_y;
+  lf* gqB = lds + E.o_gout;
+  AS_L int64_t* slotB = (AS_L int64_t*)(lds + E.o_slot);
+  const AS_C NetDev& pi = E.net[NET_PI];
+  Pf<T> pf;  // this role's first GEMM streams in under the sample / gather
+  pf_issue<T>(pf, !ROLES || do_pi ? gw_fwd(pi.l[0])
+                  : gw_fwd(E.net[role <= 2 ? NET_Q1T + role - 1 : NET_Q1 + role - 3].l[0]));
+  const AS_G float* obs = GPC(float, rb.obs);
+  const AS_G float* nobs = GPC(float, rb.next_obs);
+  const AS_G float* ract = GPC(float, rb.act);
+  const AS_G float* rrew = GPC(float, rb.rew);
+  const AS_G float* rdone = GPC(float, rb.done);
+  AS_G float* stats = GP(float, E.stats);
+
+  // optimizer step counters and this step's Adam bias-correction scalars
+  // (torch adam.py: step_size = lr / (1 - beta1^t), bias_correction2_sqrt), once per step
+  // ---- sample (replay_buffer.py:32-39) + gather (agent.py:166-193); every role
+  // draws the same indices from (seed, step), so no role waits for another's gather
+  const uint64_t step = *GPC(uint64_t, E.rng_step);
+  const int par = (int)(step & 1);  // step parity: selects the double-buffered per-step state
+  if ((!ROLES || role == 0) && rbi == 0 && tid == 0) {  // phase B of this step counts from 0
+    GP(uint32_t, E.sync)[SYNC_BDONE] = 0u;
+    GP(uint32_t, E.sync)[SYNC_BDONE + 16] = 0u;
+  }
+  if ((!ROLES || role == 0) && rbi == 0 && tid < 4 && (tid < 3 || E.auto_entropy)) {
+    const double t = GP(double, E.opt_steps)[tid] + 1.0;
+    GP(double, E.opt_steps)[tid] = t;
+    if (tid < 3) {
+      const double lr = tid == 0 ? E.actor_lr : E.critic_lr;
+      GP(float, E.adam_sc)[par * 6 + tid * 2] = (float)(-(lr / (1.0 - pow((double)E.beta1, t))));
+      GP(float, E.adam_sc)[par * 6 + tid * 2 + 1] = (float)sqrt(1.0 - pow((double)E.beta2, t));
+    } else {
+      GP(double, E.alpha_sc)[par * 2] = 1.0 - pow((double)E.beta1, t);
+      GP(double, E.alpha_sc)[par * 2 + 1] = 1.0 - pow((double)E.beta2, t);
+    }
+  }
+
+  const int64_t rb_size = GPC(int64_t, rb.state)[0], rb_pos = GPC(int64_t, rb.state)[1];
+  if (tid < R) {
+    int64_t slot = -1;
+    const int b = r0 + tid;
+    if (b < B) {
+      int64_t li;
+      if (inj_idx) {
+        li = inj_idx[b];
+      } else {
+        const Feistel f = feistel_make(E.seed, step, rb_size);
+        li = feistel_sample(f, b, rb_size);
+      }
+      slot = rb_size < rb.capacity ? li : (rb_pos + li) % rb.capacity;
+    }
+    slotB[tid] = slot;
+  }
+  __syncthreads();
+  {  // one pass, every load unconditional (clamped row 0 for padding rows): one round trip
+    const int nI = R * (O > A ? O : A);
+    for (int i = tid; i < nI; i += SAC_THREADS) {
+      const int io = i < R * O ? i : R * O - 1, ia = i < R * A ? i : R * A - 1, ir = i < R ? i : R - 1;
+      const int64_t so = slotB[io / O], sa = slotB[ia / A], sr = slotB[ir];
+      const int64_t po = (so < 0 ? 0 : so) * O + io % O, pa = (sa < 0 ? 0 : sa) * A + ia % A, pr = sr < 0 ? 0 : sr;
+      const float vo = obs[po], vn = nobs[po], va = ract[pa], vr = rrew[pr], vd = rdone[pr];
+      if (i < R * O) {
+        sB[i] = so >= 0 ? vo : 0.f;
+        s2B[i] = so >= 0 ? vn : 0.f;
+      }
+      if (i < R * A) aB[i] = sa >= 0 ? va : 0.f;
+      if (i < R) {
+        rB[i] = sr >= 0 ? vr : 0.f;
+        dB[i] = sr >= 0 ? vd : 0.f;
+      }
+    }
+  }
+  if (do_pi) {  // which = 0: target draw (role 0), 1: actor draw (role 5)
+    const int NP = (A + 1) / 2;
+    const int w_lo = ROLES ? (role == 5) : 0, w_n = ROLES ? 1 : 2;
+    for (int i = tid; i < w_n * R * NP; i += SAC_THREADS) {
+      const int which = w_lo + i / (R * NP), rem = i % (R * NP), r = rem / NP, p = rem % NP;
+      const int b = r0 + r;
+      float n0 = 0.f, n1 = 0.f;
+      if (b < B) {
+        if (inj_eps) {
+          n0 = inj_eps[((size_t)which * B + b) * A + 2 * p];
+          if (2 * p + 1 < A) n1 = inj_eps[((size_t)which * B + b) * A + 2 * p + 1];
+        } else {
+          philox_normal2(E.seed, step, (uint32_t)b, (uint32_t)which, (uint32_t)p, n0, n1);
+        }
+      }
+      lf* dst = which ? eaB : etB;
+      dst[r * A + 2 * p] = n0;
+      if (2 * p + 1 < A) dst[r * A + 2 * p + 1] = n1;
+    }
+  }
+  __syncthreads();
+  STAMP(1);
+
+  // ---- pi forward: fused, one pass over [s' ; s] (2R rows: target sample, then
+  // actor sample); role split, role 0 runs the s' rows (on the critical path) and
+  // role 5 the s rows (stashed for phase C).
+  auto pi_forward_head = [&](auto rows_c, bool tgt, bool act) {
+    constexpr int ROWS = decltype(rows_c)::value;
+    const int a0 = tgt ? (act ? R : ROWS) : 0;  // first actor row
+    if (act)
+      for (int i = tid; i < R * O; i += SAC_THREADS) GP(float, E.s_st)[(size_t)r0 * O + i] = sB[i];
+    const int Kp0 = pi.l[0].Kp;
+    for (int i = tid; i < ROWS * Kp0; i += SAC_THREADS) {
+      const int r = i / Kp0, k = i % Kp0;
+      Xb[r * ld + k] = k < O ? (r < a0 ? s2B[r * O + k] : sB[(r - a0) * O + k]) : 0.f;
+    }
+    __syncthreads();
+    STAMP(56);
+    lf* X = Xb;
+    lf* Y = Yb;
+    for (int l = 0; l < pi.L; ++l) {
+      const AS_C LayerDev& Ly = pi.l[l];
+      if (act)  // actor rows' input, into this step's parity copy
+        store_T<T, R>(X + a0 * ld, ld, Ly.Kp, Ly.K, (T*)Ly.XT + par * Ly.xt_par, Bp, r0, nvalid, nullptr);
+      if (l == 0) STAMP(57);
+      float* stash = act ? Ly.pstash + (size_t)r0 * Ly.Np : nullptr;
+      if (l == pi.L - 1)
+        layer_fwd<T, ROWS, WITH_D>(X, ld, Ly, pi.P + Ly.b_off, pi.out_act, outP, ldo, outB, ldo, stash, a0, pf,
+                           gw_fwd(E.net[NET_Q1T].l[0]));
+      else
+        layer_fwd<T, ROWS, WITH_D>(X, ld, Ly, pi.P + Ly.b_off, pi.hid_act, nullptr, 0, Y, ld, stash, a0, pf,
+                           gw_fwd(pi.l[l + 1]));
+      __syncthreads();
+      STAMP(2 + l);
+      lf* t = X;
+      X = Y;
+      Y = t;
+    }
+    // squashed-Gaussian head (models.py:79-87): one lane per (row, action dim),
+    // each row's A lanes contiguous inside one wave (AP = pow2 >= A), summed by shuffles
+    const int AP = A <= 1 ? 1 : 1 << (32 - __builtin_clz(A - 1));
+    const int rows_per_pass = SAC_THREADS / AP;
+    for (int base = 0; base < ROWS; base += rows_per_pass) {
+      const int r = base + tid / AP, j = tid % AP;
+      const bool live = r < ROWS && j < A;
+      const bool actor = r >= a0;
+      const int rr = actor ? r - a0 : r;
+      const int b = r0 + rr;
+      float lp = 0.f, corr = 0.f;
+      if (live) {
+        const lf* o = outB + r * ldo;
+        const float mu = o[j], lsr = o[A + j], e = (actor ? eaB : etB)[rr * A + j];
+        const float lo = E.ls_min, hi = E.ls_max;
+        const float ls = lsr < lo ? lo : (lsr > hi ? hi : lsr);
+        const float sd = expf(ls);
+        const float z = mu + e * sd;
+        const float act_v = tanhf(z) * E.scale;
+        const float diff = z - mu;
+        const float var = sd * sd;
+        lp = -(diff * diff) / (2.f * var) - logf(sd) - HALF_LOG_2PI;
+        corr = 2.f * ((LOG2F - z) - softplus20(-2.f * z));
+        if (actor) {
+          AS_G float* h = GP(float, E.head_st) + (size_t)b * 4 * A;
+          h[j] = mu;
+          h[A + j] = lsr;
+          h[2 * A + j] = z;
+          h[3 * A + j] = e;
+          GP(float, E.a_st)[(size_t)b * A + j] = act_v;
+        } else {
+          a2B[rr * A + j] = act_v;
+          if (ROLES) st_sc1(hand_data(E, HK_PI, rbi) + rr * A + j, act_v);
+        }
+      }
+      for (int o = 1; o < AP; o <<= 1) {
+        lp += __shfl_xor(lp, o, 64);
+        corr += __shfl_xor(corr, o, 64);
+      }
+      if (live && j == 0) {
+        const float v = lp - corr;
+        if (actor) {
+          GP(float, E.lp_st)[par * E.Br + b] = v;
+          if (b < B) stats[4 + B + b] = v;
+        } else {
+          lp2B[rr] = v;
+          if (ROLES) st_sc1(hand_data(E, HK_PI, rbi) + R * A + rr, v);
+        }
+      }
+    }
+    if (ROLES && tgt) hand_publish(E, HK_PI, rbi, ep);  // a~' and log pi' -> target critics and critics
+    __syncthreads();
+    STAMP(6);
+  };
+  if (!ROLES) {
+    pi_forward_head(std::integral_constant<int, 2 * R>(), true, true);
+  } else if (role == 0 || role == 5) {
+    if (WITH_D) count_wait(E, SYNC_DDONE, (uint32_t)E.nD + 1u);  // pi updated by the previous step's phase D
+    STAMP(59);
+    pi_forward_head(std::integral_constant<int, R>(), role == 0, role == 5);
+  }
+
+  // ---- target twin-Q (agent.py:195-211)
+  const float alpha32 = (float)*GPC(double, E.alpha_state + 1);
+  if (!ROLES || role == 1 || role == 2) {
+    if (ROLES) {
+      hand_wait(E, HK_PI, rbi, ep);
+      const AS_G float* h = hand_data(E, HK_PI, rbi);
+      for (int i = tid; i < R * A; i += SAC_THREADS) a2B[i] = ld_sc1(h + i);
+      __syncthreads();
+    }
+    for (int t = ROLES ? role - 1 : 0; t < (ROLES ? role : 2); ++t) {
+      const AS_C NetDev& q = E.net[NET_Q1T + t];
+      const int Kp0 = q.l[0].Kp;
+      for (int i = tid; i < R * Kp0; i += SAC_THREADS) {
+        const int r = i / Kp0, k = i % Kp0;
+        Xb[r * ld + k] = k < O ? s2B[r * O + k] : (k < O + A ? a2B[r * A + (k - O)] : 0.f);
+      }
+      __syncthreads();
+      mlp_forward<T, R>(q, Xb, Yb, ld, outP, outB, ldo, E.o_P1, E.ldp1, lds, false, false, Bp, r0, nvalid, pf,
+                        gw_fwd(E.net[t ? NET_Q1 : NET_Q2T].l[0]));
+      if (tid < R) {
+        qtB[t * R + tid] = outB[tid * ldo];
+        if (ROLES) st_sc1(hand_data(E, HK_T1 + t, rbi) + tid, outB[tid * ldo]);
+      }
+      __syncthreads();
+      STAMP(7 + t);
+    }
+    if (ROLES) hand_publish(E, HK_T1 + role - 1, rbi, ep);
+    STAMP(9);
+  }
+  if (!ROLES) {
+    if (tid < R) {
+      const int b = r0 + tid;
+      const float mq = fmin_nan(qtB[tid], qtB[R + tid]);
+      const float y = rB[tid] + (E.gamma * (1.f - dB[tid])) * (mq - alpha32 * lp2B[tid]);
+      yB[tid] = y;
+      if (b < B) stats[4 + b] = y;
+    }
+    __syncthreads();
+  }
+
+  // ---- critics: forward, MSE, backward (agent.py:213-236)
+  if (!ROLES || role == 3 || role == 4) {
+    for (int qi = ROLES ? role - 3 : 0; qi < (ROLES ? role - 2 : 2); ++qi) {
+      const AS_C NetDev& q = E.net[NET_Q1 + qi];
+      const int Kp0 = q.l[0].Kp;
+      for (int i = tid; i < R * Kp0; i += SAC_THREADS) {
+        const int r = i / Kp0, k = i % Kp0;
+        Xb[r * ld + k] = k < O ? sB[r * O + k] : (k < O + A ? aB[r * A + (k - O)] : 0.f);
+      }
+      __syncthreads();
+      // the layer-0 input (s, a) is shared by Q1 and Q2: its X^T is stored once
+      if (qi == 0) store_T<T, R>(Xb, ld, Kp0, q.l[0].K, q.l[0].XT, Bp, r0, nvalid, nullptr);
+      lf* X = Xb;
+      lf* Y = Yb;
+      for (int l = 0; l < q.L; ++l) {
+        const AS_C LayerDev& Ly = q.l[l];
+        if (l > 0) store_T<T, R>(X, ld, Ly.Kp, Ly.K, Ly.XT, Bp, r0, nvalid, nullptr);
+        if (l == q.L - 1)
+          layer_fwd<T, R>(X, ld, Ly, q.P + Ly.b_off, q.out_act, outP, ldo, outB, ldo, nullptr, 0, pf, gw_bwd(Ly));
+        else
+          layer_fwd<T, R>(X, ld, Ly, q.P + Ly.b_off, q.hid_act, lds + E.o_P1[l], E.ldp1[l], Y, ld, nullptr, 0, pf,
+                          gw_fwd(q.l[l + 1]));
+        __syncthreads();
+        lf* t = X;
+        X = Y;
+        Y = t;
+      }
+      STAMP(10 + 2 * qi);
+      // Backward with a UNIT seed per row first: every layer's dY is linear in
+      // the row's seed 2(q - y)/B, so U_l = dY_l / seed does not need y and runs
+      // while the target critics finish (role split); U_l stays in LDS (the Q2
+      // pre-activation buffers, unused here) and is scaled once y is known.
+      if (tid < R) {
+        float u = tid < nvalid ? 1.f : 0.f;
+        if (q.out_act != ACT_ID) u = act_bwd(q.out_act, outP[tid * ldo], u);
+        for (int n = 0; n < 32; ++n) gqB[tid * ldo + n] = n == 0 ? u : 0.f;
+      }
+      __syncthreads();
+      critic_unit_backward<T, R>(E, q, gqB, ldo, lds, pf);
+      STAMP(16);
+      // y needs both target critics and log pi'.  The target critics published
+      // only after seeing pi's flag, so their flags also order pi's payload.
+      if (ROLES) hand_wait2(E, HK_T1, HK_T2, rbi, ep);
+      STAMP(14);
+      if (tid < 64) {  // wave 0: y, loss partial, seed dL/dq (mse_loss backward: 2(q-y)/B)
+        float sq = 0.f;
+        if (tid < R) {
+          const int b = r0 + tid;
+          const bool v = tid < nvalid;
+          float y;
+          if (ROLES) {
+            const float q1t = ld_sc1(hand_data(E, HK_T1, rbi) + tid);
+            const float q2t = ld_sc1(hand_data(E, HK_T2, rbi) + tid);
+            const float lp2 = ld_sc1(hand_data(E, HK_PI, rbi) + R * A + tid);
+            // alpha after the hand-offs: a phase D sharing the launch finished before pi started
+            const float al = (float)__hip_atomic_load((double*)E.alpha_state + 1, __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_AGENT);
+            y = rB[tid] + (E.gamma * (1.f - dB[tid])) * (fmin_nan(q1t, q2t) - al * lp2);
+            if (qi == 0 && b < B) stats[4 + b] = y;
+          } else {
+            y = yB[tid];
+          }
+          const float d = outB[tid * ldo] - y;
+          sq = v ? d * d : 0.f;
+          qtB[tid] = v ? (2.0f / (float)B) * d : 0.f;  // the row's seed
+        }
+        sq = wave_sum(sq);
+        if (tid == 0) GP(float, E.lossp)[(par * E.nrt + rbi) * 4 + qi] = sq;
+      }
+      __syncthreads();
+      STAMP(15);
+      {  // dY of every layer = seed * U, stored as dY^T + bias partials for phase B
+        const AS_C LayerDev& Lo = q.l[q.L - 1];
+        store_T<T, R>(gqB, ldo, Lo.Np, Lo.N, Lo.GT, Bp, r0, nvalid, Lo.dbp, qtB);
+        for (int l = q.L - 2; l >= 0; --l) {
+          const AS_C LayerDev& Ly = q.l[l];
+          store_T<T, R>(lds + E.o_P2[l], E.ldp2[l], Ly.Np, Ly.N, Ly.GT, Bp, r0, nvalid, Ly.dbp, qtB);
+        }
+        __syncthreads();
+      }
+      STAMP(11 + 2 * qi);
+    }
+  }
+}
+
+template <typename T, bool ROLES, bool WITH_D>
+__global__ void __launch_bounds__(SAC_THREADS) sac_target_critic(const EngineDev* __restrict__ Ep, sac_replay rb,
+                                                                  const int32_t* __restrict__ inj_idx_,
+                                                                  const float* __restrict__ inj_eps_) {
+  target_critic_body<T, ROLES, WITH_D>(Ep, rb, inj_idx_, inj_eps_);
+  const AS_C EngineDev& E = *(const AS_C EngineDev*)Ep;
+  (void)E;
+  END_STAMP(60);
+}
+
+// ============================================================================ phase C
+// critics on (s, a~) with the updated weights, d a~, head backward, pi backward.
+// ROLES: block = role * nrt + row tile; role 0 pi (head + pi backward), 1/2 critics.
+// A critic role back-propagates a UNIT seed (d Q_i / d a~) and hands (q_i,
+// dQ_i/da~) to the pi role, which applies the min-Q weights -1/B, -1/2B or 0
+// (powers of two for power-of-two batches: bit-identical to seeding them).
+template <typename T, bool ROLES, bool WITH_B>
+__device__ __forceinline__ void actor_body(const EngineDev* __restrict__ Ep, int bid) {
+  const AS_C EngineDev& E = *(const AS_C EngineDev*)Ep;
+  extern __shared__ float lds_raw[];
+  lf* lds = (lf*)lds_raw;
+  constexpr int R = SAC_ROWS;
+  const int tid = threadIdx.x;
+  int rbi, role;
+  if (ROLES) {
+    rbi = bid % E.nrt;
+    role = bid / E.nrt;
+  } else {
+    if (bid % E.xs) return;  // XCD placement: see EngineDev::xs
+    rbi = bid / E.xs;
+    role = -1;
+  }
+  const bool do_pi = !ROLES || role == 0;
+  STAMP(32);
+  const int B = E.B, Bp = E.Bp, O = E.O, A = E.A, ld = E.ld, ldo = E.ldo;
+  const int r0 = rbi * R;
+  const int nvalid = min(R, B - r0);
+  const uint32_t ep = ROLES ? *GPC(uint32_t, E.sync) + 1u : 0u;
+  const int par = (int)(*GPC(uint64_t, E.rng_step) & 1);  // advanced by the last block of this phase
+  lf* Xb = lds + E.o_X;
+  lf* Yb = lds + E.o_Y;
+  lf* sB = lds + E.o_s;
+  lf* aB = lds + E.o_a;
+  lf* lpB = lds + E.o_lp;
+  lf* g1B = lds + E.o_g;
+  lf* g2B = lds + E.o_g2;
+  lf* gaB = lds + E.o_ga;
+  lf* goutB = lds + E.o_gout;
+  lf* out1 = lds + E.o_out;
+  lf* outP1 = lds + E.o_outp;
+  lf* out2 = lds + E.o_out2;
+  lf* outP2 = lds + E.o_outp2;
+  const AS_C NetDev& pi = E.net[NET_PI];
+  const float alpha32 = (float)*GPC(double, E.alpha_state + 1);
+  Pf<T> pf;  // this role's first GEMM streams in under the loads / the wait
+  pf_issue<T>(pf, !ROLES ? gw_fwd(E.net[NET_Q1].l[0])
+                  : role == 0 ? gw_bwd(pi.l[pi.L - 1]) : gw_fwd(E.net[NET_Q1 + role - 1].l[0]));
+
+  if (!ROLES || role >= 1) {
+    for (int i = tid; i < R * O; i += SAC_THREADS) sB[i] = GPC(float, E.s_st)[(size_t)r0 * O + i];
+    for (int i = tid; i < R * A; i += SAC_THREADS) aB[i] = GPC(float, E.a_st)[(size_t)r0 * A + i];
+  }
+  if (do_pi) {
+    for (int i = tid; i < R * A; i += SAC_THREADS) gaB[i] = 0.f;
+    if (tid < R) lpB[tid] = GPC(float, E.lp_st)[par * E.Br + r0 + tid];
+  }
+  __syncthreads();
+
+  if (!ROLES || role >= 1) {
+    const int q_lo = ROLES ? role - 1 : 0, q_hi = ROLES ? role : 2;
+    if (WITH_B) count_wait(E, SYNC_BDONE + 16 * q_lo, (uint32_t)E.nBq[q_lo]);  // this critic updated
+    STAMP(33);
+    // ---- Q1, Q2 on (s, a~) with the updated critics (agent.py:244-248)
+    for (int qi = q_lo; qi < q_hi; ++qi) {
+      const AS_C NetDev& q = E.net[NET_Q1 + qi];
+      const int Kp0 = q.l[0].Kp;
+      for (int i = tid; i < R * Kp0; i += SAC_THREADS) {
+        const int r = i / Kp0, k = i % Kp0;
+        Xb[r * ld + k] = k < O ? sB[r * O + k] : (k < O + A ? aB[r * A + (k - O)] : 0.f);
+      }
+      __syncthreads();
+      mlp_forward<T, R, WITH_B>(q, Xb, Yb, ld, qi ? outP2 : outP1, qi ? out2 : out1, ldo, qi ? E.o_P2 : E.o_P1,
+                        qi ? E.ldp2 : E.ldp1, lds, true, false, Bp, r0, nvalid, pf,
+                        ROLES ? gw_bwd(q.l[q.L - 1])
+                        : qi ? gw_bwd(E.net[NET_Q1].l[E.net[NET_Q1].L - 1]) : gw_fwd(E.net[NET_Q2].l[0]));
+      STAMP(36 + qi);
+    }
+    // ---- backward seeds.  L_pi = mean(alpha logpi - min Q) (agent.py:251-252); min
+    // backward splits ties.  ROLES: unit seeds, the pi role applies the weights.
+    if (tid < 64) {
+      float term = 0.f;
+      if (tid < R) {
+        const bool v = tid < nvalid;
+        float g1, g2;
+        if (ROLES) {
+          g1 = g2 = v ? 1.0f : 0.f;
+        } else {
+          const float q1 = out1[tid * ldo], q2 = out2[tid * ldo];
+          const float m = fmin_nan(q1, q2);
+          term = v ? alpha32 * lpB[tid] - m : 0.f;
+          const float gm = v ? -1.0f / (float)B : 0.f;
+          g1 = (q1 == q2) ? gm * 0.5f : (q1 > q2 ? 0.f : gm);
+          g2 = (q1 == q2) ? gm * 0.5f : (q1 < q2 ? 0.f : gm);
+        }
+        if (E.net[NET_Q1].out_act != ACT_ID) {
+          if (q_lo == 0) g1 = act_bwd(E.net[NET_Q1].out_act, outP1[tid * ldo], g1);
+          if (q_hi == 2) g2 = act_bwd(E.net[NET_Q2].out_act, outP2[tid * ldo], g2);
+        }
+        for (int n = 0; n < 32; ++n) {
+          g1B[tid * ldo + n] = n == 0 ? g1 : 0.f;
+          g2B[tid * ldo + n] = n == 0 ? g2 : 0.f;
+        }
+      }
+      if (!ROLES) {
+        term = wave_sum(term);
+        if (tid == 0) GP(float, E.lossp)[(par * E.nrt + rbi) * 4 + 2] = term;
+      }
+    }
+    __syncthreads();
+
+    // ---- d a~ through the critics: dX of layer 0, action columns
+    for (int qi = q_lo; qi < q_hi; ++qi) {
+      const AS_C NetDev& q = E.net[NET_Q1 + qi];
+      lf* G0 = mlp_backward<T, R, WITH_B>(q, qi ? g2B : g1B, ldo, Xb, Yb, ld, qi ? E.o_P2 : E.o_P1, qi ? E.ldp2 : E.ldp1,
+                                  lds, false, Bp, r0, nvalid, pf, gw_bwd(q.l[0]));
+      lf* Gx = (G0 == Xb) ? Yb : Xb;
+      layer_bwd<T, R, WITH_B>(G0, ld, q.l[0], nullptr, 0, -1, Gx, ld, pf,
+                      qi ? gw_bwd(pi.l[pi.L - 1]) : gw_bwd(E.net[NET_Q2].l[E.net[NET_Q2].L - 1]));
+      __syncthreads();
+      if (ROLES) {
+        AS_G float* h = hand_data(E, HK_C1 + qi, rbi);
+        for (int i = tid; i < R * A; i += SAC_THREADS) st_sc1(h + i, Gx[(i / A) * ld + O + i % A]);
+        if (tid < R) st_sc1(h + R * A + tid, (qi ? out2 : out1)[tid * ldo]);
+        hand_publish(E, HK_C1 + qi, rbi, ep);
+      } else {
+        for (int i = tid; i < R * A; i += SAC_THREADS) gaB[i] += Gx[(i / A) * ld + O + i % A];
+        __syncthreads();
+      }
+      STAMP(38 + qi);
+    }
+  }
+  if (!do_pi) return;
+
+  // ---- squashed-Gaussian head backward + pi backward (agent.py:255-257)
+  for (int l = 0; l < pi.L - 1; ++l) {
+    const AS_C LayerDev& Ly = pi.l[l];
+    const int ldp = E.ldp1[l];
+    lf* P = lds + E.o_P1[l];
+    const AS_G float* ps = GPC(float, Ly.pstash) + (size_t)r0 * Ly.Np;
+    for (int i = tid; i < R * Ly.Np; i += SAC_THREADS) P[(i / Ly.Np) * ldp + i % Ly.Np] = ps[i];
+  }
+  if (ROLES) {  // combine the critics' unit-seed gradients with the min-Q weights
+    hand_wait(E, HK_C1, rbi, ep);
+    hand_wait(E, HK_C2, rbi, ep);
+    const AS_G float* h1 = hand_data(E, HK_C1, rbi);
+    const AS_G float* h2 = hand_data(E, HK_C2, rbi);
+    if (tid < 64) {
+      float term = 0.f;
+      if (tid < R) {
+        const bool v = tid < nvalid;
+        const float q1 = ld_sc1(h1 + R * A + tid), q2 = ld_sc1(h2 + R * A + tid);
+        const float m = fmin_nan(q1, q2);
+        term = v ? alpha32 * lpB[tid] - m : 0.f;
+        const float gm = v ? -1.0f / (float)B : 0.f;
+        g1B[tid] = (q1 == q2) ? gm * 0.5f : (q1 > q2 ? 0.f : gm);
+        g2B[tid] = (q1 == q2) ? gm * 0.5f : (q1 < q2 ? 0.f : gm);
+      }
+      term = wave_sum(term);
+      if (tid == 0) GP(float, E.lossp)[(par * E.nrt + rbi) * 4 + 2] = term;
+    }
+    __syncthreads();
+    for (int i = tid; i < R * A; i += SAC_THREADS) {
+      const int r = i / A;
+      gaB[i] = (gaB[i] + g1B[r] * ld_sc1(h1 + i)) + g2B[r] * ld_sc1(h2 + i);
+    }
+    __syncthreads();
+    STAMP(39);
+  }
+  for (int i = tid; i < R * A; i += SAC_THREADS) {  // one lane per (row, action dim)
+    const int r = i / A, j = i % A, b = r0 + r;
+    const bool v = r < nvalid;
+    const float gl = v ? alpha32 * (1.0f / (float)B) : 0.f;
+    const AS_G float* h = GPC(float, E.head_st) + (size_t)b * 4 * A;
+    const float lo = E.ls_min, hi = E.ls_max, scale = E.scale;
+    const float mu = h[j], lsr = h[A + j], z = h[2 * A + j], e = h[3 * A + j];
+    const float ls = lsr < lo ? lo : (lsr > hi ? hi : lsr);
+    const float sd = expf(ls);
+    const float t = tanhf(z);
+    const float diff = z - mu, var = sd * sd;
+    float g_z = (gaB[r * A + j] * scale) * (1.f - t * t);
+    g_z = g_z + (-gl) * 2.f * (-1.f + 2.f * softplus20_grad(-2.f * z));
+    const float two_var = 2.f * var;
+    const float g_sq = -gl / two_var;
+    const float g_twovar = gl * (diff * diff) / (two_var * two_var);
+    const float g_var = 2.f * g_twovar;
+    float g_std = 2.f * sd * g_var - gl / sd;
+    const float g_diff = 2.f * diff * g_sq;
+    g_z = g_z + g_diff;
+    const float g_mu = -g_diff + g_z;
+    g_std = g_std + g_z * e;
+    const float g_ls = g_std * sd;
+    const bool in_range = (lsr >= lo) && (lsr <= hi);
+    float gm = v ? g_mu : 0.f, gs = (v && in_range) ? g_ls : 0.f;
+    if (pi.out_act != ACT_ID) {
+      const AS_C LayerDev& Lo = pi.l[pi.L - 1];
+      const AS_G float* ps = GPC(float, Lo.pstash) + (size_t)b * Lo.Np;
+      gm = act_bwd(pi.out_act, ps[j], gm);
+      gs = act_bwd(pi.out_act, ps[A + j], gs);
+    }
+    goutB[r * ldo + j] = gm;
+    goutB[r * ldo + A + j] = gs;
+  }
+  {
+    const int NOp = 32 * ((2 * A + 31) / 32), pad = NOp - 2 * A;
+    for (int i = tid; i < R * pad; i += SAC_THREADS) goutB[(i / pad) * ldo + 2 * A + i % pad] = 0.f;
+  }
+  __syncthreads();
+  mlp_backward<T, R>(pi, goutB, ldo, Xb, Yb, ld, E.o_P1, E.ldp1, lds, true, Bp, r0, nvalid, pf, gw_none());
+  STAMP(35);
+}
+
+// The last block of phase C to finish advances the step: RNG step, hand-off
+// epoch, and resets the completion counters (every reader of those words ran
+// earlier in this launch or runs in a later one).
+__device__ __forceinline__ void phase_c_done(const AS_C EngineDev& E) {
+  if (threadIdx.x != 0) return;
+  uint32_t* sync = (uint32_t*)E.sync;
+  const uint32_t old = __hip_atomic_fetch_add(sync + SYNC_CDONE, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (old == gridDim.x - 1) {
+    *GP(uint64_t, E.rng_step) += 1;
+    sync[SYNC_EPOCH] += 1u;
+    sync[SYNC_CDONE] = 0u;
+    sync[SYNC_DDONE] = 0u;
+  }
+}
+
+// WITH_B (role split only): blocks [0, nB) first run this step's phase B (critic
+// tiles, Polyak) and count themselves done per critic; each critic role waits
+// for its critic's count before streaming its weights.
+template <typename T, bool ROLES, bool WITH_B>
+__global__ void __launch_bounds__(SAC_THREADS) sac_actor(const EngineDev* __restrict__ Ep) {
+  PREFETCH_ARG(Ep);
+  const AS_C EngineDev& E = *(const AS_C EngineDev*)Ep;
+  if (WITH_B && (int)blockIdx.x < E.nB) {
+    extern __shared__ float lds_raw[];
+    const AS_C TileDesc& td = *((const AS_C TileDesc*)E.tilesB + blockIdx.x);
+    dw_adam_tile<T, SAC_THREADS, true>(E, E.tilesB + blockIdx.x, true, (int)(*GPC(uint64_t, E.rng_step) & 1),
+                                       (lf*)lds_raw);
+    count_done((uint32_t*)E.sync + SYNC_BDONE + 16 * (td.opt - 1));
+  } else {
+    actor_body<T, ROLES, WITH_B>(Ep, (int)blockIdx.x - (WITH_B ? E.nB : 0));
+  }
+  phase_c_done(E);
+  END_STAMP(61);
+}
+
+// ============================================================================ phases B / D kernels
+template <typename T>
+__global__ void __launch_bounds__(SAC_UPD_THREADS) sac_critic_update(const EngineDev* __restrict__ Ep,
+                                                         const TileDesc* __restrict__ tiles) {
+  const AS_C EngineDev& E = *(const AS_C EngineDev*)Ep;
+  extern __shared__ float upd_lds[];
+  dw_adam_tile<T, SAC_UPD_THREADS, false>(E, tiles + blockIdx.x, true, (int)(*GPC(uint64_t, E.rng_step) & 1),
+                                          (lf*)upd_lds);
+  END_STAMP(62);  // standalone: the launch boundary publishes (no counter)
+}
+
 template <typename T>
 __global__ void __launch_bounds__(SAC_UPD_THREADS) sac_actor_update(const EngineDev* __restrict__ Ep, const TileDesc* __restrict__ tiles,
                                                         int ntiles) {
@@ -1440,10 +1550,10 @@ __global__ void __launch_bounds__(SAC_UPD_THREADS) sac_actor_update(const Engine
   const int par = (int)((*GPC(uint64_t, E.rng_step) - 1) & 1);  // phase C already advanced the step
   extern __shared__ float upd_lds[];
   if ((int)blockIdx.x < ntiles)
-    dw_adam_tile<T, SAC_UPD_THREADS>(E, tiles + blockIdx.x, false, par, (lf*)upd_lds);
+    dw_adam_tile<T, SAC_UPD_THREADS, false>(E, tiles + blockIdx.x, false, par, (lf*)upd_lds);
   else
     alpha_and_losses(E, par, (lf*)upd_lds);
-  count_done((uint32_t*)E.sync + SYNC_DDONE);
+  END_STAMP(63);  // standalone: the launch boundary publishes (no counter)
 }
 
 // ============================================================================ policy

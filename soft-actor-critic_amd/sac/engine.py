@@ -130,6 +130,7 @@ class SacEngine:
         self.steps_done = 0
         self.lib.sac_engine_uses_roles.argtypes = [ctypes.c_void_p]
         self.roles = bool(self.lib.sac_engine_uses_roles(h))
+        self.fused = int(self.lib.sac_engine_phase_layout(h))  # 1: D in the next A's launch, 2: + B in C's
 
     # ------------------------------------------------------------------ plumbing
     def _stream(self):

@@ -251,3 +251,23 @@ def test_large_batch_uses_fused_kernels_and_runs():
     eng.train_graph(rb, 20, chunk=10)
     eng.check()
     assert all(np.isfinite(eng.losses()))
+
+
+@pytest.mark.parametrize("precision,layout", [("fp32", "1"), ("bf16", "1"), ("fp32", "2"), ("bf16", "2")])
+def test_fused_launches_equal_four_launches(precision, layout, monkeypatch):
+    """Two launches per step (phase D inside the next phase A launch, phase B
+    inside the phase C launch, in-launch completion counters) give the same
+    bits as four launches per step."""
+    out = {}
+    for fuse in (layout, "0"):
+        monkeypatch.setenv("SAC_FUSE", fuse)
+        eng, rb, c = _engine("c2", precision, capacity=5000)
+        assert eng.fused == int(fuse)
+        eng.train(rb, 3)
+        eng.train_graph(rb, 7, chunk=3)
+        eng.train(rb, 1)
+        eng.check()
+        out[fuse] = {k: v.clone() for k, v in eng.state_tensors().items()}
+        out[fuse]["stats"] = eng.stats.clone()
+    for k in out[layout]:
+        assert torch.equal(out[layout][k], out["0"][k]), k

@@ -1,7 +1,8 @@
 """Where does a phase kernel spend its time?  Runs the C2 engine from the
 -DSAC_STAMPS build (make -C soft-actor-critic_amd/csrc stamps) and prints, per
-phase and per workgroup role, the s_memtime deltas between STAMP(i) points
-(median over row tiles and over 10 steps)."""
+phase and per workgroup role, the time between STAMP(i) points in microseconds
+(s_memrealtime, 100 MHz, one clock for every XCD; median over row tiles and over
+10 steps), then a launch-wide timeline relative to the launch's first stamp."""
 import ctypes
 import os
 import sys
@@ -25,6 +26,17 @@ lib.sac_engine_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes
 assert lib.sac_engine_debug_stamped() == 1, "not the stamps build"
 nblk = 2048  # rows for every block index any phase grid can have (B/D tile grids included)
 nrt = (c["batch"] + 15) // 16
+
+
+def _tiles(dims):
+    return sum(((dims[i + 1] + 31) // 32) * ((dims[i] + 31) // 32) for i in range(len(dims) - 1))
+
+
+O_, A_, H_ = c["obs"], c["act"], c["hidden"]
+n_b = 2 * _tiles([O_ + A_] + H_ + [1])
+n_d = _tiles([O_] + H_ + [2 * A_])
+# role blocks start after the update tiles in the fused launches
+OFF = {"A": n_d + 1, "C": n_b} if eng.fused else {"A": 0, "C": 0}
 buf = torch.zeros(nblk * 64, dtype=torch.int64, device=dev)
 E.check(lib.sac_engine_debug_stamps(eng.handle, E.ptr(buf), eng._stream()))
 eng.train(rb, 20)
@@ -35,12 +47,15 @@ for it in range(10):
     eng.train(rb, 1)
     torch.cuda.synchronize()
     runs.append(buf.view(nblk, 64).cpu().numpy().copy())
-names = {0: "start", 1: "gather+eps", 56: "pi X built", 57: "pi L0 issued", 2: "pi L0", 3: "pi L1", 4: "pi L2",
+names = {58: "D done", 59: "D waited",
+         0: "start", 1: "gather+eps", 56: "pi X built", 57: "pi L0 issued", 2: "pi L0", 3: "pi L1", 4: "pi L2",
          5: "pi L3", 6: "head+publish", 7: "Qt1", 8: "Qt2", 9: "Qt published", 10: "Q1 fwd", 12: "Q2 fwd",
          16: "unit bwd", 14: "y inputs in", 15: "seed", 11: "Q1 GT stored", 13: "Q2 GT stored",
          32: "start", 36: "Q1 fwd", 37: "Q2 fwd", 38: "Q1 bwd->da", 39: "Q2 bwd->da / combined", 35: "pi bwd",
          48: "start", 49: "dW", 50: "adam", 52: "start", 53: "dW", 54: "adam"}
-PH = {"A": list(range(0, 17)) + [56, 57], "C": list(range(32, 40)), "B": [48, 49, 50], "D": [52, 53, 54]}
+names.update({33: "B waited"})
+names.update({60: "END", 61: "END", 62: "END", 63: "END"})
+PH = {"A": list(range(0, 17)) + [56, 57, 59, 60], "C": list(range(32, 40)) + [61], "B": [48, 49, 50, 62], "D": [52, 53, 54, 63]}
 ROLES = {"A": ["pi(s')", "Qt1", "Qt2", "Q1", "Q2", "pi(s)"], "C": ["pi", "Q1", "Q2"]}
 for ph, ids in PH.items():
     base = ids[0]
@@ -50,9 +65,19 @@ for ph, ids in PH.items():
         continue
     groups = {"all": np.ones(len(blk), bool)}
     if ph in ROLES and eng.roles:
-        groups = {nm: (blk // nrt) == k for k, nm in enumerate(ROLES[ph])}
-    t_first = np.array([r[r[:, base] > 0, base].min() for r in runs])
+        rb_ = blk - OFF[ph]
+        groups = {nm: (rb_ >= 0) & ((rb_ // nrt) == k) for k, nm in enumerate(ROLES[ph])}
+        if OFF[ph]:
+            groups["upd"] = rb_ < 0
     print(f"=== phase {ph}")
+    endc = {"A": 60, "C": 61, "B": 62, "D": 63}[ph]
+    spans = []
+    for r in runs:
+        live = r[:, base] > 0
+        if live.any() and (r[live, endc] > 0).any():
+            spans.append(r[live, endc].max() - r[live, base].min())
+    if spans:
+        print(f"  launch span (first block start -> last block end, stores drained): {np.median(spans) / 100:.2f} us")
     for g, m in groups.items():
         if not m.any():
             continue
@@ -62,8 +87,30 @@ for ph, ids in PH.items():
         seq.sort(key=lambda x: x[1])
         line, prev = [], 0.0
         for i, t in seq:
-            line.append(f"{names.get(i, i)} +{t - prev:.0f}")
+            line.append(f"{names.get(i, i)} +{(t - prev) / 100:.2f}")
             prev = t
-        print(f"  [{g:6s}] " + " | ".join(line) + f"   (total {prev:.0f})")
-    spans = [r[r[:, base] > 0][:, ids].max() - r[r[:, base] > 0, base].min() for r in runs]
-    print(f"  first start -> last stamp of the grid: median {np.median(spans):.0f} cycles")
+        print(f"  [{g:6s}] " + " | ".join(line) + f"   (total {prev / 100:.2f} us)")
+        # absolute: each stamp relative to the launch's earliest stamp of this phase
+        ab = []
+        for i in ids:
+            vals = []
+            for r in runs:
+                live = r[:, base] > 0
+                t0 = r[live, base].min()
+                bm = np.zeros(len(r), bool)
+                bm[np.nonzero(live)[0]] = True
+                sel_r = r[bm]
+                blk_r = np.nonzero(bm)[0]
+                gm = np.ones(len(blk_r), bool)
+                if ph in ROLES and eng.roles:
+                    rb2 = blk_r - OFF[ph]
+                    k = list(groups).index(g) if g in ROLES.get(ph, []) else -1
+                    gm = (rb2 >= 0) & ((rb2 // nrt) == k) if k >= 0 else (rb2 < 0)
+                v = sel_r[gm, i]
+                v = v[v > 0]
+                if v.size:
+                    vals.append(np.median(v) - t0)
+            if vals:
+                ab.append((np.median(vals), names.get(i, i)))
+        ab.sort()
+        print("           @ " + " | ".join(f"{n} {t / 100:.2f}" for t, n in ab))
