@@ -12,6 +12,10 @@ extern "C" {
  * ([grid][64]); only builds with -DSAC_STAMPS write them. */
 int sac_engine_debug_stamps(sac_engine *e, long long *dev_buf, void *stream);
 int sac_engine_debug_stamped(void);
+/* Launch ONE phase kernel of the current step (kind: 0 A, 1 B, 2 C, 3 D, 4 A
+ * with D inside, 5 C with B inside) on the stream.  Timing experiments only:
+ * re-running a phase out of sequence advances or corrupts the training state. */
+int sac_engine_debug_launch(sac_engine* e, const sac_replay* rb, int32_t kind, void* stream);
 /* 1 if phases A/C run role-split (per-network workgroups with in-launch
  * hand-offs), 0 if one workgroup per row tile runs all networks. */
 int sac_engine_uses_roles(const sac_engine *e);

@@ -35,6 +35,11 @@ typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 #define SAC_NW 8                // waves per row-tile workgroup
 #endif
 #define SAC_THREADS (64 * SAC_NW)
+// Wave index as a uniform (SGPR) value: threadIdx.x >> 6 is the same for every
+// lane of a wave, but the compiler's divergence analysis cannot see that, so
+// branches and loop bounds on it become exec-masked and values merged after them
+// land in VGPRs (a buffer descriptor merged that way needs a waterfall loop).
+__device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
 #define SAC_ROWS 16             // batch rows per row-tile workgroup
 #define SAC_PAD 32              // feature padding (bf16 MFMA K step)
 

@@ -700,6 +700,10 @@ int sac_engine_debug_stamps(sac_engine* e, long long* dev_buf, void* stream) {
   if (!e) return fail(SAC_E_INVALID, "null engine");
   e->h.stamps = dev_buf;
   HIPCHK(hipMemcpyAsync(e->d, &e->h, sizeof(EngineDev), hipMemcpyHostToDevice, (hipStream_t)stream));
+#ifdef SAC_STAMPS
+  HIPCHK(hipMemcpyToSymbolAsync(HIP_SYMBOL(sac_dbg_stamps), &dev_buf, sizeof(dev_buf), 0, hipMemcpyHostToDevice,
+                                (hipStream_t)stream));
+#endif
   if (e->gexec) {  // graphs captured the old kernel arguments
     (void)hipGraphExecDestroy(e->gexec);
     (void)hipGraphDestroy(e->graph);
@@ -719,6 +723,16 @@ int sac_debug_sample_indices_host(int64_t size, int32_t batch, uint64_t seed, ui
 int sac_engine_uses_roles(const sac_engine* e) { return e && e->h.roles ? 1 : 0; }
 
 int sac_engine_phase_layout(const sac_engine* e) { return e ? e->fused : 0; }
+
+int sac_engine_debug_launch(sac_engine* e, const sac_replay* rb, int32_t kind, void* stream) {
+  if (!e || !rb || kind < L_A || kind > L_BC) return fail(SAC_E_INVALID, "bad debug_launch arguments");
+  if (e->cfg.precision == SAC_PREC_BF16)
+    launch_kind<bf16>(e, kind, rb, nullptr, nullptr, (hipStream_t)stream);
+  else
+    launch_kind<float>(e, kind, rb, nullptr, nullptr, (hipStream_t)stream);
+  HIPCHK(hipGetLastError());
+  return SAC_OK;
+}
 
 int sac_engine_debug_stamped(void) {
 #ifdef SAC_STAMPS

@@ -2,6 +2,7 @@
 // Included by sac_engine.hip only.  Reference cross-walk in sac_engine.hip.
 #pragma once
 #include <type_traits>
+#include <utility>
 
 #include "sac_device.h"
 
@@ -140,7 +141,25 @@ struct TileDesc {
     __syncthreads();                                   \
     STAMP(i);                                          \
   } while (0)
+// stamps from helpers that do not see the engine descriptor (stamps builds):
+// the same buffer, published through a device global by sac_engine_debug_stamps
+__device__ long long* sac_dbg_stamps;
+#define DSTAMP(i)                                                                                          \
+  do {                                                                                                     \
+    if (threadIdx.x == 0 && sac_dbg_stamps) GP(long long, sac_dbg_stamps)[blockIdx.x * 64 + (i)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+// shader-clock counter next to the realtime stamps: clock rate = d(memtime) / d(realtime)
+#define CLK_STAMP(i)                                                                              \
+  do {                                                                                            \
+    if (threadIdx.x == 0 && E.stamps) GP(long long, E.stamps)[blockIdx.x * 64 + (i)] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
 #else
+#define DSTAMP(i) \
+  do {            \
+  } while (0)
+#define CLK_STAMP(i) \
+  do {               \
+  } while (0)
 #define STAMP(i) \
   do {           \
   } while (0)
@@ -206,7 +225,7 @@ __device__ __forceinline__ void pf_issue(Pf<T>& pf, const GemmW& w) {
   pf.tag = w.p;
 #if SAC_PF
   constexpr int KC = MM<T>::KC, FS = 64 * MM<T>::KL;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wave = wave_id();
   if (!w.p || wave >= w.NT) return;
   const int last = w.cols / KC - 1;
   const int nt1 = wave + SAC_NW < w.NT ? wave + SAC_NW : wave;
@@ -224,6 +243,88 @@ __device__ __forceinline__ void pf_issue(Pf<T>& pf, const GemmW& w) {
     pf.f1[u] = MM<T>::ld(b1 + cu * FS);
   }
 #endif
+}
+
+// Held weights: a role that waits on a hand-off (or on its sample) loads the
+// first HC chunks of its wave's first tile pair of a later GEMM step (+ that
+// pair's bias) into registers BEFORE the wait, so the step after the wait starts
+// on resident fragments instead of a cold L2/HBM stream.  Numerically identical
+// to streaming (same fragments, same chunk order).  HC = 8 covers a whole
+// 256-deep bf16 reduction: one 256x256 layer over 8 waves = one pair per wave,
+// 64 VGPRs.
+// f(integral_constant<int, U>) for U = 0..N-1: compile-time indices, so arrays
+// indexed inside stay SSA values (a runtime-indexed loop, even one unrolled
+// later, can leave the array in scratch)
+template <typename F, int... U>
+__device__ __forceinline__ void static_for_(std::integer_sequence<int, U...>, F&& f) {
+  (f(std::integral_constant<int, U>()), ...);
+}
+template <int N, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  static_for_(std::make_integer_sequence<int, N>(), f);
+}
+
+template <typename T, int HC>
+struct Held {
+  typename MM<T>::Frag f0[HC], f1[HC];
+  float b0, b1;
+  const void* tag;  // B matrix held (wave-uniform); gemm_step ignores a mismatch
+};
+template <typename T, int HC, bool COH = false>
+__device__ __forceinline__ void held_issue(Held<T, HC>& h, const GemmW& w) {
+  constexpr uint32_t FSB = 64 * MM<T>::KL * sizeof(T);
+  const int lane = threadIdx.x & 63, wave = wave_id();
+  h.tag = w.p;
+  if (!w.p || wave >= w.NT) return;
+  const int last = w.cols / MM<T>::KC - 1;
+  const int nt1 = wave + SAC_NW < w.NT ? wave + SAC_NW : wave;
+  const __amdgpu_buffer_rsrc_t rs = coh_rsrc(w.p, 0xFFFFFFF0u);
+  const uint32_t o0 = (uint32_t)(packed_lane<T>(wave, w.cols, lane) * sizeof(T));
+  const uint32_t o1 = (uint32_t)(packed_lane<T>(nt1, w.cols, lane) * sizeof(T));
+  if (w.bias) {  // layer_fwd's first pair: n0 = 16 wave + c, n1 = n0 + 16 SAC_NW
+    const int n0 = wave * 16 + (lane & 15), n1 = n0 + 16 * SAC_NW;
+    h.b0 = ldf<COH>(w.bias + (n0 < w.N ? n0 : w.N - 1));
+    h.b1 = ldf<COH>(w.bias + (n1 < w.N ? n1 : w.N - 1));
+  }
+  static_for<HC>([&](auto uc) {
+    constexpr int u = decltype(uc)::value;
+    const uint32_t cu = u < last ? u : last;
+    h.f0[u] = coh_frag<T, COH>(rs, o0 + cu * FSB);
+    h.f1[u] = coh_frag<T, COH>(rs, o1 + cu * FSB);
+  });
+}
+
+// acc{0,1} += A x B for the BM chunks [ch, ch + BM) whose B fragments are in
+// f0 / f1: all BM x RT A fragments are read from LDS first (one LDS round trip
+// for the batch instead of one per chunk), and the has1 test sits outside the
+// MFMA sequence so it stays straight-line.
+template <typename T, int RT, int BM>
+__device__ __forceinline__ void mma_batch(const lf* __restrict__ arow, int lda, int ch, bool has1,
+                                          const typename MM<T>::Frag (&f0)[BM], const typename MM<T>::Frag (&f1)[BM],
+                                          f32x4 (&acc0)[RT], f32x4 (&acc1)[RT]) {
+  constexpr int KC = MM<T>::KC;
+  typename MM<T>::Frag a[BM][RT];
+  static_for<BM>([&](auto uc) {
+    constexpr int u = decltype(uc)::value;
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) a[u][rt] = MM<T>::from_lds(arow + rt * 16 * lda + (ch + u) * KC);
+  });
+  if (has1) {
+    static_for<BM>([&](auto uc) {
+      constexpr int u = decltype(uc)::value;
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) {
+        MM<T>::mma(acc0[rt], a[u][rt], f0[u]);
+        MM<T>::mma(acc1[rt], a[u][rt], f1[u]);
+      }
+    });
+  } else {
+    static_for<BM>([&](auto uc) {
+      constexpr int u = decltype(uc)::value;
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) MM<T>::mma(acc0[rt], a[u][rt], f0[u]);
+    });
+  }
 }
 
 // acc{0,1} += A x B over chunks [ch0, nch) loaded here, in batches of BM chunks
@@ -246,15 +347,8 @@ __device__ __forceinline__ void mma_pair_from(const lf* __restrict__ arow, int l
       f0[u] = coh_frag<T, COH>(rs, o0 + cu * FSB);
       f1[u] = coh_frag<T, COH>(rs, o1 + cu * FSB);
     }
-    if (rem == BM) {  // full batch: straight-line, LDS reads free to be hoisted
-#pragma unroll
-      for (int u = 0; u < BM; ++u)
-#pragma unroll
-        for (int rt = 0; rt < RT; ++rt) {
-          const F a = MM<T>::from_lds(arow + rt * 16 * lda + (ch + u) * KC);
-          MM<T>::mma(acc0[rt], a, f0[u]);
-          if (has1) MM<T>::mma(acc1[rt], a, f1[u]);
-        }
+    if (rem == BM) {  // full batch: every A fragment read from LDS up front, then the MFMAs
+      mma_batch<T, RT, BM>(arow, lda, ch, has1, f0, f1, acc0, acc1);
     } else {
 #pragma unroll
       for (int u = 0; u < BM; ++u)
@@ -269,23 +363,89 @@ __device__ __forceinline__ void mma_pair_from(const lf* __restrict__ arow, int l
   }
 }
 
+// The dominant shape, specialised: exactly one tile pair per wave (N = 32
+// SAC_NW columns: 256 at 8 waves) and NCH reduction chunks known at compile
+// time.  Straight-line: B fragments (held, or all NCH x 2 loads issued
+// together), every A fragment from LDS, the MFMAs, the two epilogues.
+template <typename T, int RT, int NCH, bool COH, int HC, typename Epi>
+__device__ __forceinline__ void gemm_pair_fixed(const lf* __restrict__ arow, int lda, const GemmW& w, int lane,
+                                                int wave, int c, Epi& epi, const Held<T, HC ? HC : 1>* held) {
+  typedef typename MM<T>::Frag F;
+  constexpr int KC = MM<T>::KC;
+  constexpr uint32_t FSB = 64 * MM<T>::KL * sizeof(T);
+  const int nt0 = wave, nt1 = wave + SAC_NW;
+  F f0[NCH], f1[NCH];
+  bool have = false;
+  if constexpr (HC >= NCH) {
+    if (held && held->tag == w.p) {  // uniform
+      static_for<NCH>([&](auto uc) {
+        constexpr int u = decltype(uc)::value;
+        f0[u] = held->f0[u];
+        f1[u] = held->f1[u];
+      });
+      have = true;
+    }
+  }
+  if (!have) {
+    const __amdgpu_buffer_rsrc_t rs = coh_rsrc(w.p, 0xFFFFFFF0u);
+    const uint32_t o0 = (uint32_t)(packed_lane<T>(nt0, w.cols, lane) * sizeof(T));
+    const uint32_t o1 = (uint32_t)(packed_lane<T>(nt1, w.cols, lane) * sizeof(T));
+    static_for<NCH>([&](auto uc) {
+      constexpr int u = decltype(uc)::value;
+      f0[u] = coh_frag<T, COH>(rs, o0 + u * FSB);
+      f1[u] = coh_frag<T, COH>(rs, o1 + u * FSB);
+    });
+  }
+  F a[NCH][RT];
+  static_for<NCH>([&](auto uc) {
+    constexpr int u = decltype(uc)::value;
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) a[u][rt] = MM<T>::from_lds(arow + rt * 16 * lda + u * KC);
+  });
+  f32x4 acc0[RT], acc1[RT];
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt) acc0[rt] = acc1[rt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  static_for<NCH>([&](auto uc) {
+    constexpr int u = decltype(uc)::value;
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) {
+      MM<T>::mma(acc0[rt], a[u][rt], f0[u]);
+      MM<T>::mma(acc1[rt], a[u][rt], f1[u]);
+    }
+  });
+  epi(0, nt0 * 16 + c, acc0, true);
+  epi(1, nt1 * 16 + c, acc1, true);
+}
+
 // One GEMM step over ROWS rows: out tile (r, col) for every col < 16*w.NT,
 // acc = sum_k A[r][k] B[col][k]; epi(h, col, acc[RT]) consumes each tile pair.
 // Batch 0 of the first pair comes from pf; the next step's batch 0 is issued
 // into pf right after those MFMAs.
-template <typename T, int ROWS, bool COH, typename Epi>
+template <typename T, int ROWS, bool COH, int HC, typename Epi>
 __device__ __forceinline__ void gemm_step(const lf* __restrict__ A, int lda, const GemmW& w, Pf<T>& pf,
-                                          const GemmW& next, Epi epi) {
+                                          const GemmW& next, Epi epi, const Held<T, HC ? HC : 1>* held) {
   constexpr int RT = ROWS / 16;
   constexpr int KC = MM<T>::KC, KL = MM<T>::KL;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wave = wave_id();
   const int c = lane & 15, g = lane >> 4;
   const int NT = w.NT, nch = w.cols / KC;
+  const lf* arow = A + c * lda + g * KL;
+#if !SAC_PF
+  if (w.NT == 2 * SAC_NW) {  // one pair per wave (uniform branches)
+    if (nch == 8) {
+      gemm_pair_fixed<T, RT, 8, COH, HC>(arow, lda, w, lane, wave, c, epi, held);
+      return;
+    }
+    if (nch == 1) {
+      gemm_pair_fixed<T, RT, 1, COH, HC>(arow, lda, w, lane, wave, c, epi, held);
+      return;
+    }
+  }
+#endif
   if (pf.tag != w.p) pf_issue<T>(pf, w);  // chain broken by the caller: reload (uniform)
   // weight stream: sc1 buffer loads, coherent with an update phase sharing the launch
   const __amdgpu_buffer_rsrc_t rs = coh_rsrc(w.p, 0xFFFFFFF0u);
-  const lf* arow = A + c * lda + g * KL;
-  auto pair = [&](int nt0, bool first) {
+  auto pair = [&](int nt0, bool first) __attribute__((always_inline)) {
     const int nt1 = nt0 + SAC_NW;
     const bool has1 = nt1 < NT;
     const uint32_t o0 = (uint32_t)(packed_lane<T>(nt0, w.cols, lane) * sizeof(T));
@@ -315,11 +475,29 @@ __device__ __forceinline__ void gemm_step(const lf* __restrict__ A, int lda, con
     }
     mma_pair_from<T, RT, 8, COH>(arow, lda, rs, o0, o1, has1, ch0, nch, acc0, acc1);
 #else
-    (void)first;
-    mma_pair_from<T, RT, 8, COH>(arow, lda, rs, o0, o1, has1, 0, nch, acc0, acc1);
+    if (HC > 0 && first && held && held->tag == w.p) {  // resident fragments (uniform branch)
+      const int hn = nch < HC ? nch : HC;
+      if (hn == HC) {
+        mma_batch<T, RT, (HC ? HC : 1)>(arow, lda, 0, has1, held->f0, held->f1, acc0, acc1);
+      } else {
+        static_for<(HC ? HC : 1)>([&](auto uc) {
+          constexpr int u = decltype(uc)::value;
+          if (u < hn)
+#pragma unroll
+            for (int rt = 0; rt < RT; ++rt) {
+              const typename MM<T>::Frag a = MM<T>::from_lds(arow + rt * 16 * lda + u * KC);
+              MM<T>::mma(acc0[rt], a, held->f0[u]);
+              if (has1) MM<T>::mma(acc1[rt], a, held->f1[u]);
+            }
+        });
+      }
+      if (hn < nch) mma_pair_from<T, RT, 8, COH>(arow, lda, rs, o0, o1, has1, hn, nch, acc0, acc1);
+    } else {
+      mma_pair_from<T, RT, 8, COH>(arow, lda, rs, o0, o1, has1, 0, nch, acc0, acc1);
+    }
 #endif
-    epi(0, nt0 * 16 + c, acc0);
-    if (has1) epi(1, nt1 * 16 + c, acc1);
+    epi(0, nt0 * 16 + c, acc0, first);
+    if (has1) epi(1, nt1 * 16 + c, acc1, first);
   };
   // one instance of the pair code (runtime `first`) keeps the kernel's code small
   bool first = true;
@@ -338,7 +516,7 @@ __device__ __forceinline__ void gemm_step(const lf* __restrict__ A, int lda, con
 // barrier): one act switch per GEMM step instead of one per accumulator element.
 template <int ROWS>
 __device__ __forceinline__ void act_pass_fwd(lf* Y, int ldy, int NT, int act) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wave = wave_id();
   const int c = lane & 15, g = lane >> 4;
 #pragma unroll 1
   for (int nt = wave; nt < NT; nt += SAC_NW)
@@ -351,7 +529,7 @@ __device__ __forceinline__ void act_pass_fwd(lf* Y, int ldy, int NT, int act) {
 }
 template <int ROWS>
 __device__ __forceinline__ void act_pass_bwd(lf* G, int ldg, const lf* P, int ldp, int NT, int K, int act) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wave = wave_id();
   const int c = lane & 15, g = lane >> 4;
 #pragma unroll 1
   for (int nt = wave; nt < NT; nt += SAC_NW) {
@@ -367,13 +545,13 @@ __device__ __forceinline__ void act_pass_bwd(lf* G, int ldg, const lf* P, int ld
 
 // Forward: Y[r][n] = act(sum_k X[r][k] W[n][k] + b[n]) for n < Np (padded -> 0).
 // P (optional) keeps the pre-activation; Pg (optional) stashes rows >= pg_row0.
-template <typename T, int ROWS, bool COH = false>
+template <typename T, int ROWS, bool COH = false, int HC = 0>
 __device__ __forceinline__ void layer_fwd(const lf* X, int ldx, const AS_C LayerDev& L, const float* bias_, int act, lf* P,
                                           int ldp, lf* Y, int ldy, float* Pg_, int pg_row0, Pf<T>& pf,
-                                          const GemmW& next) {
+                                          const GemmW& next, const Held<T, HC ? HC : 1>* held = nullptr) {
   const AS_G float* bias = GPC(float, bias_);
   AS_G float* Pg = GP(float, Pg_);
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wave = wave_id();
   const int g = lane >> 4;
   const int N = L.N, Np = L.Np;
   // The first pair's bias is loaded before the step: a load issued after the
@@ -384,12 +562,16 @@ __device__ __forceinline__ void layer_fwd(const lf* X, int ldx, const AS_C Layer
   if (pf.tag != w.p) pf_issue<T>(pf, w);  // bias arrives with the prefetched weights
   const float bpre0 = pf.b0, bpre1 = pf.b1;
 #else
-  const float bpre0 = ldf<COH>((const float*)bias + (n0 < N ? n0 : N - 1));
-  const float bpre1 = ldf<COH>((const float*)bias + (n1 < N ? n1 : N - 1));
+  const bool hb = HC > 0 && held && held->tag == w.p;  // bias held with the fragments
+  const float bpre0 = hb ? held->b0 : ldf<COH>((const float*)bias + (n0 < N ? n0 : N - 1));
+  const float bpre1 = hb ? held->b1 : ldf<COH>((const float*)bias + (n1 < N ? n1 : N - 1));
 #endif
-  gemm_step<T, ROWS, COH>(X, ldx, w, pf, next, [&](int h, int n, const f32x4* acc) {
+  if (HC == 8) DSTAMP(20);
+  // first: the wave's first tile pair, whose columns are n0 / n1 (bias preloaded)
+  gemm_step<T, ROWS, COH, HC>(X, ldx, w, pf, next, [&](int h, int n, const f32x4* acc, bool first) {
+    if (HC == 8 && h == 0) DSTAMP(21);
     const bool nv = n < N;
-    const float bn = n == n0 ? bpre0 : n == n1 ? bpre1 : ldf<COH>((const float*)bias + (nv ? n : N - 1));
+    const float bn = first ? (h ? bpre1 : bpre0) : ldf<COH>((const float*)bias + (nv ? n : N - 1));
 #pragma unroll
     for (int rt = 0; rt < ROWS / 16; ++rt)
 #pragma unroll
@@ -400,17 +582,20 @@ __device__ __forceinline__ void layer_fwd(const lf* X, int ldx, const AS_C Layer
         Y[r * ldy + n] = act == ACT_RELU ? (p > 0.f ? p : 0.f) : p;
         if (Pg && r >= pg_row0) Pg[(size_t)(r - pg_row0) * Np + n] = p;
       }
-  });
+  }, held);
+  if (HC == 8) DSTAMP(22);
   if (act != ACT_RELU && act != ACT_ID) act_pass_fwd<ROWS>(Y, ldy, Np >> 4, act);
+  if (HC == 8) DSTAMP(23);
 }
 
 // dX: Gout[r][k] = act'(Pprev[r][k]) * sum_n G[r][n] W[n][k]   (act_prev < 0: no act')
-template <typename T, int ROWS, bool COH = false>
+template <typename T, int ROWS, bool COH = false, int HC = 0>
 __device__ __forceinline__ void layer_bwd(const lf* G, int ldg, const AS_C LayerDev& L, const lf* Pprev, int ldp,
-                                          int act_prev, lf* Gout, int ldo, Pf<T>& pf, const GemmW& next) {
+                                          int act_prev, lf* Gout, int ldo, Pf<T>& pf, const GemmW& next,
+                                          const Held<T, HC ? HC : 1>* held = nullptr) {
   const int g = (threadIdx.x & 63) >> 4;
   const int K = L.K;
-  gemm_step<T, ROWS, COH>(G, ldg, gw_bwd(L), pf, next, [&](int, int k, const f32x4* acc) {
+  gemm_step<T, ROWS, COH, HC>(G, ldg, gw_bwd(L), pf, next, [&](int, int k, const f32x4* acc, bool) {
     const bool kv = k < K;
 #pragma unroll
     for (int rt = 0; rt < ROWS / 16; ++rt)
@@ -421,7 +606,7 @@ __device__ __forceinline__ void layer_bwd(const lf* G, int ldg, const AS_C Layer
         if (act_prev == ACT_RELU && !(Pprev[r * ldp + k] > 0.f)) v = 0.f;
         Gout[r * ldo + k] = v;
       }
-  });
+  }, held);
   if (act_prev >= 0 && act_prev != ACT_RELU && act_prev != ACT_ID)
     act_pass_bwd<ROWS>(Gout, ldo, Pprev, ldp, L.Kp >> 4, K, act_prev);
 }
@@ -480,10 +665,12 @@ __device__ __forceinline__ void store_T(const lf* __restrict__ src, int lds_ld, 
 // output layer writes (Pout, Yout) with stride ldo.  keepP: per-layer
 // pre-activations into lds[o_P[l]] (stride ldp[l]).  storeXT: each layer's input
 // transposed into L.XT (ROWS must be SAC_ROWS).  after: the GEMM step that follows.
-template <typename T, int ROWS, bool COH = false>
+// HELD: layers 0 and 1 start on fragments held in h0 / h1 (see Held).
+template <typename T, int ROWS, bool COH = false, bool HELD = false>
 __device__ __forceinline__ void mlp_forward(const AS_C NetDev& net, lf* Xb, lf* Yb, int ld, lf* Pout, lf* Yout, int ldo,
                                             const AS_C int* o_P, const AS_C int* ldp, lf* lds, bool keepP, bool storeXT, int Bp,
-                                            int col0, int nvalid, Pf<T>& pf, const GemmW& after) {
+                                            int col0, int nvalid, Pf<T>& pf, const GemmW& after,
+                                            const Held<T, 1>* h0 = nullptr, const Held<T, 8>* h1 = nullptr) {
   lf* X = Xb;
   lf* Y = Yb;
   for (int l = 0; l < net.L; ++l) {
@@ -493,11 +680,17 @@ __device__ __forceinline__ void mlp_forward(const AS_C NetDev& net, lf* Xb, lf* 
     if (storeXT) {
       if constexpr (ROWS == SAC_ROWS) store_T<T, ROWS>(X, ld, Ly.Kp, Ly.K, Ly.XT, Bp, col0, nvalid, nullptr);
     }
-    if (out)
-      layer_fwd<T, ROWS, COH>(X, ld, Ly, net.P + Ly.b_off, net.out_act, Pout, ldo, Yout, ldo, nullptr, 0, pf, next);
+    const int act = out ? net.out_act : net.hid_act;
+    lf* Pl = out ? Pout : (keepP ? lds + o_P[l] : nullptr);
+    const int ldpl = out ? ldo : (keepP ? ldp[l] : 0);
+    lf* Yl = out ? Yout : Y;
+    const int ldyl = out ? ldo : ld;
+    if (HELD && l == 0)
+      layer_fwd<T, ROWS, COH, 1>(X, ld, Ly, net.P + Ly.b_off, act, Pl, ldpl, Yl, ldyl, nullptr, 0, pf, next, h0);
+    else if (HELD && l == 1)
+      layer_fwd<T, ROWS, COH, 8>(X, ld, Ly, net.P + Ly.b_off, act, Pl, ldpl, Yl, ldyl, nullptr, 0, pf, next, h1);
     else
-      layer_fwd<T, ROWS, COH>(X, ld, Ly, net.P + Ly.b_off, net.hid_act, keepP ? lds + o_P[l] : nullptr,
-                         keepP ? ldp[l] : 0, Y, ld, nullptr, 0, pf, next);
+      layer_fwd<T, ROWS, COH>(X, ld, Ly, net.P + Ly.b_off, act, Pl, ldpl, Yl, ldyl, nullptr, 0, pf, next);
     __syncthreads();
     lf* t = X;
     X = Y;
@@ -508,15 +701,18 @@ __device__ __forceinline__ void mlp_forward(const AS_C NetDev& net, lf* Xb, lf* 
 // Backward from d(output pre-activation) Gout [ROWS][ldo] down to layer 0's
 // pre-activation gradient.  storeGT: each layer's dY^T + bias partial sums.
 // Returns the buffer (stride ld) holding d(pre-act of layer 0).
-template <typename T, int ROWS, bool COH = false>
+// HELD: the output layer's and layer Lh-1's dX steps start on fragments held
+// in h0 / h1 (see Held).
+template <typename T, int ROWS, bool COH = false, bool HELD = false>
 __device__ __forceinline__ lf* mlp_backward(const AS_C NetDev& net, const lf* Gout, int ldo, lf* Xb, lf* Yb, int ld,
                                             const AS_C int* o_P, const AS_C int* ldp, lf* lds, bool storeGT, int Bp, int col0,
-                                            int nvalid, Pf<T>& pf, const GemmW& after) {
+                                            int nvalid, Pf<T>& pf, const GemmW& after,
+                                            const Held<T, 1>* h0 = nullptr, const Held<T, 8>* h1 = nullptr) {
   const int Lh = net.L - 1;
   const AS_C LayerDev& Lo = net.l[Lh];
   if (storeGT) store_T<T, ROWS>(Gout, ldo, Lo.Np, Lo.N, Lo.GT, Bp, col0, nvalid, Lo.dbp);
-  layer_bwd<T, ROWS, COH>(Gout, ldo, Lo, lds + o_P[Lh - 1], ldp[Lh - 1], net.hid_act, Yb, ld, pf,
-                     Lh - 1 >= 1 ? gw_bwd(net.l[Lh - 1]) : after);
+  layer_bwd<T, ROWS, COH, HELD ? 1 : 0>(Gout, ldo, Lo, lds + o_P[Lh - 1], ldp[Lh - 1], net.hid_act, Yb, ld, pf,
+                                        Lh - 1 >= 1 ? gw_bwd(net.l[Lh - 1]) : after, (const Held<T, 1>*)h0);
   __syncthreads();
   lf* G = Yb;
   lf* Gn = Xb;
@@ -524,7 +720,11 @@ __device__ __forceinline__ lf* mlp_backward(const AS_C NetDev& net, const lf* Go
     const AS_C LayerDev& Ly = net.l[l];
     if (storeGT) store_T<T, ROWS>(G, ld, Ly.Np, Ly.N, Ly.GT, Bp, col0, nvalid, Ly.dbp);
     if (l == 0) break;
-    layer_bwd<T, ROWS, COH>(G, ld, Ly, lds + o_P[l - 1], ldp[l - 1], net.hid_act, Gn, ld, pf,
+    if (HELD && l == Lh - 1)
+      layer_bwd<T, ROWS, COH, 8>(G, ld, Ly, lds + o_P[l - 1], ldp[l - 1], net.hid_act, Gn, ld, pf,
+                                 l - 1 >= 1 ? gw_bwd(net.l[l - 1]) : after, h1);
+    else
+      layer_bwd<T, ROWS, COH>(G, ld, Ly, lds + o_P[l - 1], ldp[l - 1], net.hid_act, Gn, ld, pf,
                        l - 1 >= 1 ? gw_bwd(net.l[l - 1]) : after);
     __syncthreads();
     lf* t = G;
@@ -647,7 +847,7 @@ __device__ __forceinline__ void dw_adam_tile(const AS_C EngineDev& E, const Tile
     for (int rt = bs; rt < td.nrt; rt += 8) bsum += GPC(float, td.dbp)[(size_t)rt * td.N + td.n0 + bn];
   // ---- 2. dW = dY^T X over the batch, staged through LDS in 512-B row chunks;
   // waves 0-3 run one 16x16 sub-tile each, chunks in batch order
-  const int lane = tid & 63, wave = tid >> 6;
+  const int lane = tid & 63, wave = wave_id();
   const int c = lane & 15, g = lane >> 4;
   const int ns = (wave >> 1) * 16, ks = (wave & 1) * 16;
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
@@ -939,6 +1139,7 @@ __device__ __forceinline__ void target_critic_body(const EngineDev* __restrict__
   }
   const bool do_pi = !ROLES || role == 0 || role == 5;
   STAMP(0);
+  CLK_STAMP(40);
   const int B = E.B, Bp = E.Bp, O = E.O, A = E.A, ld = E.ld, ldo = E.ldo;
   const int r0 = rbi * R;
   const int nvalid = min(R, B - r0);
@@ -966,6 +1167,15 @@ __device__ __forceinline__ void target_critic_body(const EngineDev* __restrict__
   Pf<T> pf;  // this role's first GEMM streams in under the sample / gather
   pf_issue<T>(pf, !ROLES || do_pi ? gw_fwd(pi.l[0])
                   : gw_fwd(E.net[role <= 2 ? NET_Q1T + role - 1 : NET_Q1 + role - 3].l[0]));
+  // pi(s') (the critical path): layers 0 and 1 held under the sample / gather
+  // (after phase D's count when D shares the launch)
+  Held<T, 1> ph0;
+  Held<T, 8> ph1;
+  ph0.tag = ph1.tag = nullptr;
+  if (!WITH_D && ROLES && role == 0) {
+    held_issue<T, 1>(ph0, gw_fwd(pi.l[0]));
+    held_issue<T, 8>(ph1, gw_fwd(pi.l[1]));
+  }
   const AS_G float* obs = GPC(float, rb.obs);
   const AS_G float* nobs = GPC(float, rb.next_obs);
   const AS_G float* ract = GPC(float, rb.act);
@@ -1077,12 +1287,18 @@ __device__ __forceinline__ void target_critic_body(const EngineDev* __restrict__
         store_T<T, R>(X + a0 * ld, ld, Ly.Kp, Ly.K, (T*)Ly.XT + par * Ly.xt_par, Bp, r0, nvalid, nullptr);
       if (l == 0) STAMP(57);
       float* stash = act ? Ly.pstash + (size_t)r0 * Ly.Np : nullptr;
-      if (l == pi.L - 1)
-        layer_fwd<T, ROWS, WITH_D>(X, ld, Ly, pi.P + Ly.b_off, pi.out_act, outP, ldo, outB, ldo, stash, a0, pf,
-                           gw_fwd(E.net[NET_Q1T].l[0]));
+      const bool out = l == pi.L - 1;
+      const int act_l = out ? pi.out_act : pi.hid_act;
+      lf* Pl = out ? outP : nullptr;
+      lf* Yl = out ? outB : Y;
+      const int ldl = out ? ldo : ld;
+      const GemmW nx = out ? gw_fwd(E.net[NET_Q1T].l[0]) : gw_fwd(pi.l[l + 1]);
+      if (l == 0)
+        layer_fwd<T, ROWS, WITH_D, 1>(X, ld, Ly, pi.P + Ly.b_off, act_l, Pl, ldl, Yl, ldl, stash, a0, pf, nx, &ph0);
+      else if (l == 1)
+        layer_fwd<T, ROWS, WITH_D, 8>(X, ld, Ly, pi.P + Ly.b_off, act_l, Pl, ldl, Yl, ldl, stash, a0, pf, nx, &ph1);
       else
-        layer_fwd<T, ROWS, WITH_D>(X, ld, Ly, pi.P + Ly.b_off, pi.hid_act, nullptr, 0, Y, ld, stash, a0, pf,
-                           gw_fwd(pi.l[l + 1]));
+        layer_fwd<T, ROWS, WITH_D>(X, ld, Ly, pi.P + Ly.b_off, act_l, Pl, ldl, Yl, ldl, stash, a0, pf, nx);
       __syncthreads();
       STAMP(2 + l);
       lf* t = X;
@@ -1146,7 +1362,13 @@ __device__ __forceinline__ void target_critic_body(const EngineDev* __restrict__
   if (!ROLES) {
     pi_forward_head(std::integral_constant<int, 2 * R>(), true, true);
   } else if (role == 0 || role == 5) {
-    if (WITH_D) count_wait(E, SYNC_DDONE, (uint32_t)E.nD + 1u);  // pi updated by the previous step's phase D
+    if (WITH_D) {
+      count_wait(E, SYNC_DDONE, (uint32_t)E.nD + 1u);  // pi updated by the previous step's phase D
+      if (role == 0) {
+        held_issue<T, 1, true>(ph0, gw_fwd(pi.l[0]));
+        held_issue<T, 8, true>(ph1, gw_fwd(pi.l[1]));
+      }
+    }
     STAMP(59);
     pi_forward_head(std::integral_constant<int, R>(), role == 0, role == 5);
   }
@@ -1154,7 +1376,12 @@ __device__ __forceinline__ void target_critic_body(const EngineDev* __restrict__
   // ---- target twin-Q (agent.py:195-211)
   const float alpha32 = (float)*GPC(double, E.alpha_state + 1);
   if (!ROLES || role == 1 || role == 2) {
+    // role split: the target critic's layers 0 and 1 held while a~' is computed
+    Held<T, 1> qh0;
+    Held<T, 8> qh1;
     if (ROLES) {
+      held_issue<T, 1>(qh0, gw_fwd(E.net[NET_Q1T + role - 1].l[0]));
+      held_issue<T, 8>(qh1, gw_fwd(E.net[NET_Q1T + role - 1].l[1]));
       hand_wait(E, HK_PI, rbi, ep);
       const AS_G float* h = hand_data(E, HK_PI, rbi);
       for (int i = tid; i < R * A; i += SAC_THREADS) a2B[i] = ld_sc1(h + i);
@@ -1168,8 +1395,8 @@ __device__ __forceinline__ void target_critic_body(const EngineDev* __restrict__
         Xb[r * ld + k] = k < O ? s2B[r * O + k] : (k < O + A ? a2B[r * A + (k - O)] : 0.f);
       }
       __syncthreads();
-      mlp_forward<T, R>(q, Xb, Yb, ld, outP, outB, ldo, E.o_P1, E.ldp1, lds, false, false, Bp, r0, nvalid, pf,
-                        gw_fwd(E.net[t ? NET_Q1 : NET_Q2T].l[0]));
+      mlp_forward<T, R, false, ROLES>(q, Xb, Yb, ld, outP, outB, ldo, E.o_P1, E.ldp1, lds, false, false, Bp, r0,
+                                      nvalid, pf, gw_fwd(E.net[t ? NET_Q1 : NET_Q2T].l[0]), &qh0, &qh1);
       if (tid < R) {
         qtB[t * R + tid] = outB[tid * ldo];
         if (ROLES) st_sc1(hand_data(E, HK_T1 + t, rbi) + tid, outB[tid * ldo]);
@@ -1284,6 +1511,7 @@ __global__ void __launch_bounds__(SAC_THREADS) sac_target_critic(const EngineDev
   const AS_C EngineDev& E = *(const AS_C EngineDev*)Ep;
   (void)E;
   END_STAMP(60);
+  CLK_STAMP(41);
 }
 
 // ============================================================================ phase C
@@ -1347,6 +1575,12 @@ __device__ __forceinline__ void actor_body(const EngineDev* __restrict__ Ep, int
   if (!ROLES || role >= 1) {
     const int q_lo = ROLES ? role - 1 : 0, q_hi = ROLES ? role : 2;
     if (WITH_B) count_wait(E, SYNC_BDONE + 16 * q_lo, (uint32_t)E.nBq[q_lo]);  // this critic updated
+    Held<T, 1> ch0;
+    Held<T, 8> ch1;
+    if (ROLES) {  // one critic per role: its layers 0 and 1 held under the input loads
+      held_issue<T, 1, WITH_B>(ch0, gw_fwd(E.net[NET_Q1 + q_lo].l[0]));
+      held_issue<T, 8, WITH_B>(ch1, gw_fwd(E.net[NET_Q1 + q_lo].l[1]));
+    }
     STAMP(33);
     // ---- Q1, Q2 on (s, a~) with the updated critics (agent.py:244-248)
     for (int qi = q_lo; qi < q_hi; ++qi) {
@@ -1357,10 +1591,11 @@ __device__ __forceinline__ void actor_body(const EngineDev* __restrict__ Ep, int
         Xb[r * ld + k] = k < O ? sB[r * O + k] : (k < O + A ? aB[r * A + (k - O)] : 0.f);
       }
       __syncthreads();
-      mlp_forward<T, R, WITH_B>(q, Xb, Yb, ld, qi ? outP2 : outP1, qi ? out2 : out1, ldo, qi ? E.o_P2 : E.o_P1,
-                        qi ? E.ldp2 : E.ldp1, lds, true, false, Bp, r0, nvalid, pf,
-                        ROLES ? gw_bwd(q.l[q.L - 1])
-                        : qi ? gw_bwd(E.net[NET_Q1].l[E.net[NET_Q1].L - 1]) : gw_fwd(E.net[NET_Q2].l[0]));
+      mlp_forward<T, R, WITH_B, ROLES>(q, Xb, Yb, ld, qi ? outP2 : outP1, qi ? out2 : out1, ldo,
+                                       qi ? E.o_P2 : E.o_P1, qi ? E.ldp2 : E.ldp1, lds, true, false, Bp, r0, nvalid, pf,
+                                       ROLES ? gw_bwd(q.l[q.L - 1])
+                                       : qi ? gw_bwd(E.net[NET_Q1].l[E.net[NET_Q1].L - 1]) : gw_fwd(E.net[NET_Q2].l[0]),
+                                       &ch0, &ch1);
       STAMP(36 + qi);
     }
     // ---- backward seeds.  L_pi = mean(alpha logpi - min Q) (agent.py:251-252); min
@@ -1426,6 +1661,14 @@ __device__ __forceinline__ void actor_body(const EngineDev* __restrict__ Ep, int
     lf* P = lds + E.o_P1[l];
     const AS_G float* ps = GPC(float, Ly.pstash) + (size_t)r0 * Ly.Np;
     for (int i = tid; i < R * Ly.Np; i += SAC_THREADS) P[(i / Ly.Np) * ldp + i % Ly.Np] = ps[i];
+  }
+  // pi's last two dX steps held while the critics run (pi is not written in this launch)
+  Held<T, 1> bh0;
+  Held<T, 8> bh1;
+  bh0.tag = bh1.tag = nullptr;
+  if (ROLES) {
+    held_issue<T, 1>(bh0, gw_bwd(pi.l[pi.L - 1]));
+    held_issue<T, 8>(bh1, gw_bwd(pi.l[pi.L - 2]));
   }
   if (ROLES) {  // combine the critics' unit-seed gradients with the min-Q weights
     hand_wait(E, HK_C1, rbi, ep);
@@ -1493,7 +1736,8 @@ __device__ __forceinline__ void actor_body(const EngineDev* __restrict__ Ep, int
     for (int i = tid; i < R * pad; i += SAC_THREADS) goutB[(i / pad) * ldo + 2 * A + i % pad] = 0.f;
   }
   __syncthreads();
-  mlp_backward<T, R>(pi, goutB, ldo, Xb, Yb, ld, E.o_P1, E.ldp1, lds, true, Bp, r0, nvalid, pf, gw_none());
+  mlp_backward<T, R, false, true>(pi, goutB, ldo, Xb, Yb, ld, E.o_P1, E.ldp1, lds, true, Bp, r0, nvalid, pf, gw_none(),
+                                  &bh0, &bh1);
   STAMP(35);
 }
 
