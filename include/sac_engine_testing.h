@@ -16,6 +16,9 @@ int sac_engine_debug_stamped(void);
  * with D inside, 5 C with B inside) on the stream.  Timing experiments only:
  * re-running a phase out of sequence advances or corrupts the training state. */
 int sac_engine_debug_launch(sac_engine* e, const sac_replay* rb, int32_t kind, void* stream);
+/* The last step whose phase A took its batch from the record phase C staged
+ * (0: none yet); synchronises the stream. */
+int sac_engine_debug_staged_step(sac_engine* e, uint64_t* step_out, void* stream);
 /* 1 if phases A/C run role-split (per-network workgroups with in-launch
  * hand-offs), 0 if one workgroup per row tile runs all networks. */
 int sac_engine_uses_roles(const sac_engine *e);

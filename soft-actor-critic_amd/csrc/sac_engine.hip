@@ -247,6 +247,8 @@ static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
   h.alpha_sc = (double*)P(lay.take(2 * 2 * 8));
   h.sync = (uint32_t*)P(lay.take((size_t)(SYNC_FLAGS + HK_COUNT * nrt * 16) * 4));
   h.hand = (float*)P(lay.take((size_t)HK_COUNT * nrt * SAC_HAND_STRIDE * 4));
+  h.stg_stride = (16 + 2 * SAC_ROWS * O + SAC_ROWS * A + 2 * SAC_ROWS + 15) / 16 * 16;
+  h.stg = (float*)P(lay.take((size_t)nrt * h.stg_stride * 4));
   int nB = 0, nD = 0;
   for (int ni = NET_PI; ni <= NET_Q2; ++ni)
     for (int l = 0; l < h.net[ni].L; ++l)
@@ -317,6 +319,10 @@ static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
       int roles = 6 * nrt <= 256 && SAC_ROWS * (A + 1) <= SAC_HAND_STRIDE;
       if (const char* v = getenv("SAC_ROLES")) roles = roles && atoi(v) != 0;
       h.roles = roles;
+      // phase C stages the next step's batch (SAC_STAGE=0 turns it off)
+      int stage = 1;
+      if (const char* v = getenv("SAC_STAGE")) stage = atoi(v) != 0;
+      h.stage = stage;
     }
     h.auto_entropy = c->auto_entropy;
     h.gamma = c->gamma;
@@ -435,6 +441,7 @@ template <typename T>
 static void launch_kind(sac_engine* e, int kind, const sac_replay* rb, const int32_t* idx, const float* eps,
                         hipStream_t s) {
   const size_t lf = std::max(e->lds_bytes, (size_t)SAC_UPD_LDS);
+  const int stg = e->h.stage ? e->nrt : 0;  // stager blocks of phase C
   switch (kind) {
     case L_A:
       if (e->h.roles)
@@ -447,9 +454,9 @@ static void launch_kind(sac_engine* e, int kind, const sac_replay* rb, const int
       break;
     case L_C:
       if (e->h.roles)
-        sac_actor<T, true, false><<<e->nrt * 3, SAC_THREADS, lf, s>>>(e->d);
+        sac_actor<T, true, false><<<e->nrt * 3 + stg, SAC_THREADS, lf, s>>>(e->d, *rb);
       else
-        sac_actor<T, false, false><<<e->nrt * e->h.xs, SAC_THREADS, lf, s>>>(e->d);
+        sac_actor<T, false, false><<<e->nrt * e->h.xs + stg, SAC_THREADS, lf, s>>>(e->d, *rb);
       break;
     case L_D:
       sac_actor_update<T><<<e->nD + 1, SAC_UPD_THREADS, SAC_UPD_LDS, s>>>(e->d, e->tilesD, e->nD);
@@ -458,7 +465,7 @@ static void launch_kind(sac_engine* e, int kind, const sac_replay* rb, const int
       sac_target_critic<T, true, true><<<e->nD + 1 + e->nrt * 6, SAC_THREADS, lf, s>>>(e->d, *rb, idx, eps);
       break;
     case L_BC:
-      sac_actor<T, true, true><<<e->nB + e->nrt * 3, SAC_THREADS, lf, s>>>(e->d);
+      sac_actor<T, true, true><<<e->nB + e->nrt * 3 + stg, SAC_THREADS, lf, s>>>(e->d, *rb);
       break;
   }
 }
@@ -600,6 +607,14 @@ int sac_engine_check(sac_engine* e, void* stream) {
   HIPCHK(hipMemcpyAsync(w, e->h.sync, sizeof(w), hipMemcpyDeviceToHost, (hipStream_t)stream));
   HIPCHK(hipStreamSynchronize((hipStream_t)stream));
   if (w[1]) return fail(SAC_E_HIP, "a workgroup hand-off timed out: results of the affected steps are invalid");
+  return SAC_OK;
+}
+
+int sac_engine_debug_staged_step(sac_engine* e, uint64_t* step_out, void* stream) {
+  if (!e || !step_out) return fail(SAC_E_INVALID, "bad debug_staged_step arguments");
+  HIPCHK(hipMemcpyAsync(step_out, e->h.sync + SYNC_STAGED, sizeof(uint64_t), hipMemcpyDeviceToHost,
+                        (hipStream_t)stream));
+  HIPCHK(hipStreamSynchronize((hipStream_t)stream));
   return SAC_OK;
 }
 

@@ -100,6 +100,13 @@ struct EngineDev {
   float* hand;     // hand-off payloads [HK_COUNT][nrt][SAC_HAND_STRIDE]
   float* stats;
   long long* stamps;  // optional in-kernel timestamps (SAC_STAMPS builds)
+  // Next-step batch staging: phase C's stager blocks sample and gather step
+  // t+1's rows per row tile into stg (header: step, replay size, replay write
+  // slot, replay obs pointer; then s, s', a, r, d); phase A of step t+1 uses a
+  // record whose header matches and gathers itself otherwise.
+  float* stg;
+  int stg_stride;  // floats per row-tile record
+  int stage;       // stager blocks launched with phase C
   // LDS layout (float offsets)
   int o_X, o_Y, o_P1[SAC_DEV_LAYERS], ldp1[SAC_DEV_LAYERS], o_P2[SAC_DEV_LAYERS], ldp2[SAC_DEV_LAYERS];
   int o_s, o_s2, o_a, o_a2, o_r, o_d, o_et, o_ea, o_out, o_outp, o_out2, o_outp2, o_lp, o_qt, o_y, o_g, o_g2,
@@ -142,7 +149,10 @@ struct TileDesc {
     STAMP(i);                                          \
   } while (0)
 // stamps from helpers that do not see the engine descriptor (stamps builds):
-// the same buffer, published through a device global by sac_engine_debug_stamps
+// the same buffer, published through a device global by sac_engine_debug_stamps.
+// Reading that global waits (vmcnt) for every load the wave has in flight, so a
+// probe placed after register-held weight loads serialises them: measured
+// layer times there are not the real ones.
 __device__ long long* sac_dbg_stamps;
 #define DSTAMP(i)                                                                                          \
   do {                                                                                                     \
@@ -566,10 +576,8 @@ __device__ __forceinline__ void layer_fwd(const lf* X, int ldx, const AS_C Layer
   const float bpre0 = hb ? held->b0 : ldf<COH>((const float*)bias + (n0 < N ? n0 : N - 1));
   const float bpre1 = hb ? held->b1 : ldf<COH>((const float*)bias + (n1 < N ? n1 : N - 1));
 #endif
-  if (HC == 8) DSTAMP(20);
   // first: the wave's first tile pair, whose columns are n0 / n1 (bias preloaded)
   gemm_step<T, ROWS, COH, HC>(X, ldx, w, pf, next, [&](int h, int n, const f32x4* acc, bool first) {
-    if (HC == 8 && h == 0) DSTAMP(21);
     const bool nv = n < N;
     const float bn = first ? (h ? bpre1 : bpre0) : ldf<COH>((const float*)bias + (nv ? n : N - 1));
 #pragma unroll
@@ -583,9 +591,7 @@ __device__ __forceinline__ void layer_fwd(const lf* X, int ldx, const AS_C Layer
         if (Pg && r >= pg_row0) Pg[(size_t)(r - pg_row0) * Np + n] = p;
       }
   }, held);
-  if (HC == 8) DSTAMP(22);
   if (act != ACT_RELU && act != ACT_ID) act_pass_fwd<ROWS>(Y, ldy, Np >> 4, act);
-  if (HC == 8) DSTAMP(23);
 }
 
 // dX: Gout[r][k] = act'(Pprev[r][k]) * sum_n G[r][n] W[n][k]   (act_prev < 0: no act')
@@ -1021,7 +1027,8 @@ __device__ __forceinline__ void alpha_and_losses(const AS_C EngineDev& E, int pa
 // indices than their consumers and the grid fits one block per CU, so every
 // spin terminates; spins are still bounded and set E.sync[1] on a timeout.
 enum HandKind { HK_PI = 0, HK_T1 = 1, HK_T2 = 2, HK_C1 = 3, HK_C2 = 4, HK_COUNT = 5 };
-enum SyncWord { SYNC_EPOCH = 0, SYNC_TIMEOUT = 1, SYNC_DDONE = 16, SYNC_BDONE = 32, SYNC_CDONE = 64, SYNC_FLAGS = 128 };
+// SYNC_STAGED (u64 at words 4-5): step whose phase A last used a staged batch record
+enum SyncWord { SYNC_EPOCH = 0, SYNC_TIMEOUT = 1, SYNC_STAGED = 4, SYNC_DDONE = 16, SYNC_BDONE = 32, SYNC_CDONE = 64, SYNC_FLAGS = 128 };
 #define SAC_HAND_STRIDE 576  // floats per (kind, row tile) payload: >= SAC_ROWS * (act_dim + 1)
 
 __device__ __forceinline__ AS_G uint32_t* hand_flag(const AS_C EngineDev& E, int kind, int rbi) {
@@ -1091,6 +1098,87 @@ __device__ __forceinline__ void count_wait(const AS_C EngineDev& E, int word, ui
     }
   }
   __syncthreads();
+}
+
+// ============================================================================ sample + gather
+// Row tile r0's replay slots for `step` (replay_buffer.py:32-39: distinct
+// uniform logical rows, 0 = oldest; -1 for padding rows): threads tid < R.
+__device__ __forceinline__ void tile_slots(const AS_C EngineDev& E, const sac_replay& rb, uint64_t step,
+                                           int64_t rb_size, int64_t rb_pos, int r0, const AS_G int32_t* inj_idx,
+                                           AS_L int64_t* slotB) {
+  const int tid = threadIdx.x;
+  if (tid < SAC_ROWS) {
+    int64_t slot = -1;
+    const int b = r0 + tid;
+    if (b < E.B) {
+      int64_t li;
+      if (inj_idx) {
+        li = inj_idx[b];
+      } else {
+        const Feistel f = feistel_make(E.seed, step, rb_size);
+        li = feistel_sample(f, b, rb_size);
+      }
+      slot = rb_size < rb.capacity ? li : (rb_pos + li) % rb.capacity;
+    }
+    slotB[tid] = slot;
+  }
+}
+
+// Gather the tile's rows (agent.py:166-193) into s, s2 [R][O], a [R][A], r, d [R]
+// (LDS or global): one pass, every load unconditional (row 0 for padding rows).
+template <typename Dst>
+__device__ __forceinline__ void gather_rows(const sac_replay& rb, const AS_L int64_t* slotB, int O, int A, Dst s,
+                                            Dst s2, Dst a, Dst r, Dst d) {
+  constexpr int R = SAC_ROWS;
+  const AS_G float* obs = GPC(float, rb.obs);
+  const AS_G float* nobs = GPC(float, rb.next_obs);
+  const AS_G float* ract = GPC(float, rb.act);
+  const AS_G float* rrew = GPC(float, rb.rew);
+  const AS_G float* rdone = GPC(float, rb.done);
+  const int nI = R * (O > A ? O : A);
+  for (int i = threadIdx.x; i < nI; i += SAC_THREADS) {
+    const int io = i < R * O ? i : R * O - 1, ia = i < R * A ? i : R * A - 1, ir = i < R ? i : R - 1;
+    const int64_t so = slotB[io / O], sa = slotB[ia / A], sr = slotB[ir];
+    const int64_t po = (so < 0 ? 0 : so) * O + io % O, pa = (sa < 0 ? 0 : sa) * A + ia % A, pr = sr < 0 ? 0 : sr;
+    const float vo = obs[po], vn = nobs[po], va = ract[pa], vr = rrew[pr], vd = rdone[pr];
+    if (i < R * O) {
+      s[i] = so >= 0 ? vo : 0.f;
+      s2[i] = so >= 0 ? vn : 0.f;
+    }
+    if (i < R * A) a[i] = sa >= 0 ? va : 0.f;
+    if (i < R) {
+      r[i] = sr >= 0 ? vr : 0.f;
+      d[i] = sr >= 0 ? vd : 0.f;
+    }
+  }
+}
+
+// Stager block (phase C): step t+1's rows of row tile rbi into E.stg.  Phase C
+// is the step's last reader of the previous record (phase A of step t consumed
+// it before this launch began); the next launch sees the stores.
+__device__ __forceinline__ void stage_next_batch(const AS_C EngineDev& E, const sac_replay& rb, int rbi, lf* lds) {
+  constexpr int R = SAC_ROWS;
+  const uint64_t step = *GPC(uint64_t, E.rng_step) + 1;  // advanced at the end of this launch
+  const int64_t rb_size = GPC(int64_t, rb.state)[0], rb_pos = GPC(int64_t, rb.state)[1];
+  AS_G float* rec = GP(float, E.stg) + (size_t)rbi * E.stg_stride;
+  AS_G uint64_t* hdr = (AS_G uint64_t*)rec;
+  if (rb_size < E.B) {  // nothing to sample: leave no matching record
+    if (threadIdx.x == 0) hdr[0] = ~0ull;
+    return;
+  }
+  AS_L int64_t* slotB = (AS_L int64_t*)lds;
+  tile_slots(E, rb, step, rb_size, rb_pos, rbi * R, nullptr, slotB);
+  __syncthreads();
+  const int O = E.O, A = E.A;
+  AS_G float* p = rec + 16;
+  gather_rows<AS_G float*>(rb, slotB, O, A, p, p + R * O, p + 2 * R * O, p + 2 * R * O + R * A,
+                           p + 2 * R * O + R * A + R);
+  if (threadIdx.x == 0) {
+    hdr[0] = step;
+    hdr[1] = (uint64_t)rb_size;
+    hdr[2] = (uint64_t)rb_pos;
+    hdr[3] = (uint64_t)(uintptr_t)rb.obs;
+  }
 }
 
 // ============================================================================ phase A
@@ -1176,11 +1264,6 @@ __device__ __forceinline__ void target_critic_body(const EngineDev* __restrict__
     held_issue<T, 1>(ph0, gw_fwd(pi.l[0]));
     held_issue<T, 8>(ph1, gw_fwd(pi.l[1]));
   }
-  const AS_G float* obs = GPC(float, rb.obs);
-  const AS_G float* nobs = GPC(float, rb.next_obs);
-  const AS_G float* ract = GPC(float, rb.act);
-  const AS_G float* rrew = GPC(float, rb.rew);
-  const AS_G float* rdone = GPC(float, rb.done);
   AS_G float* stats = GP(float, E.stats);
 
   // optimizer step counters and this step's Adam bias-correction scalars
@@ -1207,39 +1290,30 @@ __device__ __forceinline__ void target_critic_body(const EngineDev* __restrict__
   }
 
   const int64_t rb_size = GPC(int64_t, rb.state)[0], rb_pos = GPC(int64_t, rb.state)[1];
-  if (tid < R) {
-    int64_t slot = -1;
-    const int b = r0 + tid;
-    if (b < B) {
-      int64_t li;
-      if (inj_idx) {
-        li = inj_idx[b];
-      } else {
-        const Feistel f = feistel_make(E.seed, step, rb_size);
-        li = feistel_sample(f, b, rb_size);
-      }
-      slot = rb_size < rb.capacity ? li : (rb_pos + li) % rb.capacity;
+  bool staged = false;
+  if (E.stage && !inj_idx) {  // the record phase C staged for this step: copied speculatively,
+    // its loads in flight together with the step / replay-state loads above
+    const AS_G float* rec = GPC(float, E.stg) + (size_t)rbi * E.stg_stride;
+    const AS_C uint64_t* hdr = (const AS_C uint64_t*)rec;
+    const AS_G float* p = rec + 16;
+    for (int i = tid; i < R * O; i += SAC_THREADS) {
+      sB[i] = p[i];
+      s2B[i] = p[R * O + i];
     }
-    slotB[tid] = slot;
+    for (int i = tid; i < R * A; i += SAC_THREADS) aB[i] = p[2 * R * O + i];
+    if (tid < R) {
+      rB[tid] = p[2 * R * O + R * A + tid];
+      dB[tid] = p[2 * R * O + R * A + R + tid];
+    }
+    staged = hdr[0] == step && hdr[1] == (uint64_t)rb_size && hdr[2] == (uint64_t)rb_pos &&
+             hdr[3] == (uint64_t)(uintptr_t)rb.obs;
   }
-  __syncthreads();
-  {  // one pass, every load unconditional (clamped row 0 for padding rows): one round trip
-    const int nI = R * (O > A ? O : A);
-    for (int i = tid; i < nI; i += SAC_THREADS) {
-      const int io = i < R * O ? i : R * O - 1, ia = i < R * A ? i : R * A - 1, ir = i < R ? i : R - 1;
-      const int64_t so = slotB[io / O], sa = slotB[ia / A], sr = slotB[ir];
-      const int64_t po = (so < 0 ? 0 : so) * O + io % O, pa = (sa < 0 ? 0 : sa) * A + ia % A, pr = sr < 0 ? 0 : sr;
-      const float vo = obs[po], vn = nobs[po], va = ract[pa], vr = rrew[pr], vd = rdone[pr];
-      if (i < R * O) {
-        sB[i] = so >= 0 ? vo : 0.f;
-        s2B[i] = so >= 0 ? vn : 0.f;
-      }
-      if (i < R * A) aB[i] = sa >= 0 ? va : 0.f;
-      if (i < R) {
-        rB[i] = sr >= 0 ? vr : 0.f;
-        dB[i] = sr >= 0 ? vd : 0.f;
-      }
-    }
+  if (staged && rbi == 0 && (!ROLES || role == 0) && tid == 0)
+    *(AS_G uint64_t*)(GP(uint32_t, E.sync) + 4) = step;  // SYNC_STAGED: the staged path ran (tests)
+  if (!staged) {  // uniform
+    tile_slots(E, rb, step, rb_size, rb_pos, r0, inj_idx, slotB);
+    __syncthreads();
+    gather_rows<lf*>(rb, slotB, O, A, sB, s2B, aB, rB, dB);
   }
   if (do_pi) {  // which = 0: target draw (role 0), 1: actor draw (role 5)
     const int NP = (A + 1) / 2;
@@ -1759,18 +1833,23 @@ __device__ __forceinline__ void phase_c_done(const AS_C EngineDev& E) {
 // WITH_B (role split only): blocks [0, nB) first run this step's phase B (critic
 // tiles, Polyak) and count themselves done per critic; each critic role waits
 // for its critic's count before streaming its weights.
+// After the role blocks: E.stage ? nrt stager blocks (next step's batch).
 template <typename T, bool ROLES, bool WITH_B>
-__global__ void __launch_bounds__(SAC_THREADS) sac_actor(const EngineDev* __restrict__ Ep) {
+__global__ void __launch_bounds__(SAC_THREADS) sac_actor(const EngineDev* __restrict__ Ep, sac_replay rb) {
   PREFETCH_ARG(Ep);
   const AS_C EngineDev& E = *(const AS_C EngineDev*)Ep;
+  extern __shared__ float lds_raw[];
+  const int bid = (int)blockIdx.x - (WITH_B ? E.nB : 0);
+  const int nrole = ROLES ? 3 * E.nrt : E.nrt * E.xs;
   if (WITH_B && (int)blockIdx.x < E.nB) {
-    extern __shared__ float lds_raw[];
     const AS_C TileDesc& td = *((const AS_C TileDesc*)E.tilesB + blockIdx.x);
     dw_adam_tile<T, SAC_THREADS, true>(E, E.tilesB + blockIdx.x, true, (int)(*GPC(uint64_t, E.rng_step) & 1),
                                        (lf*)lds_raw);
     count_done((uint32_t*)E.sync + SYNC_BDONE + 16 * (td.opt - 1));
+  } else if (bid >= nrole) {
+    stage_next_batch(E, rb, bid - nrole, (lf*)lds_raw);
   } else {
-    actor_body<T, ROLES, WITH_B>(Ep, (int)blockIdx.x - (WITH_B ? E.nB : 0));
+    actor_body<T, ROLES, WITH_B>(Ep, bid);
   }
   phase_c_done(E);
   END_STAMP(61);

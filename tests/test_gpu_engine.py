@@ -253,6 +253,44 @@ def test_large_batch_uses_fused_kernels_and_runs():
     assert all(np.isfinite(eng.losses()))
 
 
+@pytest.mark.parametrize("cfg,precision,fuse", [("c2", "bf16", "0"), ("c2", "fp32", "2"), ("c3", "bf16", "0")])
+def test_staged_batch_equals_in_step_gather(cfg, precision, fuse, monkeypatch):
+    """Phase C staging step t+1's batch (sampled and gathered one launch early)
+    gives the same bits as phase A gathering it, across graph replays, a replay
+    push between calls (the staged record goes stale and phase A gathers), and
+    injected indices.  The staged path must actually run."""
+    import ctypes
+
+    from sac import _engine as E
+
+    monkeypatch.setenv("SAC_FUSE", fuse)
+    out = {}
+    for stage in ("1", "0"):
+        monkeypatch.setenv("SAC_STAGE", stage)
+        eng, rb, c = _engine(cfg, precision, capacity=5000)
+        eng.train(rb, 3)
+        eng.train_graph(rb, 5, chunk=2)
+        if stage == "1":
+            lib = eng.lib
+            lib.sac_engine_debug_staged_step.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+            got = ctypes.c_uint64(0)
+            E.check(lib.sac_engine_debug_staged_step(eng.handle, ctypes.byref(got), eng._stream()))
+            assert got.value > 0, "phase A never used a staged batch"
+        g = np.random.default_rng(5)
+        n = 7
+        rb.push_batch(g.standard_normal((n, c["obs"]), dtype=np.float32), g.uniform(-1, 1, (n, c["act"])),
+                      g.standard_normal(n), g.standard_normal((n, c["obs"]), dtype=np.float32), g.random(n) < 0.1)
+        eng.train(rb, 2)
+        idx = torch.from_numpy(g.choice(len(rb), size=(2, c["batch"]), replace=True).astype(np.int32))
+        eng.train(rb, 2, indices=idx)
+        eng.train(rb, 2)
+        eng.check()
+        out[stage] = {k: v.clone() for k, v in eng.state_tensors().items()}
+        out[stage]["stats"] = eng.stats.clone()
+    for k in out["1"]:
+        assert torch.equal(out["1"][k], out["0"][k]), k
+
+
 @pytest.mark.parametrize("precision,layout", [("fp32", "1"), ("bf16", "1"), ("fp32", "2"), ("bf16", "2")])
 def test_fused_launches_equal_four_launches(precision, layout, monkeypatch):
     """Two launches per step (phase D inside the next phase A launch, phase B

@@ -44,6 +44,13 @@ __global__ void __launch_bounds__(512) k(const bf16* W, long long* out, float* s
         a[u] = f0[(u + it) & 7];
       }
     }
+    if (VAR & 32) {  // B streamed from global (L2-warm): loads issued before the A reads
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        f0[u] = *(const AS_G bf16x8*)(GPC(bf16, W) + ((size_t)(wave * 8 + u) * 64 + lane) * 8);
+        f1[u] = *(const AS_G bf16x8*)(GPC(bf16, W) + ((size_t)((wave + 8) * 8 + u) * 64 + lane) * 8);
+      }
+    }
     if (VAR & 2) {
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
@@ -104,6 +111,8 @@ int main() {
   CHK(hipMalloc(&sink, 256 * 16 * 4));
   CHK(hipMalloc(&out, 256 * 8 * 8));
   run<1 | 2 | 4 | 8>("full: fp32 LDS A + MFMA + epilogue + barrier", W, out, sink);
+  run<32 | 1 | 2 | 4 | 8>("full, B streamed (L2-warm)", W, out, sink);
+  run<32 | 16 | 2 | 4 | 8>("full, B streamed, bf16 LDS A image", W, out, sink);
   run<16 | 2 | 4 | 8>("full, bf16 LDS A image", W, out, sink);
   run<2 | 4 | 8>("no A reads (register A)", W, out, sink);
   run<1 | 4 | 8>("no MFMA", W, out, sink);
