@@ -51,6 +51,13 @@ def _make_logger(cfg, env_name, agent_name):
     return ExperimentLogger(cfg, env_name=env_name, agent_name=agent_name)
 
 
+def due_updates(old_steps: int, new_steps: int, update_frequency: int, gradient_steps: int) -> int:
+    """Gradient steps the reference loop runs while its env-step counter goes
+    from old_steps to new_steps: ``gradient_steps`` at every step t with
+    t % update_frequency == 0 (agent.py:361-364)."""
+    return (new_steps // update_frequency - old_steps // update_frequency) * gradient_steps
+
+
 class SAC:
     def __init__(self, env, config: dict):
         self.env = env
@@ -173,6 +180,43 @@ class SAC:
             act = eng.policy_act(obs, eps)
         return act.cpu().numpy()[0]
 
+    def select_actions(self, states: Any, deterministic: bool = False) -> np.ndarray:
+        """Policy actions for N observations [N, obs]: one H2D copy, ONE policy
+        kernel, one D2H copy (the batched form of ``select_action``; row i draws
+        its noise from the same torch generator stream as N single calls would
+        for N = 1)."""
+        eng = self._engine()
+        host = np.ascontiguousarray(np.asarray(states, dtype=np.float32).reshape(-1, self.obs_size))
+        obs = torch.from_numpy(host)
+        if self.device.type == "cuda":
+            obs = obs.pin_memory().to(self.device, non_blocking=True)
+        if deterministic:
+            act = eng.policy_act(obs)
+        else:
+            eps = torch.distributions.utils._standard_normal((host.shape[0], self.action_size), torch.float32,
+                                                             self.device)
+            act = eng.policy_act(obs, eps)
+        return act.cpu().numpy()
+
+    def store_transitions(self, states: Any, actions: Any, rewards: Any, next_states: Any, dones: Any) -> None:
+        """N transitions in env order: one pinned H2D copy + one push kernel."""
+        self.replay_buffer.push_batch(states, actions, rewards, next_states, dones)
+
+    def _run_updates(self, n: int) -> None:
+        """n consecutive gradient steps (agent.py:361-364): one engine call, no
+        host sync (device RNG); per-step calls in reference-RNG mode."""
+        if n <= 0:
+            return
+        if self.rng_mode == "reference":
+            for _ in range(n):
+                self.training_step()
+            return
+        self.replay_buffer._check(self.config["train"]["batch_size"])
+        if n >= self.graph_chunk:
+            self._engine().train_graph(self.replay_buffer, n, self.graph_chunk)
+        else:
+            self._engine().train(self.replay_buffer, n)
+
     def can_update(self) -> bool:
         if self.config["train"]["warming_steps"] > self.config["buffer"]["capacity"]:
             print("Warning: warming_steps is greater than replay buffer capacity.")
@@ -265,8 +309,7 @@ class SAC:
                 episode_steps += 1
                 total_steps += 1
                 if self.can_update() and total_steps % update_every == 0:
-                    for _ in range(n_grad):
-                        self.training_step()
+                    self._run_updates(n_grad)
                 if active_logger is not None and self.config["logger"]["log_q_values"]:
                     self._log_q_values(
                         states=torch.FloatTensor(np.asarray(state)).unsqueeze(0).to(self.device),
@@ -298,6 +341,74 @@ class SAC:
 
             save_rewards(active_logger.run_dir, active_logger.episode_rewards)
             save_lengths(active_logger.run_dir, active_logger.episode_lengths)
+        return metrics
+
+    def run_vectorized_training_loop(self, total_env_steps: int, vec_env: Any = None, logger=None,
+                                     tqdm_disable: bool = True, print_rewards: bool = False,
+                                     seed: Optional[int] = None) -> Dict[str, float]:
+        """Batched form of ``run_training_loop`` (agent.py:329-418) over a
+        ``SyncVectorEnv`` of N envs.
+
+        Per vector step: ONE policy kernel for the N actions, the N env steps on
+        the host, ONE push of the N transitions, then every gradient step that
+        fell due in those N env steps (``update_frequency`` /
+        ``gradient_steps_per_update``, counted per env step exactly as the
+        reference counts them) as ONE engine call: K steps per launch sequence,
+        hipGraph replay when K >= graph_chunk, no host synchronisation.  With
+        N = 1 it performs the reference loop's exact sequence of pushes,
+        updates and RNG draws (tests/test_gpu_rollout.py).
+
+        ``vec_env`` defaults to ``self.env`` (pass a ``SyncVectorEnv`` as the
+        agent's env so ``_set_seed`` seeds env i with seed + i).  Stops after the
+        first vector step that reaches ``total_env_steps``."""
+        env = vec_env if vec_env is not None else self.env
+        if not hasattr(env, "num_envs"):
+            raise TypeError("run_vectorized_training_loop needs a vectorised env (sac.vector_env.SyncVectorEnv)")
+        active_logger = logger or self.logger
+        tr = self.config["train"]
+        update_every = tr.get("update_frequency", 1)
+        n_grad = tr.get("gradient_steps_per_update", 1)
+        N = env.num_envs
+        obs, _ = env.reset(seed=seed)
+        ep_ret = np.zeros(N, np.float64)
+        ep_len = np.zeros(N, np.int64)
+        returns_window = deque(maxlen=100)
+        best_avg_return = -float("inf")
+        avg_return = float("nan")
+        total_steps = total_episodes = grad_steps = 0
+        log_episodes = active_logger is not None and self.config["logger"]["log_episode_stats"]
+        pbar = _tqdm(range((int(total_env_steps) + N - 1) // N), disable=tqdm_disable)
+        for _ in pbar:
+            actions = self.select_actions(obs)
+            next_obs, rewards, terminated, truncated, info = env.step(actions)
+            dones = np.logical_or(terminated, truncated)
+            self.store_transitions(obs, actions, rewards, info["final_obs"], dones)
+            old = total_steps
+            total_steps += N
+            due = due_updates(old, total_steps, update_every, n_grad)
+            if due and self.can_update():
+                self._run_updates(due)
+                grad_steps += due
+            ep_ret += rewards
+            ep_len += 1
+            for i in np.nonzero(dones)[0]:
+                returns_window.append(float(ep_ret[i]))
+                avg_return = float(np.mean(returns_window))
+                best_avg_return = max(best_avg_return, avg_return)
+                if log_episodes:
+                    active_logger.log_episode_metrics(episode_idx=total_episodes, reward=float(ep_ret[i]),
+                                                      length=int(ep_len[i]))
+                if print_rewards:
+                    print(f"Episode {total_episodes}, Return: {ep_ret[i]:.2f}, "
+                          f"Average Return(last 100 episodes): {avg_return:.2f}")
+                total_episodes += 1
+                ep_ret[i] = 0.0
+                ep_len[i] = 0
+            obs = next_obs
+        metrics = {"total_episodes": total_episodes, "best_avg_return": best_avg_return,
+                   "final_avg_return": avg_return, "total_env_steps": total_steps, "gradient_steps": grad_steps}
+        if active_logger is not None:
+            active_logger.log_hparams(self.config, metrics)
         return metrics
 
     def eval_agent(self, num_episodes: int, render_mode: Optional[str] = None, tqdm_disable: bool = False,

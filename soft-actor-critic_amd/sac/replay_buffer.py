@@ -97,7 +97,30 @@ class ReplayBuffer:
             self.flush()
 
     def push_batch(self, states, actions, rewards, next_states, dones) -> None:
-        """Append n transitions at once (device or host arrays; rows in order)."""
+        """Append n transitions at once (device or host arrays; rows in order).
+
+        Host inputs are packed into ONE pinned [n][2O+A+2] buffer: one H2D copy
+        and one push kernel per batch (the vectorised rollout's per-step cost)."""
+        if not any(isinstance(x, torch.Tensor) and x.is_cuda for x in (states, actions, rewards, next_states, dones)):
+            st = np.asarray(states, np.float32)
+            n = st.shape[0]
+            if n == 0:
+                return
+            st = st.reshape(n, -1)
+            ac = np.asarray(actions, np.float32).reshape(n, -1)
+            if not self._alloc_done:
+                self._alloc(st.shape[1], ac.shape[1])
+            self.flush()
+            O, A = self.obs_dim, self.act_dim
+            host = torch.empty(n, self.row_width, dtype=torch.float32, pin_memory=torch.cuda.is_available())
+            h = host.numpy()
+            h[:, :O] = st
+            h[:, O:O + A] = ac
+            h[:, O + A] = np.asarray(rewards, np.float32).reshape(n)
+            h[:, O + A + 1:2 * O + A + 1] = np.asarray(next_states, np.float32).reshape(n, -1)
+            h[:, -1] = np.asarray(dones).reshape(n).astype(bool)
+            self._push_device_rows(host.to(self.device, non_blocking=True))
+            return
         st = torch.as_tensor(states, dtype=torch.float32)
         n = st.shape[0]
         if n == 0:

@@ -1,0 +1,124 @@
+"""Vectorised rollout + batched training-loop driver on the MI355X (SURVEY §8
+f1/f2).  The parity anchor is the reference loop itself (agent.py:329-418, as
+mirrored by SAC.run_training_loop): with one env the batched driver must
+produce the same replay rows and the same engine state bit for bit; with N envs
+the batched action kernel and the single-copy push must equal their per-row
+forms."""
+import copy
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _cfg(batch=16, warming=24, update_frequency=1, grad_steps=1, precision="fp32", capacity=4096):
+    return {
+        "sac": {"gamma": 0.99, "tau": 0.005, "alpha": 0.2, "auto_entropy_tuning": True, "actor_lr": 3e-4,
+                "critic_lr": 3e-4, "alpha_lr": 3e-4},
+        "q_net": {"hidden_sizes": [32, 32], "hidden_layers_act": "relu", "output_activation": "identity"},
+        "policy_net": {"hidden_sizes": [32, 32], "hidden_layers_act": "relu", "output_activation": "identity",
+                       "log_std_min": -20, "log_std_max": 2, "action_scale": 1.0},
+        "buffer": {"capacity": capacity},
+        "train": {"gradient_steps_per_update": grad_steps, "update_frequency": update_frequency, "seed": 3,
+                  "batch_size": batch, "warming_steps": warming, "device": "cuda", "precision": precision,
+                  "graph_chunk": 4},
+        "logger": {"enabled": False, "env_name": "probe", "agent_name": "SAC", "log_episode_stats": False,
+                   "log_q_values": False, "save_model": {"enabled": False, "path": None}},
+    }
+
+
+def _env():
+    from sac.envs import OneDPointMassReachEnv
+
+    return OneDPointMassReachEnv(max_steps=9, action_low=-0.5, action_high=0.5, goal_tolerance=0.1)
+
+
+def _replay_rows(agent):
+    rb = agent.replay_buffer
+    rb.flush()
+    n = len(rb)
+    torch.cuda.synchronize()
+    return {k: getattr(rb, k)[:n].cpu().clone() for k in ("obs", "act", "rew", "next_obs", "done")}
+
+
+@pytest.mark.parametrize("update_frequency,grad_steps", [(1, 1), (3, 5)])
+def test_vectorized_loop_one_env_equals_reference_loop(update_frequency, grad_steps):
+    from sac.agent import SAC
+    from sac.vector_env import SyncVectorEnv
+
+    cfg = _cfg(update_frequency=update_frequency, grad_steps=grad_steps)
+    ref = SAC(_env(), copy.deepcopy(cfg))
+    m_ref = ref.run_training_loop(num_episodes=12, tqdm_disable=True)
+    T = len(ref.replay_buffer)
+    assert ref.engine.steps_done > 0
+    vec = SAC(SyncVectorEnv([_env]), copy.deepcopy(cfg))
+    m_vec = vec.run_vectorized_training_loop(T)
+    torch.cuda.synchronize()
+    assert m_vec["total_env_steps"] == T and m_vec["total_episodes"] == m_ref["total_episodes"]
+    assert m_vec["gradient_steps"] == ref.engine.steps_done == vec.engine.steps_done
+    assert m_vec["final_avg_return"] == pytest.approx(m_ref["final_avg_return"], rel=0, abs=1e-9)
+    ra, rb = _replay_rows(ref), _replay_rows(vec)
+    for k in ra:
+        assert torch.equal(ra[k], rb[k]), k
+    sa, sb = ref.engine.state_tensors(), vec.engine.state_tensors()
+    for k in sa:
+        assert torch.equal(sa[k], sb[k]), k
+
+
+def test_batched_actions_equal_per_row_actions():
+    from sac.agent import SAC
+    from sac.vector_env import SyncVectorEnv
+
+    cfg = _cfg()
+    agent = SAC(SyncVectorEnv([_env] * 37), cfg)
+    obs = np.random.default_rng(0).standard_normal((37, 1)).astype(np.float32)
+    batched = agent.select_actions(obs, deterministic=True)
+    rows = np.stack([agent.select_action(obs[i], deterministic=True) for i in range(37)])
+    assert batched.shape == (37, 1) and np.array_equal(batched, rows)
+    # stochastic: N draws of one (N, A) noise block == the kernel on the same eps
+    torch.manual_seed(9)
+    a1 = agent.select_actions(obs)
+    torch.manual_seed(9)
+    eps = torch.distributions.utils._standard_normal((37, 1), torch.float32, agent.device)
+    a2 = agent.engine.policy_act(torch.from_numpy(obs).cuda(), eps).cpu().numpy()
+    assert np.array_equal(a1, a2)
+
+
+@pytest.mark.parametrize("n", [1, 5, 300])
+def test_batched_push_equals_per_row_push(n):
+    from sac.replay_buffer import ReplayBuffer
+
+    g = np.random.default_rng(n)
+    s, s2 = g.standard_normal((n, 24)).astype(np.float32), g.standard_normal((n, 24)).astype(np.float32)
+    a = g.uniform(-1, 1, (n, 4)).astype(np.float32)
+    r = g.standard_normal(n)  # float64 rewards, as gym returns them
+    d = g.random(n) < 0.3
+    cap = 257  # wraps for n = 300
+    rb1 = ReplayBuffer(cap, device="cuda", obs_dim=24, act_dim=4)
+    rb2 = ReplayBuffer(cap, device="cuda", obs_dim=24, act_dim=4)
+    rb1.push_batch(s, a, r, s2, d)
+    for i in range(n):
+        rb2.push(s[i], a[i], float(r[i]), s2[i], bool(d[i]))
+    rb2.flush()
+    torch.cuda.synchronize()
+    assert len(rb1) == len(rb2) == min(n, cap)
+    for k in ("obs", "act", "rew", "next_obs", "done", "state"):
+        assert torch.equal(getattr(rb1, k), getattr(rb2, k)), k
+
+
+def test_vectorized_loop_many_envs_runs_and_counts():
+    from sac.agent import SAC
+    from sac.vector_env import SyncVectorEnv
+
+    cfg = _cfg(batch=32, warming=64, update_frequency=2, grad_steps=3, precision="bf16")
+    agent = SAC(SyncVectorEnv([_env] * 16), cfg)
+    m = agent.run_vectorized_training_loop(16 * 20)
+    torch.cuda.synchronize()
+    assert m["total_env_steps"] == 320 and len(agent.replay_buffer) == 320
+    # updates only once the buffer holds warming_steps rows: from vector step 4 on (64 rows)
+    assert m["gradient_steps"] == sum(3 * 8 for _ in range(4, 21))
+    assert agent.engine.steps_done == m["gradient_steps"]
+    agent.engine.check()
+    assert all(np.isfinite(agent.engine.losses()[:3]))
