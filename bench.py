@@ -228,7 +228,17 @@ def main():
         raise SystemExit(f"non-finite losses after benchmark: {losses}")
 
     # per-phase device time (hipEvents on the launch stream), then roofline of the dominant kernel
-    phase_ms = eng.time_phases(rb, 100)
+    # Each interval also holds the cost of the event after it; the timed region
+    # above ran the same launches from hipGraphs with no events.  The per-launch
+    # event cost = (sum of the intervals of one step - the event-free step time)
+    # / launches per step; interval - that cost = the kernel's own duration (the
+    # figure rocprofv3 --kernel-trace reports: profiles/<round>_kernel_stats.csv).
+    tp = eng.time_phases(rb, 100)
+    phase_ms, empty_ms = tp[:4], tp[4]
+    step_ms = elapsed / args.steps * 1e3
+    n_launch = sum(1 for x in phase_ms if x > 0)
+    ev_cost = max((sum(phase_ms) - step_ms) / n_launch, 0.0)
+    kern_ms = [x - ev_cost if x > 0 else 0.0 for x in phase_ms]
     flops, f_total, _, _ = gemm_flops(c["obs"], c["act"], c["hidden"], c["batch"])
     if eng.fused:  # D inside the next A launch (and with layout 2, B inside the C launch)
         flops = [flops[0] + flops[3], flops[1], flops[2], 0]
@@ -239,7 +249,7 @@ def main():
 
     kname = E.load_library().sac_phase_kernel_name(dom).decode()
     traffic, traffic_src = pmc_traffic(kname) if args.config == "c2" and args.precision == "bf16" else (None, None)
-    achieved = flops[dom] / (phase_ms[dom] * 1e-3) / 1e12
+    achieved = flops[dom] / (kern_ms[dom] * 1e-3) / 1e12
     peak = PEAK_TFLOPS[args.precision]
 
     if rank == 0:
@@ -265,13 +275,18 @@ def main():
                        "global_batch": c["batch"] * world, "parallelism": f"replicas{world}"},
             "replay_sample_GBps_in_step": round(sps / world * c["batch"] * W * 4 / 1e9, 4),
             "replay_sample_GBps_sweep": sweep,
-            "phase_ms": [round(x, 5) for x in phase_ms],
+            "phase_ms": [round(x, 5) for x in kern_ms],
+            "phase_event_interval_ms": [round(x, 5) for x in phase_ms],
+            "event_cost_ms": round(ev_cost, 5),
+            "empty_kernel_event_interval_ms": round(empty_ms, 5),
             "step_gemm_flops_survey": f_total,
             "roofline": {"bound": "mfma", "kernel": kname, "achieved": round(achieved, 3), "peak": peak,
                          "unit": "TFLOP/s", "frac": round(achieved / peak, 5), "traffic": traffic,
                          "traffic_source": traffic_src, "flops_per_launch": flops[dom],
-                         "avg_launch_ms": round(phase_ms[dom], 5),
-                         "timing": "hipEvents around the kernel on its launch stream, 100 steps"},
+                         "avg_launch_ms": round(kern_ms[dom], 5),
+                         "timing": "hipEvents after every launch on the launch stream over 100 steps; "
+                                   "avg_launch_ms = mean interval of this kernel's launches minus the per-launch "
+                                   "event cost (event intervals of a step - event-free graph step time, per launch)"},
             "losses_last": [round(x, 6) for x in losses],
         }
         if world == 1 and not args.no_cpu_baseline:

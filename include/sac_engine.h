@@ -164,10 +164,15 @@ int sac_replay_sample_indices(const sac_replay *rb, int32_t batch, uint64_t seed
                               uint64_t step, int32_t *out, void *stream);
 
 /* Profiling: runs n_steps with hipEvents after each launch and returns the
- * mean device time per phase launch in ms: [0]=A target+critic-backward,
- * [1]=B critic dW+Adam+Polyak, [2]=C actor, [3]=D actor dW+Adam+alpha.  Fused
- * layouts (sac_engine_phase_layout()): 1 = D shares the next step's A launch
- * ([0] is that launch, [3] = 0); 2 = also B shares C's launch ([1] = 0).
+ * mean event interval per phase launch in ms (ms_host holds 5 floats):
+ * [0]=A target+critic-backward, [1]=B critic dW+Adam+Polyak, [2]=C actor,
+ * [3]=D actor dW+Adam+alpha, [4]=the same interval for an empty kernel launched
+ * the same way (diagnostic: an event + dispatch pair alone).  Each interval
+ * includes its event's cost; bench.py removes it using the event-free graph
+ * step time.  The sequence is queued behind a spin kernel, so the intervals are
+ * device time, not host-submission time.
+ * Fused layouts (sac_engine_phase_layout()): 1 = D shares the next step's A
+ * launch ([0] is that launch, [3] = 0); 2 = also B shares C's launch ([1] = 0).
  * Synchronises the stream. */
 int sac_engine_time_phases(sac_engine *e, const sac_replay *rb, int32_t n_steps,
                            float *ms_host, void *stream);

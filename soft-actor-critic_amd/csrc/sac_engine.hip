@@ -141,6 +141,7 @@ struct sac_engine {
   std::vector<TileDesc> hostB, hostD;
   int nB = 0, nD = 0;
   size_t lds_bytes = 0;
+  size_t upd_lds = 0;  // dynamic LDS of an update tile (SAC_UPD_LDS_FOR(upd_slots))
   int nrt = 0;
   int fused = 0;  // 0: A B C D per step; 1: D inside the next A's launch; 2: also B inside C's
   // graph cache
@@ -362,6 +363,11 @@ static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
     e->h.nB = nB;
     e->h.nD = nD;
     e->lds_bytes = (size_t)lo * 4;
+    {  // update tiles stage up to 4 batch chunks of 512 B per operand row per round
+      const int bch = 512 / esz;
+      e->h.upd_slots = std::min(4, (Bp + bch - 1) / bch);
+      e->upd_lds = SAC_UPD_LDS_FOR(e->h.upd_slots);
+    }
     e->nrt = nrt;
     // self-contained update tiles (phase B: critics + Polyak, phase D: policy)
     const int esz2 = esz;
@@ -422,7 +428,8 @@ static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
 
 template <typename T>
 static void set_lds_attrs(size_t bytes) {
-  const int b = (int)std::max(bytes, (size_t)SAC_UPD_LDS);
+  (void)bytes;
+  const int b = 160 * 1024;  // the launch passes what it needs; the attribute is the cap
   (void)hipFuncSetAttribute((const void*)sac_target_critic<T, false, false>, hipFuncAttributeMaxDynamicSharedMemorySize, b);
   (void)hipFuncSetAttribute((const void*)sac_target_critic<T, true, false>, hipFuncAttributeMaxDynamicSharedMemorySize, b);
   (void)hipFuncSetAttribute((const void*)sac_target_critic<T, true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, b);
@@ -430,6 +437,18 @@ static void set_lds_attrs(size_t bytes) {
   (void)hipFuncSetAttribute((const void*)sac_actor<T, true, false>, hipFuncAttributeMaxDynamicSharedMemorySize, b);
   (void)hipFuncSetAttribute((const void*)sac_actor<T, true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, b);
   (void)hipFuncSetAttribute((const void*)sac_policy_act_kernel<T>, hipFuncAttributeMaxDynamicSharedMemorySize, b);
+  (void)hipFuncSetAttribute((const void*)sac_critic_update<T>, hipFuncAttributeMaxDynamicSharedMemorySize, b);
+  (void)hipFuncSetAttribute((const void*)sac_actor_update<T>, hipFuncAttributeMaxDynamicSharedMemorySize, b);
+}
+
+// empty kernel: the dispatch + event gap of sac_engine_time_phases
+__global__ void sac_noop_kernel() {}
+// one wave spinning `ticks` of the 100 MHz realtime clock: holds the stream
+// while the host enqueues a timed sequence, so its launches run back to back
+// at device speed instead of host-submission speed
+__global__ void sac_spin_kernel(long long ticks) {
+  const long long t0 = __builtin_amdgcn_s_memrealtime();
+  while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(8);
 }
 
 // Launch kinds of a step sequence.  Unfused: A B C D per step.  Fused (role
@@ -440,7 +459,7 @@ enum LaunchKind { L_A = 0, L_B = 1, L_C = 2, L_D = 3, L_DA = 4, L_BC = 5 };
 template <typename T>
 static void launch_kind(sac_engine* e, int kind, const sac_replay* rb, const int32_t* idx, const float* eps,
                         hipStream_t s) {
-  const size_t lf = std::max(e->lds_bytes, (size_t)SAC_UPD_LDS);
+  const size_t lf = std::max(e->lds_bytes, e->upd_lds);
   const int stg = e->h.stage ? e->nrt : 0;  // stager blocks of phase C
   switch (kind) {
     case L_A:
@@ -450,7 +469,7 @@ static void launch_kind(sac_engine* e, int kind, const sac_replay* rb, const int
         sac_target_critic<T, false, false><<<e->nrt * e->h.xs, SAC_THREADS, lf, s>>>(e->d, *rb, idx, eps);
       break;
     case L_B:
-      sac_critic_update<T><<<e->nB, SAC_UPD_THREADS, SAC_UPD_LDS, s>>>(e->d, e->tilesB);
+      sac_critic_update<T><<<e->nB, SAC_UPD_THREADS, e->upd_lds, s>>>(e->d, e->tilesB);
       break;
     case L_C:
       if (e->h.roles)
@@ -459,7 +478,7 @@ static void launch_kind(sac_engine* e, int kind, const sac_replay* rb, const int
         sac_actor<T, false, false><<<e->nrt * e->h.xs + stg, SAC_THREADS, lf, s>>>(e->d, *rb);
       break;
     case L_D:
-      sac_actor_update<T><<<e->nD + 1, SAC_UPD_THREADS, SAC_UPD_LDS, s>>>(e->d, e->tilesD, e->nD);
+      sac_actor_update<T><<<e->nD + 1, SAC_UPD_THREADS, e->upd_lds, s>>>(e->d, e->tilesD, e->nD);
       break;
     case L_DA:
       sac_target_critic<T, true, true><<<e->nD + 1 + e->nrt * 6, SAC_THREADS, lf, s>>>(e->d, *rb, idx, eps);
@@ -573,7 +592,7 @@ int sac_engine_create(const sac_engine_config* cfg, const sac_engine_buffers* bu
   e->cfg = *cfg;
   e->buf = *buf;
   plan(cfg, e, (char*)buf->workspace);
-  if (e->lds_bytes > 160 * 1024) {
+  if (std::max(e->lds_bytes, e->upd_lds) > 160 * 1024) {
     const size_t lb = e->lds_bytes;
     delete e;
     return fail(SAC_E_INVALID, "layer widths need " + std::to_string(lb) + " B of LDS per workgroup (max 163840)");
@@ -769,6 +788,10 @@ int sac_engine_time_phases(sac_engine* e, const sac_replay* rb, int32_t n_steps,
   std::vector<hipEvent_t> ev;
   hipEvent_t start;
   HIPCHK(hipEventCreate(&start));
+  // hold the stream while the whole sequence is enqueued (~0.2 ms of host time
+  // per step), so the intervals are device time, not host-submission time
+  const long long hold = std::min(20000000LL, 20000LL * n_steps + 200000LL);
+  sac_spin_kernel<<<1, 64, 0, s>>>(hold);
   HIPCHK(hipEventRecord(start, s));
   launch_steps(e, rb, n_steps, nullptr, nullptr, s, &kinds, &ev);
   HIPCHK(hipStreamSynchronize(s));
@@ -788,6 +811,27 @@ int sac_engine_time_phases(sac_engine* e, const sac_replay* rb, int32_t n_steps,
     ms_host[3] = 0.f;
   } else {
     for (int p = 0; p < 4; ++p) ms_host[p] = avg(p);
+  }
+  // the same event pattern around empty launches: the per-launch gap
+  {
+    const int n = 64;
+    std::vector<hipEvent_t> ez(n + 1);
+    for (auto& x : ez) HIPCHK(hipEventCreate(&x));
+    sac_spin_kernel<<<1, 64, 0, s>>>(200000LL);  // 2 ms: every empty launch queued behind it
+    HIPCHK(hipEventRecord(ez[0], s));
+    for (int i = 1; i <= n; ++i) {
+      sac_noop_kernel<<<1, 64, 0, s>>>();
+      HIPCHK(hipEventRecord(ez[i], s));
+    }
+    HIPCHK(hipStreamSynchronize(s));
+    double tot = 0.0;
+    for (int i = 1; i <= n; ++i) {
+      float ms = 0.f;
+      HIPCHK(hipEventElapsedTime(&ms, ez[i - 1], ez[i]));
+      tot += ms;
+    }
+    ms_host[4] = (float)(tot / n);
+    for (auto& x : ez) (void)hipEventDestroy(x);
   }
   (void)hipEventDestroy(start);
   for (auto& x : ev) (void)hipEventDestroy(x);

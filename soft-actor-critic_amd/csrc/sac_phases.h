@@ -72,6 +72,7 @@ struct EngineDev {
   // tiles onto 8/xs XCDs whose L2s then share one weight stream (speed only).
   int xs;
   int roles;  // phases A / C split into per-network workgroups (see "role hand-offs")
+  int upd_slots;  // update tiles: batch chunks staged per round (LDS slots, 1..4)
   // update tiles, read by the fused launches (phase D inside phase A's launch,
   // phase B inside phase C's launch)
   const TileDesc* tilesB;
@@ -797,9 +798,10 @@ __device__ __forceinline__ void count_done(uint32_t* counter) {
 //      shares the launch can read them after the completion counter.
 #define SAC_UPD_THREADS 1024
 #define SAC_UPD_BCH (512 / (int)sizeof(T))  // batch columns staged per chunk (512 B per row)
-// dynamic LDS of an update tile: stage 64 x 528 B | 2 x [32][33] f32 | [32][9] f32
+// dynamic LDS of an update tile: upd_slots x stage 64 x 528 B | 2 x [32][33] f32 | [32][17] f32
 // (>= the alpha block's 5 x 1024 floats)
-#define SAC_UPD_LDS (64 * 528 + 2 * 32 * 33 * 4 + 32 * 9 * 4)
+#define SAC_UPD_SLOT_BYTES (64 * 528)
+#define SAC_UPD_LDS_FOR(slots) ((slots) * SAC_UPD_SLOT_BYTES + 2 * 32 * 33 * 4 + 32 * 17 * 4)
 template <typename T, int UT, bool COH>
 __device__ __forceinline__ void dw_adam_tile(const AS_C EngineDev& E, const TileDesc* tdp_, bool polyak, int par,
                                              lf* lds) {
@@ -811,10 +813,12 @@ __device__ __forceinline__ void dw_adam_tile(const AS_C EngineDev& E, const Tile
   STAMP(polyak ? 48 : 52);
   const int tid = threadIdx.x;
   const int Bp = E.Bp;
-  // LDS: stage [64][SAC_UPD_BCH + pad] of T | acc / new params [32][33] f32 | targets [32][33] | bias reduce [32][9]
+  // LDS: stage [64][SAC_UPD_BCH + pad] of T | acc / new params [32][33] f32 | targets [32][33] | bias reduce [32][17]
   const int lds_row = SAC_UPD_BCH + 16 / (int)sizeof(T);  // +16 B per row: rows start on different banks
   AS_L T* stage = (AS_L T*)lds;
-  lf* accs = lds + (64 * lds_row * (int)sizeof(T) + 15) / 16 * 4;
+  const int nslot = E.upd_slots;
+  const int slot_el = 64 * lds_row;  // T elements per stage slot
+  lf* accs = lds + (nslot * slot_el * (int)sizeof(T) + 15) / 16 * 4;
   lf* tgts = accs + 32 * 33;
   lf* red = tgts + 32 * 33;
   // this step's Adam scalars (written by phase A)
@@ -847,49 +851,96 @@ __device__ __forceinline__ void dw_adam_tile(const AS_C EngineDev& E, const Tile
     vb = GPC(float, td.bv)[td.n0 + tid];
     if (polyak) tbv = GPC(float, td.tb)[td.n0 + tid];
   }
+  // bias gradient: the row tiles' partial sums, 16 lanes per column (512
+  // threads for 8- and 16-wave blocks alike); each lane's loads are issued 8 at
+  // a time (one round trip per 8 row tiles, not one per row tile: 256 row tiles
+  // at B = 4096) and added in row-tile order
   float bsum = 0.f;
-  const int bn = tid >> 3, bs = tid & 7;
-  if (do_bias && tid < 256 && td.n0 + bn < td.N)
-    for (int rt = bs; rt < td.nrt; rt += 8) bsum += GPC(float, td.dbp)[(size_t)rt * td.N + td.n0 + bn];
-  // ---- 2. dW = dY^T X over the batch, staged through LDS in 512-B row chunks;
-  // waves 0-3 run one 16x16 sub-tile each, chunks in batch order
+  const int bn = tid >> 4, bs = tid & 15;
+  if (do_bias && tid < 512 && td.n0 + bn < td.N) {
+    const AS_G float* dbp = GPC(float, td.dbp) + td.n0 + bn;
+    for (int rt0 = bs; rt0 < td.nrt; rt0 += 16 * 8) {
+      float pv[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int rt = rt0 + 16 * u;
+        pv[u] = rt < td.nrt ? dbp[(size_t)rt * td.N] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (rt0 + 16 * u < td.nrt) bsum += pv[u];
+    }
+  }
+  // ---- 2. dW = dY^T X over the batch, staged through LDS in 512-B row chunks,
+  // nslot chunks per round (every load of a round in flight before its first
+  // LDS store: one round trip per nslot chunks); waves 0-3 run one 16x16
+  // sub-tile each, chunks in batch order
   const int lane = tid & 63, wave = wave_id();
   const int c = lane & 15, g = lane >> 4;
   const int ns = (wave >> 1) * 16, ks = (wave & 1) * 16;
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-  for (int b0 = 0; b0 < Bp; b0 += SAC_UPD_BCH) {
-    const int bch = Bp - b0 < SAC_UPD_BCH ? Bp - b0 : SAC_UPD_BCH;
-    const int per_row = bch / EPR;  // 16-B pieces per operand row of this chunk
-    for (int i = tid; i < 64 * per_row; i += UT) {
-      const int row = i / per_row, pc = i % per_row;
-      const AS_G T* src = row < 32 ? GPC(T, td.GT) + (size_t)row * Bp
-                                   : GPC(T, td.XT) + par * td.xt_par + (size_t)(row - 32) * Bp;
-      *(AS_L u32x4*)(stage + row * lds_row + pc * EPR) = *(const AS_G u32x4*)(src + b0 + pc * EPR);
+  constexpr int MAXS = 4, PPT = 64 * (SAC_UPD_BCH / EPR) / UT;  // slots, pieces per thread per full chunk
+  for (int r0 = 0; r0 < Bp; r0 += nslot * SAC_UPD_BCH) {
+    u32x4 rg[MAXS][PPT];
+#pragma unroll
+    for (int sl = 0; sl < MAXS; ++sl) {
+      const int b0 = r0 + sl * SAC_UPD_BCH;
+      if (sl < nslot && b0 < Bp) {  // uniform
+        const int bch = Bp - b0 < SAC_UPD_BCH ? Bp - b0 : SAC_UPD_BCH;
+        const int per_row = bch / EPR;  // 16-B pieces per operand row of this chunk
+#pragma unroll
+        for (int pi = 0; pi < PPT; ++pi) {
+          const int i = tid + pi * UT;
+          const int row = i / per_row, pc = i % per_row;
+          const AS_G T* src = row < 32 ? GPC(T, td.GT) + (size_t)row * Bp
+                                       : GPC(T, td.XT) + par * td.xt_par + (size_t)(row - 32) * Bp;
+          if (i < 64 * per_row) rg[sl][pi] = *(const AS_G u32x4*)(src + b0 + pc * EPR);
+        }
+      }
+    }
+#pragma unroll
+    for (int sl = 0; sl < MAXS; ++sl) {
+      const int b0 = r0 + sl * SAC_UPD_BCH;
+      if (sl < nslot && b0 < Bp) {
+        const int bch = Bp - b0 < SAC_UPD_BCH ? Bp - b0 : SAC_UPD_BCH;
+        const int per_row = bch / EPR;
+#pragma unroll
+        for (int pi = 0; pi < PPT; ++pi) {
+          const int i = tid + pi * UT;
+          const int row = i / per_row, pc = i % per_row;
+          if (i < 64 * per_row) *(AS_L u32x4*)(stage + sl * slot_el + row * lds_row + pc * EPR) = rg[sl][pi];
+        }
+      }
     }
     __syncthreads();
     if (wave < 4) {
-      const AS_L T* arow = stage + (ns + c) * lds_row + g * KL;
-      const AS_L T* brow = stage + (32 + ks + c) * lds_row + g * KL;
-      for (int ch = 0; ch < bch / KC; ++ch) {
-        typename MM<T>::Frag a, b;
-        if constexpr (sizeof(T) == 2) {
-          a = *(const AS_L bf16x8*)(arow + ch * KC);
-          b = *(const AS_L bf16x8*)(brow + ch * KC);
-        } else {
-          a = *(const AS_L f32x4*)(arow + ch * KC);
-          b = *(const AS_L f32x4*)(brow + ch * KC);
+      for (int sl = 0; sl < nslot; ++sl) {
+        const int b0 = r0 + sl * SAC_UPD_BCH;
+        if (b0 >= Bp) break;
+        const int bch = Bp - b0 < SAC_UPD_BCH ? Bp - b0 : SAC_UPD_BCH;
+        const AS_L T* arow = stage + sl * slot_el + (ns + c) * lds_row + g * KL;
+        const AS_L T* brow = stage + sl * slot_el + (32 + ks + c) * lds_row + g * KL;
+        for (int ch = 0; ch < bch / KC; ++ch) {
+          typename MM<T>::Frag a, b;
+          if constexpr (sizeof(T) == 2) {
+            a = *(const AS_L bf16x8*)(arow + ch * KC);
+            b = *(const AS_L bf16x8*)(brow + ch * KC);
+          } else {
+            a = *(const AS_L f32x4*)(arow + ch * KC);
+            b = *(const AS_L f32x4*)(brow + ch * KC);
+          }
+          MM<T>::mma(acc, a, b);
         }
-        MM<T>::mma(acc, a, b);
       }
     }
-    __syncthreads();  // the stage is refilled by the next chunk
+    __syncthreads();  // the stage is refilled by the next round
   }
   STAMP(polyak ? 49 : 53);
   if (wave < 4) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) accs[(ns + g * 4 + i) * 33 + ks + c] = acc[i];
   }
-  if (do_bias && tid < 256) red[bn * 9 + bs] = bsum;
+  if (do_bias && tid < 512) red[bn * 17 + bs] = bsum;
   __syncthreads();
   STAMP(polyak ? 50 : 54);
   // ---- 3. elements: Adam + Polyak on the masters; new values -> LDS
@@ -921,7 +972,7 @@ __device__ __forceinline__ void dw_adam_tile(const AS_C EngineDev& E, const Tile
   }
   if (do_bias && tid < 32 && td.n0 + tid < td.N) {
     float gb = 0.f;
-    for (int q = 0; q < 8; ++q) gb += red[tid * 9 + q];
+    for (int q = 0; q < 16; ++q) gb += red[tid * 17 + q];
     const float pbn = adam_elem(pb, mb, vb, gb, w1, b2, w2, bc2s, eps, neg_step);
     if (COH)
       coh_storef((float*)td.b + td.n0 + tid, pb);

@@ -214,7 +214,9 @@ class SacEngine:
         return (act, lp) if want_log_pi else act
 
     def time_phases(self, replay, n_steps: int) -> List[float]:
-        out = (ctypes.c_float * 4)()
+        """[A, B, C, D, gap]: mean hipEvent interval per phase launch (ms) and
+        that of an empty kernel launched the same way (see sac_engine.h)."""
+        out = (ctypes.c_float * 5)()
         E.check(self.lib.sac_engine_time_phases(self.handle, ctypes.byref(replay.desc), int(n_steps), out,
                                                 self._stream()))
         self.steps_done += n_steps
