@@ -220,6 +220,7 @@ def main():
     eng, rb, c = build_engine(args.config, args.precision, seed, device)
 
     eng.train_graph(rb, args.warmup, args.chunk)
+    eng.train_graph(rb, 0, args.chunk)  # capture the chunk graph now if warmup < chunk (runs no step)
     elapsed = timed_region(lambda: eng.train_graph(rb, args.steps, args.chunk), torch.cuda.synchronize, device)
     total_steps = args.steps * world
     eng.check()  # in-launch hand-offs all completed

@@ -135,7 +135,8 @@ int sac_engine_train(sac_engine *e, const sac_replay *rb, int32_t n_steps,
                      const int32_t *indices, const float *eps, void *stream);
 
 /* Same, replayed from a captured hipGraph of `chunk` steps (device sampler and
- * device eps only).  n_steps need not be a multiple of chunk. */
+ * device eps only).  n_steps need not be a multiple of chunk; n_steps = 0
+ * only captures the graph (no step runs). */
 int sac_engine_train_graph(sac_engine *e, const sac_replay *rb, int32_t n_steps,
                            int32_t chunk, void *stream);
 

@@ -662,7 +662,7 @@ int sac_engine_train_graph(sac_engine* e, const sac_replay* rb, int32_t n_steps,
   if (chunk < 1) return fail(SAC_E_INVALID, "chunk >= 1");
   hipStream_t s = (hipStream_t)stream;
   const bool same = e->gexec && e->gchunk == chunk && !memcmp(&e->gkey, rb, sizeof(sac_replay));
-  if (!same && n_steps >= chunk) {
+  if (!same && (n_steps >= chunk || n_steps == 0)) {  // n_steps == 0: capture only
     if (e->gexec) (void)hipGraphExecDestroy(e->gexec);
     if (e->graph) (void)hipGraphDestroy(e->graph);
     e->gexec = nullptr;

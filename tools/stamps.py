@@ -44,7 +44,9 @@ torch.cuda.synchronize()
 # mode "rerun": after each step, phase A launched again right behind itself
 # (instruction cache warm from the first A) and only that second A is stamped.
 # Timing experiment: the extra A advances the training state out of sequence.
-rerun = len(sys.argv) > 3 and sys.argv[3] == "rerun"
+# mode "rerunC": the same with phase C (weights read by the first C are warm for the second)
+rerun = len(sys.argv) > 3 and sys.argv[3] in ("rerun", "rerunC")
+rerun_kind = 2 if rerun and sys.argv[3] == "rerunC" else 0
 if rerun:
     lib.sac_engine_debug_launch.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p]
     desc = rb.desc
@@ -53,10 +55,10 @@ for it in range(10):
     buf.zero_()
     eng.train(rb, 1)
     if rerun:
-        E.check(lib.sac_engine_debug_launch(eng.handle, ctypes.byref(desc), 0, eng._stream()))
+        E.check(lib.sac_engine_debug_launch(eng.handle, ctypes.byref(desc), rerun_kind, eng._stream()))
         torch.cuda.synchronize()
         buf.zero_()
-        E.check(lib.sac_engine_debug_launch(eng.handle, ctypes.byref(desc), 0, eng._stream()))
+        E.check(lib.sac_engine_debug_launch(eng.handle, ctypes.byref(desc), rerun_kind, eng._stream()))
     torch.cuda.synchronize()
     runs.append(buf.view(nblk, 64).cpu().numpy().copy())
 names = {58: "D done", 59: "D waited",
