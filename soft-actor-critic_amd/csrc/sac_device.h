@@ -40,7 +40,9 @@ typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 // branches and loop bounds on it become exec-masked and values merged after them
 // land in VGPRs (a buffer descriptor merged that way needs a waterfall loop).
 __device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
+#ifndef SAC_ROWS
 #define SAC_ROWS 16             // batch rows per row-tile workgroup
+#endif
 #define SAC_PAD 32              // feature padding (bf16 MFMA K step)
 
 // ----------------------------------------------------------------------------- MFMA

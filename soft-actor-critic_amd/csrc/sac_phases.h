@@ -1311,7 +1311,14 @@ __device__ __forceinline__ void target_critic_body(const EngineDev* __restrict__
   Held<T, 1> ph0;
   Held<T, 8> ph1;
   ph0.tag = ph1.tag = nullptr;
-  if (!WITH_D && ROLES && role == 0) {
+  // late_ph1: layers 0 and 1's fragments are issued after the step counter's
+  // and the staged record's loads, so waiting for those (vmcnt retires in issue
+  // order) does not also wait for ~72 KB of cold weights (they land under the
+  // eps draw and the X build)
+  constexpr int MXS = 4;  // staged floats of s / s' per thread, at most
+  const bool late_ph1 = !WITH_D && ROLES && role == 0 && E.stage && !inj_idx_ &&
+                        SAC_ROWS * E.O <= MXS * SAC_THREADS && SAC_ROWS * E.A <= SAC_THREADS;
+  if (!WITH_D && ROLES && role == 0 && !late_ph1) {
     held_issue<T, 1>(ph0, gw_fwd(pi.l[0]));
     held_issue<T, 8>(ph1, gw_fwd(pi.l[1]));
   }
@@ -1347,14 +1354,49 @@ __device__ __forceinline__ void target_critic_body(const EngineDev* __restrict__
     const AS_G float* rec = GPC(float, E.stg) + (size_t)rbi * E.stg_stride;
     const AS_C uint64_t* hdr = (const AS_C uint64_t*)rec;
     const AS_G float* p = rec + 16;
-    for (int i = tid; i < R * O; i += SAC_THREADS) {
-      sB[i] = p[i];
-      s2B[i] = p[R * O + i];
-    }
-    for (int i = tid; i < R * A; i += SAC_THREADS) aB[i] = p[2 * R * O + i];
-    if (tid < R) {
-      rB[tid] = p[2 * R * O + R * A + tid];
-      dB[tid] = p[2 * R * O + R * A + R + tid];
+    if (late_ph1) {  // uniform: the record's loads, then layer 1's fragments, then the record's stores
+      float vs[MXS], vs2[MXS], va = 0.f, vr = 0.f, vd = 0.f;
+#pragma unroll
+      for (int u = 0; u < MXS; ++u) {
+        const int i = tid + u * SAC_THREADS;
+        vs[u] = vs2[u] = 0.f;
+        if (i < R * O) {
+          vs[u] = p[i];
+          vs2[u] = p[R * O + i];
+        }
+      }
+      if (tid < R * A) va = p[2 * R * O + tid];
+      if (tid < R) {
+        vr = p[2 * R * O + R * A + tid];
+        vd = p[2 * R * O + R * A + R + tid];
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      held_issue<T, 1>(ph0, gw_fwd(pi.l[0]));
+      held_issue<T, 8>(ph1, gw_fwd(pi.l[1]));
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int u = 0; u < MXS; ++u) {
+        const int i = tid + u * SAC_THREADS;
+        if (i < R * O) {
+          sB[i] = vs[u];
+          s2B[i] = vs2[u];
+        }
+      }
+      if (tid < R * A) aB[tid] = va;
+      if (tid < R) {
+        rB[tid] = vr;
+        dB[tid] = vd;
+      }
+    } else {
+      for (int i = tid; i < R * O; i += SAC_THREADS) {
+        sB[i] = p[i];
+        s2B[i] = p[R * O + i];
+      }
+      for (int i = tid; i < R * A; i += SAC_THREADS) aB[i] = p[2 * R * O + i];
+      if (tid < R) {
+        rB[tid] = p[2 * R * O + R * A + tid];
+        dB[tid] = p[2 * R * O + R * A + R + tid];
+      }
     }
     staged = hdr[0] == step && hdr[1] == (uint64_t)rb_size && hdr[2] == (uint64_t)rb_pos &&
              hdr[3] == (uint64_t)(uintptr_t)rb.obs;
