@@ -248,6 +248,8 @@ static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
   h.alpha_sc = (double*)P(lay.take(2 * 2 * 8));
   h.sync = (uint32_t*)P(lay.take((size_t)(SYNC_FLAGS + HK_COUNT * nrt * 16) * 4));
   h.hand = (float*)P(lay.take((size_t)HK_COUNT * nrt * SAC_HAND_STRIDE * 4));
+  h.gstride = SAC_ROWS * (A + 1);
+  h.gran = (uint64_t*)P(lay.take((size_t)G_COUNT * nrt * h.gstride * 8));
   h.stg_stride = (16 + 2 * SAC_ROWS * O + SAC_ROWS * A + 2 * SAC_ROWS + 15) / 16 * 16;
   h.stg = (float*)P(lay.take((size_t)nrt * h.stg_stride * 4));
   int nB = 0, nD = 0;

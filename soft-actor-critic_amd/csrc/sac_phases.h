@@ -72,6 +72,8 @@ struct EngineDev {
   // tiles onto 8/xs XCDs whose L2s then share one weight stream (speed only).
   int xs;
   int roles;  // phases A / C split into per-network workgroups (see "role hand-offs")
+  int gstride;     // granules per (kind, row tile): SAC_ROWS * (act_dim + 1)
+  uint64_t* gran;  // [G_COUNT][nrt][gstride] data-tagged hand-off granules (gran_put)
   int upd_slots;  // update tiles: batch chunks staged per round (LDS slots, 1..4)
   // update tiles, read by the fused launches (phase D inside phase A's launch,
   // phase B inside phase C's launch)
@@ -1151,6 +1153,39 @@ __device__ __forceinline__ void count_wait(const AS_C EngineDev& E, int word, ui
   __syncthreads();
 }
 
+// Data-tagged granules (MI355X_MICROARCH.md, handoff-1to1) for the hand-offs
+// whose consumer needs a few values per row: one 8-B sc1 store carries {value,
+// epoch}, and the consumer's lanes poll the values themselves.  There is no
+// drain, no separate flag, and one round trip.  Epochs advance once per step and
+// are never reset, so a granule left from an earlier step never matches.
+//   G_Q1T / G_Q2T: Q1t(s', a~') / Q2t per row (target critics -> critics),
+//   G_LP:          log pi(a~'|s') per row (target critic 1 -> critics),
+//   G_C1 / G_C2:   dQ_i/da~ [R][A] then q_i [R] (phase C critics -> pi).
+enum GranKind { G_Q1T = 0, G_Q2T = 1, G_LP = 2, G_C1 = 3, G_C2 = 4, G_COUNT = 5 };
+__device__ __forceinline__ AS_G uint64_t* gran_at(const AS_C EngineDev& E, int kind, int rbi) {
+  return GP(uint64_t, E.gran) + (size_t)(kind * E.nrt + rbi) * E.gstride;
+}
+__device__ __forceinline__ void gran_put(AS_G uint64_t* g, float v, uint32_t ep) {
+  const uint64_t x = (uint64_t)__float_as_uint(v) | ((uint64_t)ep << 32);
+  __hip_atomic_store((uint64_t*)g, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// one lane: the granule's value once it carries epoch ep (bounded spin; a
+// timeout sets the engine's error flag, see sac_engine_check)
+__device__ __forceinline__ float gran_get(const AS_C EngineDev& E, const AS_G uint64_t* g, uint32_t ep) {
+  uint64_t x = 0;
+  for (int it = 0;; ++it) {
+    x = __hip_atomic_load((uint64_t*)g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if ((uint32_t)(x >> 32) == ep) break;
+    if (it > (1 << 22)) {
+      __hip_atomic_store((uint32_t*)GP(uint32_t, E.sync) + SYNC_TIMEOUT, 1u, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+      break;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+  return __uint_as_float((uint32_t)x);
+}
+
 // ============================================================================ sample + gather
 // Row tile r0's replay slots for `step` (replay_buffer.py:32-39: distinct
 // uniform logical rows, 0 = oldest; -1 for padding rows): threads tid < R.
@@ -1552,6 +1587,7 @@ __device__ __forceinline__ void target_critic_body(const EngineDev* __restrict__
       hand_wait(E, HK_PI, rbi, ep);
       const AS_G float* h = hand_data(E, HK_PI, rbi);
       for (int i = tid; i < R * A; i += SAC_THREADS) a2B[i] = ld_sc1(h + i);
+      if (role == 1 && tid < R) gran_put(gran_at(E, G_LP, rbi) + tid, ld_sc1(h + R * A + tid), ep);
       __syncthreads();
     }
     for (int t = ROLES ? role - 1 : 0; t < (ROLES ? role : 2); ++t) {
@@ -1566,12 +1602,11 @@ __device__ __forceinline__ void target_critic_body(const EngineDev* __restrict__
                                       nvalid, pf, gw_fwd(E.net[t ? NET_Q1 : NET_Q2T].l[0]), &qh0, &qh1);
       if (tid < R) {
         qtB[t * R + tid] = outB[tid * ldo];
-        if (ROLES) st_sc1(hand_data(E, HK_T1 + t, rbi) + tid, outB[tid * ldo]);
+        if (ROLES) gran_put(gran_at(E, t ? G_Q2T : G_Q1T, rbi) + tid, outB[tid * ldo], ep);
       }
       __syncthreads();
       STAMP(7 + t);
     }
-    if (ROLES) hand_publish(E, HK_T1 + role - 1, rbi, ep);
     STAMP(9);
   }
   if (!ROLES) {
@@ -1625,9 +1660,7 @@ __device__ __forceinline__ void target_critic_body(const EngineDev* __restrict__
       __syncthreads();
       critic_unit_backward<T, R>(E, q, gqB, ldo, lds, pf);
       STAMP(16);
-      // y needs both target critics and log pi'.  The target critics published
-      // only after seeing pi's flag, so their flags also order pi's payload.
-      if (ROLES) hand_wait2(E, HK_T1, HK_T2, rbi, ep);
+      // y needs both target critics and log pi' (granules: each lane polls its row's three)
       STAMP(14);
       if (tid < 64) {  // wave 0: y, loss partial, seed dL/dq (mse_loss backward: 2(q-y)/B)
         float sq = 0.f;
@@ -1636,9 +1669,9 @@ __device__ __forceinline__ void target_critic_body(const EngineDev* __restrict__
           const bool v = tid < nvalid;
           float y;
           if (ROLES) {
-            const float q1t = ld_sc1(hand_data(E, HK_T1, rbi) + tid);
-            const float q2t = ld_sc1(hand_data(E, HK_T2, rbi) + tid);
-            const float lp2 = ld_sc1(hand_data(E, HK_PI, rbi) + R * A + tid);
+            const float q1t = gran_get(E, gran_at(E, G_Q1T, rbi) + tid, ep);
+            const float q2t = gran_get(E, gran_at(E, G_Q2T, rbi) + tid, ep);
+            const float lp2 = gran_get(E, gran_at(E, G_LP, rbi) + tid, ep);
             // alpha after the hand-offs: a phase D sharing the launch finished before pi started
             const float al = (float)__hip_atomic_load((double*)E.alpha_state + 1, __ATOMIC_RELAXED,
                                                       __HIP_MEMORY_SCOPE_AGENT);
@@ -1808,10 +1841,10 @@ __device__ __forceinline__ void actor_body(const EngineDev* __restrict__ Ep, int
                       qi ? gw_bwd(pi.l[pi.L - 1]) : gw_bwd(E.net[NET_Q2].l[E.net[NET_Q2].L - 1]));
       __syncthreads();
       if (ROLES) {
-        AS_G float* h = hand_data(E, HK_C1 + qi, rbi);
-        for (int i = tid; i < R * A; i += SAC_THREADS) st_sc1(h + i, Gx[(i / A) * ld + O + i % A]);
-        if (tid < R) st_sc1(h + R * A + tid, (qi ? out2 : out1)[tid * ldo]);
-        hand_publish(E, HK_C1 + qi, rbi, ep);
+        AS_G uint64_t* g = gran_at(E, G_C1 + qi, rbi);
+        for (int i = tid; i < R * A; i += SAC_THREADS) gran_put(g + i, Gx[(i / A) * ld + O + i % A], ep);
+        if (tid < R) gran_put(g + R * A + tid, (qi ? out2 : out1)[tid * ldo], ep);
+        __syncthreads();  // Gx is reused by the next critic's backward
       } else {
         for (int i = tid; i < R * A; i += SAC_THREADS) gaB[i] += Gx[(i / A) * ld + O + i % A];
         __syncthreads();
@@ -1838,15 +1871,13 @@ __device__ __forceinline__ void actor_body(const EngineDev* __restrict__ Ep, int
     held_issue<T, 8>(bh1, gw_bwd(pi.l[pi.L - 2]));
   }
   if (ROLES) {  // combine the critics' unit-seed gradients with the min-Q weights
-    hand_wait(E, HK_C1, rbi, ep);
-    hand_wait(E, HK_C2, rbi, ep);
-    const AS_G float* h1 = hand_data(E, HK_C1, rbi);
-    const AS_G float* h2 = hand_data(E, HK_C2, rbi);
+    const AS_G uint64_t* h1 = gran_at(E, G_C1, rbi);
+    const AS_G uint64_t* h2 = gran_at(E, G_C2, rbi);
     if (tid < 64) {
       float term = 0.f;
       if (tid < R) {
         const bool v = tid < nvalid;
-        const float q1 = ld_sc1(h1 + R * A + tid), q2 = ld_sc1(h2 + R * A + tid);
+        const float q1 = gran_get(E, h1 + R * A + tid, ep), q2 = gran_get(E, h2 + R * A + tid, ep);
         const float m = fmin_nan(q1, q2);
         term = v ? alpha32 * lpB[tid] - m : 0.f;
         const float gm = v ? -1.0f / (float)B : 0.f;
@@ -1859,7 +1890,7 @@ __device__ __forceinline__ void actor_body(const EngineDev* __restrict__ Ep, int
     __syncthreads();
     for (int i = tid; i < R * A; i += SAC_THREADS) {
       const int r = i / A;
-      gaB[i] = (gaB[i] + g1B[r] * ld_sc1(h1 + i)) + g2B[r] * ld_sc1(h2 + i);
+      gaB[i] = (gaB[i] + g1B[r] * gran_get(E, h1 + i, ep)) + g2B[r] * gran_get(E, h2 + i, ep);
     }
     __syncthreads();
     STAMP(39);
