@@ -1160,8 +1160,9 @@ __device__ __forceinline__ void count_wait(const AS_C EngineDev& E, int word, ui
 // are never reset, so a granule left from an earlier step never matches.
 //   G_Q1T / G_Q2T: Q1t(s', a~') / Q2t per row (target critics -> critics),
 //   G_LP:          log pi(a~'|s') per row (target critic 1 -> critics),
-//   G_C1 / G_C2:   dQ_i/da~ [R][A] then q_i [R] (phase C critics -> pi).
-enum GranKind { G_Q1T = 0, G_Q2T = 1, G_LP = 2, G_C1 = 3, G_C2 = 4, G_COUNT = 5 };
+//   G_C1 / G_C2:   dQ_i/da~ [R][A] then q_i [R] (phase C critics -> pi),
+//   G_PI:          a~' [R][A] then log pi' [R] (pi(s') -> target critics).
+enum GranKind { G_Q1T = 0, G_Q2T = 1, G_LP = 2, G_C1 = 3, G_C2 = 4, G_PI = 5, G_COUNT = 6 };
 __device__ __forceinline__ AS_G uint64_t* gran_at(const AS_C EngineDev& E, int kind, int rbi) {
   return GP(uint64_t, E.gran) + (size_t)(kind * E.nrt + rbi) * E.gstride;
 }
@@ -1539,7 +1540,7 @@ __device__ __forceinline__ void target_critic_body(const EngineDev* __restrict__
           GP(float, E.a_st)[(size_t)b * A + j] = act_v;
         } else {
           a2B[rr * A + j] = act_v;
-          if (ROLES) st_sc1(hand_data(E, HK_PI, rbi) + rr * A + j, act_v);
+          if (ROLES) gran_put(gran_at(E, G_PI, rbi) + rr * A + j, act_v, ep);
         }
       }
       for (int o = 1; o < AP; o <<= 1) {
@@ -1553,11 +1554,10 @@ __device__ __forceinline__ void target_critic_body(const EngineDev* __restrict__
           if (b < B) stats[4 + B + b] = v;
         } else {
           lp2B[rr] = v;
-          if (ROLES) st_sc1(hand_data(E, HK_PI, rbi) + R * A + rr, v);
+          if (ROLES) gran_put(gran_at(E, G_PI, rbi) + R * A + rr, v, ep);
         }
       }
     }
-    if (ROLES && tgt) hand_publish(E, HK_PI, rbi, ep);  // a~' and log pi' -> target critics and critics
     __syncthreads();
     STAMP(6);
   };
@@ -1584,10 +1584,9 @@ __device__ __forceinline__ void target_critic_body(const EngineDev* __restrict__
     if (ROLES) {
       held_issue<T, 1>(qh0, gw_fwd(E.net[NET_Q1T + role - 1].l[0]));
       held_issue<T, 8>(qh1, gw_fwd(E.net[NET_Q1T + role - 1].l[1]));
-      hand_wait(E, HK_PI, rbi, ep);
-      const AS_G float* h = hand_data(E, HK_PI, rbi);
-      for (int i = tid; i < R * A; i += SAC_THREADS) a2B[i] = ld_sc1(h + i);
-      if (role == 1 && tid < R) gran_put(gran_at(E, G_LP, rbi) + tid, ld_sc1(h + R * A + tid), ep);
+      const AS_G uint64_t* h = gran_at(E, G_PI, rbi);  // a~' and log pi' from pi(s')
+      for (int i = tid; i < R * A; i += SAC_THREADS) a2B[i] = gran_get(E, h + i, ep);
+      if (role == 1 && tid < R) gran_put(gran_at(E, G_LP, rbi) + tid, gran_get(E, h + R * A + tid, ep), ep);
       __syncthreads();
     }
     for (int t = ROLES ? role - 1 : 0; t < (ROLES ? role : 2); ++t) {
