@@ -271,8 +271,14 @@ static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
     lo += floats;
     return o;
   };
-  h.o_X = lt(2 * R * h.ld);
-  h.o_Y = lt(2 * R * h.ld);
+  // role split of phases A/C (decided here: it sizes the LDS): 6 * nrt
+  // workgroups must be co-resident (one per CU).  Only the one-block-per-row-
+  // tile kernels run pi on [s'; s] (2R rows); with roles every MLP pass is R rows.
+  int roles = 6 * nrt <= 256 && SAC_ROWS * (A + 1) <= SAC_HAND_STRIDE;
+  if (const char* v = getenv("SAC_ROLES")) roles = roles && atoi(v) != 0;
+  const int xrows = roles ? R : 2 * R;
+  h.o_X = lt(xrows * h.ld);
+  h.o_Y = lt(xrows * h.ld);
   const int Lhq = c->q_layers - 1, Lhp = c->pi_layers - 1;
   for (int l = 0; l < std::max(Lhq, Lhp); ++l) {
     int np = 0;
@@ -293,8 +299,8 @@ static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
   h.o_d = lt(R);
   h.o_et = lt(R * A);
   h.o_ea = lt(R * A);
-  h.o_out = lt(2 * R * h.ldo);
-  h.o_outp = lt(2 * R * h.ldo);
+  h.o_out = lt(xrows * h.ldo);
+  h.o_outp = lt(xrows * h.ldo);
   h.o_out2 = lt(R * h.ldo);
   h.o_outp2 = lt(R * h.ldo);
   h.o_lp = lt(R);
@@ -319,8 +325,6 @@ static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
       if (const char* v = getenv("SAC_XS")) xs = std::max(1, atoi(v));
       h.xs = xs;
       // role split of phases A/C: 6 * nrt workgroups must be co-resident (one per CU)
-      int roles = 6 * nrt <= 256 && SAC_ROWS * (A + 1) <= SAC_HAND_STRIDE;
-      if (const char* v = getenv("SAC_ROLES")) roles = roles && atoi(v) != 0;
       h.roles = roles;
       // phase C stages the next step's batch (SAC_STAGE=0 turns it off)
       int stage = 1;
