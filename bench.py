@@ -67,12 +67,14 @@ def synthetic_replay(rb, cap, obs, act, seed):
     torch.cuda.synchronize()
 
 
-def build_engine(cfgname, precision, seed, device):
+def build_engine(cfgname, precision, seed, device, capacity=None):
     from sac.engine import SacEngine
     from sac.models import PolicyNetwork, QNetwork
     from sac.replay_buffer import ReplayBuffer
 
-    c = CONFIGS[cfgname]
+    c = dict(CONFIGS[cfgname])
+    if capacity:
+        c["capacity"] = capacity
     pi = PolicyNetwork(c["obs"], c["act"], c["hidden"], seed=seed).to(device)
     q1 = QNetwork(c["obs"], c["act"], c["hidden"], seed=seed).to(device)
     q2 = QNetwork(c["obs"], c["act"], c["hidden"], seed=seed + 1).to(device)
@@ -89,62 +91,104 @@ def build_engine(cfgname, precision, seed, device):
 
 
 def gather_sweep(rb, device, sizes=(256, 4096, 65536, 1_048_576), reps=20):
-    """Standalone device sampler + SoA gather: GB/s of (s,a,r,s',d) delivered."""
+    """Standalone replay sample + gather (SURVEY §8d roofline leg), two forms:
+      sample_gather: the device sampler's B distinct rows gathered in ONE kernel
+                     (sac_replay_sample_gather), for B <= len(rb);
+      gather:        sac_replay_gather of B uniform rows drawn WITH replacement
+                     (torch.randint, outside the timed loop) -- the bandwidth leg,
+                     which also runs B = 1,048,576 > the 1e6-row buffer.
+    Returns {form: {B: GB/s}} with GB/s = B_gather / kernel time, B_gather =
+    4 B (2 obs + act + 2) bytes read (the gather writes as many
+    again), plus the per-launch ms of each point (hipEvents on the launch
+    stream, the current torch stream)."""
     from sac import _engine as E
     import ctypes
 
     lib = E.load_library()
-    out = {}
     W = 2 * rb.obs_dim + rb.act_dim + 2
+    st = E.stream_handle(device)
+    desc = rb.desc
+    out = {"sample_gather": {}, "gather": {}, "ms": {}}
+    f = dict(dtype=torch.float32, device=device)
     for B in sizes:
-        if B > len(rb):
-            continue
-        idx = torch.empty(B, dtype=torch.int32, device=device)
-        f = dict(dtype=torch.float32, device=device)
         s, a, r, s2, d = (torch.empty(B, rb.obs_dim, **f), torch.empty(B, rb.act_dim, **f), torch.empty(B, **f),
                           torch.empty(B, rb.obs_dim, **f), torch.empty(B, **f))
-        st = E.stream_handle(device)
-        desc = rb.desc
-
-        def once(k):
-            E.check(lib.sac_replay_sample_indices(ctypes.byref(desc), B, 7, k, E.ptr(idx), st))
-            E.check(lib.sac_replay_gather(ctypes.byref(desc), E.ptr(idx), B, E.ptr(s), E.ptr(a), E.ptr(r),
-                                          E.ptr(s2), E.ptr(d), st))
-
-        for k in range(3):
-            once(k)
-        torch.cuda.synchronize()
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        for k in range(reps):
-            once(k)
-        e1.record()
-        torch.cuda.synchronize()
-        ms = e0.elapsed_time(e1) / reps
-        out[str(B)] = round(B * W * 4 / (ms * 1e-3) / 1e9, 3)
+        ptrs = [E.ptr(t) for t in (s, a, r, s2, d)]
+        ridx = torch.randint(0, len(rb), (B,), dtype=torch.int32, device=device,
+                             generator=torch.Generator(device=device).manual_seed(B))
+        forms = {"gather": lambda k: E.check(lib.sac_replay_gather(ctypes.byref(desc), E.ptr(ridx), B, *ptrs, st))}
+        if B <= len(rb):
+            forms["sample_gather"] = lambda k: E.check(lib.sac_replay_sample_gather(
+                ctypes.byref(desc), B, 7, k, None, *ptrs, st))
+        for form, once in forms.items():
+            for k in range(3):
+                once(k)
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for k in range(reps):
+                once(k)
+            e1.record()
+            torch.cuda.synchronize()
+            ms = e0.elapsed_time(e1) / reps
+            out[form][str(B)] = round(B * W * 4 / (ms * 1e-3) / 1e9, 3)
+            out["ms"][f"{form}/{B}"] = round(ms, 5)
     return out
 
 
-def pmc_traffic(kernel):
+def bf16_deviation(cfgname, seed, device, steps=3):
+    """The bf16 perf mode's loss deviation: fp32 and bf16 engines from the same
+    init (bench.build_engine seeding) fed the same injected indices and eps for
+    `steps` steps; max over steps of |L_bf16 - L_fp32| / max(|L_fp32|, floor)
+    per loss (floor 1e-3; L_pi: mean|y| of the step, as tests/test_gpu_parity.py).
+    The fp32 engine is the parity mode tests/ pin against the oracle at 1e-4."""
+    c = CONFIGS[cfgname]
+    engs = {p: build_engine(cfgname, p, seed, device, capacity=max(4096, c["batch"] * 2)) for p in ("fp32", "bf16")}
+    B, A = c["batch"], c["act"]
+    g = np.random.default_rng(123)
+    dev = [0.0] * 4
+    for _ in range(steps):
+        idx = torch.from_numpy(g.choice(len(engs["fp32"][1]), size=(1, B), replace=False).astype(np.int32))
+        eps = torch.from_numpy(g.standard_normal((1, 2, B, A)).astype(np.float32))
+        res = {}
+        for p, (eng, rb, _) in engs.items():
+            eng.train(rb, 1, indices=idx, eps=eps)
+            res[p] = (eng.losses(), float(eng.last_targets().abs().mean()))
+        (lf, ym), (lb, _) = res["fp32"], res["bf16"]
+        for i in range(4):
+            if np.isnan(lf[i]):
+                continue
+            floor = ym if i == 2 else 1e-3
+            dev[i] = max(dev[i], abs(lb[i] - lf[i]) / max(abs(lf[i]), floor))
+    return {"loss_rel_dev_vs_fp32": [round(x, 7) for x in dev], "steps": steps,
+            "losses": ["L_Q1", "L_Q2", "L_pi (floor mean|y|)", "L_alpha"]}
+
+
+def pmc_traffic(kernel, config, precision):
     """HBM-side bytes per launch of `kernel` from the newest committed PMC
-    summary (profiles/<round>_pmc.json, written by tools/pmc_summary.py from
-    separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this bench)."""
+    summary for this (config, precision) (profiles/<round>_pmc*.json, written
+    by tools/pmc_summary.py from separate rocprofv3 --pmc FETCH_SIZE /
+    WRITE_SIZE passes of this bench), or (None, None)."""
     import glob
 
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc.json")))
-    if not files:
-        return None, None
-    with open(files[-1]) as f:
-        d = json.load(f)
-    k = d.get("kernels", {}).get(kernel)
-    if not k:
-        return None, None
-    return k["hbm_bytes_per_launch"], os.path.relpath(files[-1], ROOT)
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc*.json")), reverse=True):
+        with open(path) as f:
+            d = json.load(f)
+        if d.get("config", "c2") != config or d.get("precision", "bf16") != precision:
+            continue
+        k = d.get("kernels", {}).get(kernel)
+        if k:
+            return k["hbm_bytes_per_launch"], os.path.relpath(path, ROOT)
+    return None, None
 
 
-def cpu_baseline(cfgname, seconds=12.0):
-    """Oracle (numpy restatement of the reference step incl. its deque +
-    random.sample replay) on the host, single BLAS thread, bounded sample."""
+def cpu_baseline(cfgname, seconds=5.0):
+    """The reference CPU path on the host: the oracle (numpy restatement of the
+    reference step, incl. its deque + random.sample replay over the full
+    buffer) timed per BASELINE.md §4 -- BLAS threads 1 and T (T = the host's
+    CPU share: OMP_NUM_THREADS, else os.cpu_count()), full training_step()s and
+    update-only steps (batch sampled outside the timed loop), `seconds` each.
+    value = the faster full-step leg; every leg is listed."""
     from threadpoolctl import threadpool_limits
 
     from oracle import sac_oracle as O
@@ -175,20 +219,29 @@ def cpu_baseline(cfgname, seconds=12.0):
                           mlp([O_ + A_] + c["hidden"] + [1], 2), hp, A_)
     B = c["batch"]
     erng = np.random.default_rng(1)
-    n = 0
-    with threadpool_limits(limits=1):
-        t0 = time.perf_counter()
-        while True:
-            b = O.sample_batch(buf, B)
-            O.training_step(st, hp, b, erng.standard_normal((B, A_), dtype=np.float32),
-                            erng.standard_normal((B, A_), dtype=np.float32))
-            n += 1
-            el = time.perf_counter() - t0
-            if el >= seconds:
-                break
-    return {"value": round(n / el, 3), "unit": "gradient steps/s", "cores": 1, "kind": "port",
-            "sample": f"{n} full training_step()s (deque+random.sample over {cap} rows, B={B}) in {el:.1f}s, "
-                      "numpy fp32, 1 BLAS thread"}
+    nthr = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
+    fixed = O.sample_batch(buf, B)
+    legs = []
+    for threads in (1, nthr):
+        for kind in ("full", "update_only"):
+            n = 0
+            with threadpool_limits(limits=threads):
+                t0 = time.perf_counter()
+                while True:
+                    b = O.sample_batch(buf, B) if kind == "full" else fixed
+                    O.training_step(st, hp, b, erng.standard_normal((B, A_), dtype=np.float32),
+                                    erng.standard_normal((B, A_), dtype=np.float32))
+                    n += 1
+                    el = time.perf_counter() - t0
+                    if el >= seconds:
+                        break
+            legs.append({"threads": threads, "kind": kind, "steps_per_s": round(n / el, 3), "steps": n,
+                         "seconds": round(el, 2)})
+    full = max((l for l in legs if l["kind"] == "full"), key=lambda l: l["steps_per_s"])
+    return {"value": full["steps_per_s"], "unit": "gradient steps/s", "cores": full["threads"], "kind": "port",
+            "sample": f"full training_step()s (deque+random.sample over {cap} rows, B={B}) and update-only steps, "
+                      f"numpy fp32, BLAS threads 1 and {nthr} (host CPU share), {seconds:.0f}s per leg",
+            "host_threads": nthr, "legs": legs}
 
 
 def main():
@@ -197,10 +250,12 @@ def main():
     ap.add_argument("--steps", type=int, default=2000)
     ap.add_argument("--warmup", type=int, default=200)
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
-    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--precision", default="fp32", choices=["bf16", "fp32"],
+                    help="headline arithmetic; fp32 is the reference's (bf16 is also timed unless --no-bf16)")
     ap.add_argument("--chunk", type=int, default=64)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-sweep", action="store_true")
+    ap.add_argument("--no-bf16", action="store_true")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -214,19 +269,25 @@ def main():
 
         dist.init_process_group("nccl", device_id=device)
 
-    from sac.replicas import replica_seed, timed_region
+    from sac.replicas import aggregate_metrics, replica_seed, timed_region
 
     seed = replica_seed(0, rank)
-    eng, rb, c = build_engine(args.config, args.precision, seed, device)
+    # graph chunk <= the timed steps, so a short driver run is graph-replayed too
+    chunk = max(1, min(args.chunk, args.steps))
 
-    eng.train_graph(rb, args.warmup, args.chunk)
-    eng.train_graph(rb, 0, args.chunk)  # capture the chunk graph now if warmup < chunk (runs no step)
-    elapsed = timed_region(lambda: eng.train_graph(rb, args.steps, args.chunk), torch.cuda.synchronize, device)
+    def timed(precision):
+        eng, rb, c = build_engine(args.config, precision, seed, device)
+        eng.train_graph(rb, args.warmup, chunk)
+        eng.train_graph(rb, 0, chunk)  # capture the chunk graph now if warmup < chunk (runs no step)
+        el = timed_region(lambda: eng.train_graph(rb, args.steps, chunk), torch.cuda.synchronize, device)
+        eng.check()  # in-launch hand-offs all completed (raises HandoffTimeout otherwise)
+        ls = eng.losses()
+        if not all(np.isfinite(ls[:3])):
+            raise SystemExit(f"non-finite losses after benchmark ({precision}): {ls}")
+        return eng, rb, c, el, ls
+
+    eng, rb, c, elapsed, losses = timed(args.precision)
     total_steps = args.steps * world
-    eng.check()  # in-launch hand-offs all completed
-    losses = eng.losses()
-    if not all(np.isfinite(losses[:3])):
-        raise SystemExit(f"non-finite losses after benchmark: {losses}")
 
     # per-phase device time (hipEvents on the launch stream), then roofline of the dominant kernel
     # Each interval also holds the cost of the event after it; the timed region
@@ -249,9 +310,13 @@ def main():
     from sac import _engine as E
 
     kname = E.load_library().sac_phase_kernel_name(dom).decode()
-    traffic, traffic_src = pmc_traffic(kname) if args.config == "c2" and args.precision == "bf16" else (None, None)
+    traffic, traffic_src = pmc_traffic(kname, args.config, args.precision)
     achieved = flops[dom] / (kern_ms[dom] * 1e-3) / 1e12
     peak = PEAK_TFLOPS[args.precision]
+    replica = None
+    if dist:  # the periodic RCCL metric all-reduce of the replicas, here once per run
+        replica = aggregate_metrics([args.steps, elapsed] + list(losses) + [float(eng.alpha_state[1]), 0.0],
+                                    device=device)
 
     if rank == 0:
         sweep = {} if args.no_sweep else gather_sweep(rb, device)
@@ -272,10 +337,10 @@ def main():
             "data": "synthetic (numpy default_rng, SURVEY §8d), random-init reference-seeded weights",
             "config": {"workload": f"{args.config}: {c['name']} obs={c['obs']} act={c['act']} "
                                    f"2x{c['hidden']} MLPs, buffer={c['capacity']}, batch={c['batch']}, "
-                                   "auto-alpha, device sampler",
-                       "global_batch": c["batch"] * world, "parallelism": f"replicas{world}"},
+                                   f"auto-alpha, device sampler, {args.precision} arithmetic",
+                       "global_batch": c["batch"] * world, "parallelism": f"replicas{world}",
+                       "graph_chunk": chunk},
             "replay_sample_GBps_in_step": round(sps / world * c["batch"] * W * 4 / 1e9, 4),
-            "replay_sample_GBps_sweep": sweep,
             "phase_ms": [round(x, 5) for x in kern_ms],
             "phase_event_interval_ms": [round(x, 5) for x in phase_ms],
             "event_cost_ms": round(ev_cost, 5),
@@ -288,8 +353,32 @@ def main():
                          "timing": "hipEvents after every launch on the launch stream over 100 steps; "
                                    "avg_launch_ms = mean interval of this kernel's launches minus the per-launch "
                                    "event cost (event intervals of a step - event-free graph step time, per launch)"},
+            "step_roofline": {"achieved_TFLOPs": round(f_total * sps / world / 1e12, 3), "peak": peak,
+                              "frac": round(f_total * sps / world / 1e12 / peak, 5),
+                              "note": "SURVEY F_alg per step x steps/s of one learner"},
             "losses_last": [round(x, 6) for x in losses],
         }
+        if sweep:
+            line["replay_sample_GBps_sweep"] = sweep["sample_gather"]
+            line["replay_gather_GBps_sweep"] = sweep["gather"]
+            bmax = max(int(b) for b in sweep["gather"])
+            ms = sweep["ms"][f"gather/{bmax}"]
+            gtr, gsrc = pmc_traffic("replay_gather_kernel", "gather", "fp32")
+            line["roofline_gather"] = {
+                "bound": "hbm", "kernel": "replay_gather_kernel", "batch": bmax,
+                "achieved": sweep["gather"][str(bmax)], "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                "frac": round(sweep["gather"][str(bmax)] / PEAK_HBM_GBS, 5), "traffic": gtr,
+                "traffic_source": gsrc, "bytes_per_launch": bmax * W * 4, "avg_launch_ms": ms,
+                "note": "B_gather = 4 B (2 obs + act + 2) bytes read per launch (SURVEY §8d); the kernel writes "
+                        "as many again; rows uniform with replacement over the 1e6-row buffer"}
+        if not args.no_bf16 and args.precision == "fp32" and world == 1:  # single-process leg: no barriers
+            eb, rbb, _, elb, lsb = timed("bf16")
+            line["value_bf16"] = round(total_steps / elb, 2)
+            line["ms_per_step_bf16"] = round(elb / args.steps * 1e3, 5)
+            line["bf16_parity"] = bf16_deviation(args.config, seed, device)
+            del eb, rbb
+        if replica is not None:
+            line["replica_metrics"] = replica
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(args.config)
         print(json.dumps(line), flush=True)

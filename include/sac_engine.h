@@ -28,7 +28,9 @@
  *   - replay storage is struct-of-arrays, fp32, ring-ordered:
  *     obs[cap][obs_dim], act[cap][act_dim], rew[cap], next_obs[cap][obs_dim],
  *     done[cap]; state[0] = number of valid rows, state[1] = next write slot
- *     (the oldest row once full).
+ *     (the oldest row once full), state[2] = push generation (incremented by
+ *     every push and by ReplayBuffer.clear(); a batch the engine staged for
+ *     the next step is used only while it matches).
  */
 #ifndef SAC_ENGINE_H
 #define SAC_ENGINE_H
@@ -95,7 +97,7 @@ typedef struct sac_replay {
   float *obs, *act, *rew, *next_obs, *done;
   int64_t capacity;
   int32_t obs_dim, act_dim;
-  int64_t *state;        /* device [2]: size, next write slot */
+  int64_t *state;        /* device [3]: size, next write slot, push generation */
 } sac_replay;
 
 typedef struct sac_engine sac_engine;
@@ -164,6 +166,16 @@ int sac_replay_gather(const sac_replay *rb, const int32_t *logical_idx, int32_t 
 int sac_replay_sample_indices(const sac_replay *rb, int32_t batch, uint64_t seed,
                               uint64_t step, int32_t *out, void *stream);
 
+/* Device sampler + gather in ONE kernel: the sampler's `batch` distinct rows
+ * for (seed, step) gathered into SoA outputs as sac_replay_gather does (the
+ * indices are also written to idx_out unless it is NULL).  The caller
+ * guarantees batch <= size (Python raises the reference's ValueError first).
+ * Replaces: ReplayBuffer.sample + SAC.sample_batch (replay_buffer.py:32-39,
+ * agent.py:166-193) with the device RNG in place of random.sample. */
+int sac_replay_sample_gather(const sac_replay *rb, int32_t batch, uint64_t seed,
+                             uint64_t step, int32_t *idx_out, float *s, float *a,
+                             float *r, float *s2, float *d, void *stream);
+
 /* Profiling: runs n_steps with hipEvents after each launch and returns the
  * mean event interval per phase launch in ms (ms_host holds 5 floats):
  * [0]=A target+critic-backward, [1]=B critic dW+Adam+Polyak, [2]=C actor,
@@ -182,6 +194,14 @@ int sac_engine_time_phases(sac_engine *e, const sac_replay *rb, int32_t n_steps,
  * workgroup hand-off of the role-split phase kernels gave up waiting (the
  * affected steps are invalid), else 0.  Replaces: nothing (diagnostic). */
 int sac_engine_check(sac_engine *e, void *stream);
+
+/* Asynchronous status read: copies the engine's two status words [launch
+ * epoch, hand-off timeout flag] into host_dst (pinned host memory; valid once
+ * the stream has reached this point).  A non-zero timeout flag means a step's
+ * results are invalid; the Python API raises RuntimeError on it (lazily, with
+ * no per-step synchronisation).  sac_engine_clear_status resets the flag. */
+int sac_engine_read_status(sac_engine *e, uint32_t *host_dst, void *stream);
+int sac_engine_clear_status(sac_engine *e, void *stream);
 
 /* Launch layout of a step: 0 = four launches (A B C D); 1 = phase D of step
  * k runs inside phase A's launch of step k + 1 (three launches); 2 = also phase

@@ -26,6 +26,10 @@ int sac_engine_uses_roles(const sac_engine *e);
  * inside sac_engine_train and sac_replay_sample_indices): out[b] = b-th element
  * of the Philox-keyed Feistel permutation of [0, size) for RNG (seed, step). */
 int sac_debug_sample_indices_host(int64_t size, int32_t batch, uint64_t seed, uint64_t step, int32_t *out);
+/* Polls a hand-off wait makes before it gives up and sets the timeout flag
+ * (default 1 << 22, about 0.3 s); synchronises the stream.  A bound of 0
+ * forces the timeout path (tests/test_gpu_engine.py): the API must raise. */
+int sac_engine_debug_set_spin_limit(sac_engine *e, int32_t polls, void *stream);
 #ifdef __cplusplus
 }
 #endif

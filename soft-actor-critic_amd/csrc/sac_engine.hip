@@ -70,44 +70,84 @@ __global__ void replay_push_kernel(sac_replay rb, const float* __restrict__ rows
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     rb.state[0] = new_size;
     rb.state[1] = new_pos;
+    rb.state[2] += 1;  // push generation (a staged batch record of an older generation is stale)
   }
 }
 
-// SoA gather, one float per thread-iteration over the flattened [B][W] batch.
-__global__ void replay_gather_kernel(sac_replay rb, const int32_t* __restrict__ idx, int B, float* __restrict__ s,
-                                     float* __restrict__ a, float* __restrict__ r, float* __restrict__ s2,
-                                     float* __restrict__ d) {
-  const int O = rb.obs_dim, A = rb.act_dim;
-  const int64_t size = rb.state[0], pos = rb.state[1];
-  const int W = 2 * O + A + 2;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < (int64_t)B * W;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    int64_t b, c;
-    // field-major flattening keeps each field's reads/writes contiguous
-    if (i < (int64_t)B * O) {
-      b = i / O; c = i % O;
-      const int64_t li = idx[b];
-      const int64_t sl = size < rb.capacity ? li : (pos + li) % rb.capacity;
-      s[i] = rb.obs[sl * O + c];
-    } else if (i < (int64_t)B * (2 * O)) {
-      const int64_t j = i - (int64_t)B * O;
-      b = j / O; c = j % O;
-      const int64_t li = idx[b];
-      const int64_t sl = size < rb.capacity ? li : (pos + li) % rb.capacity;
-      s2[j] = rb.next_obs[sl * O + c];
-    } else if (i < (int64_t)B * (2 * O + A)) {
-      const int64_t j = i - (int64_t)B * 2 * O;
-      b = j / A; c = j % A;
-      const int64_t li = idx[b];
-      const int64_t sl = size < rb.capacity ? li : (pos + li) % rb.capacity;
-      a[j] = rb.act[sl * A + c];
-    } else {
-      const int64_t j = i - (int64_t)B * (2 * O + A);
-      b = j >> 1;
-      const int64_t li = idx[b];
-      const int64_t sl = size < rb.capacity ? li : (pos + li) % rb.capacity;
-      if (j & 1) d[b] = rb.done[sl]; else r[b] = rb.rew[sl];
+// Replay gather by LOGICAL index (reference replay_buffer.py:32-39 +
+// agent.py:166-193), one wave per 64 batch rows.  Lane l resolves row b0+l's
+// ring slot ONCE (32-bit index load or the device sampler, one conditional
+// subtract instead of a 64-bit modulo); then each field is copied
+// row-vectorised: the wave's 64 output rows of a field are one contiguous span
+// of the SoA output, swept 16 B per lane (4 B when the field width is not a
+// multiple of 4 floats), each lane taking its source row's slot from the
+// owner lane by a shuffle.  Loads are issued in batches of GATHER_GB before
+// their stores (memory-level parallelism: a batch's rows are independent).
+#define GATHER_GB 8
+template <typename V>
+__device__ __forceinline__ void gather_field(const float* __restrict__ src, int W, float* __restrict__ dst, int nrow,
+                                             int64_t slot, int lane) {
+  constexpr int EV = sizeof(V) / 4;  // floats per access
+  const int Q = W / EV;              // accesses per row
+  const int total = nrow * Q;
+  const V* __restrict__ sv = (const V*)src;
+  V* __restrict__ dv = (V*)dst;
+  for (int i0 = 0; i0 < total; i0 += 64 * GATHER_GB) {
+    V v[GATHER_GB];
+#pragma unroll
+    for (int u = 0; u < GATHER_GB; ++u) {
+      const int i = i0 + u * 64 + lane;
+      const int row = (unsigned)i / (unsigned)Q, q = i - row * Q;
+      const int64_t sl = __shfl(slot, row < 64 ? row : 63, 64);  // every lane joins the shuffle
+      if (i < total) v[u] = sv[sl * Q + q];
     }
+#pragma unroll
+    for (int u = 0; u < GATHER_GB; ++u) {
+      const int i = i0 + u * 64 + lane;
+      if (i < total) dv[i] = v[u];
+    }
+  }
+}
+
+template <bool SAMPLE>
+__global__ void __launch_bounds__(256) replay_gather_kernel(sac_replay rb, const int32_t* __restrict__ idx, int B,
+                                                            uint64_t seed, uint64_t step, int32_t* __restrict__ idx_out,
+                                                            float* __restrict__ s, float* __restrict__ a,
+                                                            float* __restrict__ r, float* __restrict__ s2,
+                                                            float* __restrict__ d) {
+  const int lane = threadIdx.x & 63;
+  const int b0 = (int)(((size_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6) * 64;
+  if (b0 >= B) return;  // whole waves
+  const int nrow = B - b0 < 64 ? B - b0 : 64;
+  const int O = rb.obs_dim, A = rb.act_dim;
+  const int64_t size = rb.state[0], pos = rb.state[1], cap = rb.capacity;
+  int64_t slot = 0;
+  if (lane < nrow) {
+    int64_t li;
+    if (SAMPLE) {
+      const Feistel f = feistel_make(seed, step, size);
+      li = feistel_sample(f, b0 + lane, size);
+      if (idx_out) idx_out[b0 + lane] = (int32_t)li;
+    } else {
+      li = idx[b0 + lane];
+    }
+    const int64_t p = pos + li;  // li < size <= cap, pos < cap
+    slot = size < cap ? li : (p >= cap ? p - cap : p);
+  }
+  if ((O & 3) == 0) {
+    gather_field<f32x4>(rb.obs, O, s + (size_t)b0 * O, nrow, slot, lane);
+    gather_field<f32x4>(rb.next_obs, O, s2 + (size_t)b0 * O, nrow, slot, lane);
+  } else {
+    gather_field<float>(rb.obs, O, s + (size_t)b0 * O, nrow, slot, lane);
+    gather_field<float>(rb.next_obs, O, s2 + (size_t)b0 * O, nrow, slot, lane);
+  }
+  if ((A & 3) == 0)
+    gather_field<f32x4>(rb.act, A, a + (size_t)b0 * A, nrow, slot, lane);
+  else
+    gather_field<float>(rb.act, A, a + (size_t)b0 * A, nrow, slot, lane);
+  if (lane < nrow) {
+    r[b0 + lane] = rb.rew[slot];
+    d[b0 + lane] = rb.done[slot];
   }
 }
 
@@ -345,6 +385,7 @@ static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
     h.target_entropy = c->target_entropy;
     h.alpha_lr = c->alpha_lr;
     h.seed = c->seed;
+    h.spin_limit = 1 << 22;
     float* parts[5] = {e->buf.pi, e->buf.q1, e->buf.q2, e->buf.q1t, e->buf.q2t};
     float* ms[3] = {e->buf.pi_m, e->buf.q1_m, e->buf.q2_m};
     float* vs[3] = {e->buf.pi_v, e->buf.q1_v, e->buf.q2_v};
@@ -720,10 +761,40 @@ int sac_replay_push(const sac_replay* rb, const float* rows, int64_t n, int64_t 
 int sac_replay_gather(const sac_replay* rb, const int32_t* logical_idx, int32_t batch, float* s, float* a, float* r,
                       float* s2, float* d, void* stream) {
   if (!rb || !logical_idx || batch < 1 || !s || !a || !r || !s2 || !d) return fail(SAC_E_INVALID, "bad gather arguments");
-  const int64_t total = (int64_t)batch * (2 * rb->obs_dim + rb->act_dim + 2);
-  const int blocks = (int)std::min<int64_t>(8192, (total + 255) / 256);
-  replay_gather_kernel<<<blocks, 256, 0, (hipStream_t)stream>>>(*rb, logical_idx, batch, s, a, r, s2, d);
+  const int blocks = (batch + 255) / 256;  // one wave per 64 rows
+  replay_gather_kernel<false><<<blocks, 256, 0, (hipStream_t)stream>>>(*rb, logical_idx, batch, 0, 0, nullptr, s, a,
+                                                                       r, s2, d);
   HIPCHK(hipGetLastError());
+  return SAC_OK;
+}
+
+int sac_replay_sample_gather(const sac_replay* rb, int32_t batch, uint64_t seed, uint64_t step, int32_t* idx_out,
+                             float* s, float* a, float* r, float* s2, float* d, void* stream) {
+  if (!rb || batch < 1 || !s || !a || !r || !s2 || !d) return fail(SAC_E_INVALID, "bad sample_gather arguments");
+  const int blocks = (batch + 255) / 256;
+  replay_gather_kernel<true><<<blocks, 256, 0, (hipStream_t)stream>>>(*rb, nullptr, batch, seed, step, idx_out, s, a,
+                                                                      r, s2, d);
+  HIPCHK(hipGetLastError());
+  return SAC_OK;
+}
+
+int sac_engine_read_status(sac_engine* e, uint32_t* host_dst, void* stream) {
+  if (!e || !host_dst) return fail(SAC_E_INVALID, "bad read_status arguments");
+  HIPCHK(hipMemcpyAsync(host_dst, e->h.sync, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, (hipStream_t)stream));
+  return SAC_OK;
+}
+
+int sac_engine_clear_status(sac_engine* e, void* stream) {
+  if (!e) return fail(SAC_E_INVALID, "null engine");
+  HIPCHK(hipMemsetAsync(e->h.sync + SYNC_TIMEOUT, 0, sizeof(uint32_t), (hipStream_t)stream));
+  return SAC_OK;
+}
+
+int sac_engine_debug_set_spin_limit(sac_engine* e, int32_t polls, void* stream) {
+  if (!e || polls < 0) return fail(SAC_E_INVALID, "bad spin limit");
+  e->h.spin_limit = polls;
+  HIPCHK(hipMemcpyAsync(e->d, &e->h, sizeof(EngineDev), hipMemcpyHostToDevice, (hipStream_t)stream));
+  HIPCHK(hipStreamSynchronize((hipStream_t)stream));
   return SAC_OK;
 }
 

@@ -110,6 +110,7 @@ struct EngineDev {
   float* stg;
   int stg_stride;  // floats per row-tile record
   int stage;       // stager blocks launched with phase C
+  int spin_limit;  // polls before a hand-off wait gives up and sets SYNC_TIMEOUT (~0.3 s at 1 << 22)
   // LDS layout (float offsets)
   int o_X, o_Y, o_P1[SAC_DEV_LAYERS], ldp1[SAC_DEV_LAYERS], o_P2[SAC_DEV_LAYERS], ldp2[SAC_DEV_LAYERS];
   int o_s, o_s2, o_a, o_a2, o_r, o_d, o_et, o_ea, o_out, o_outp, o_out2, o_outp2, o_lp, o_qt, o_y, o_g, o_g2,
@@ -1088,9 +1089,12 @@ __device__ __forceinline__ void alpha_and_losses(const AS_C EngineDev& E, int pa
 // stores (s_waitcnt vmcnt(0)) before a workgroup barrier, then one lane stores
 // the flag (sc1); the consumer polls the flag with sc1 loads from one lane and
 // joins the others at a barrier.  Flags carry a per-launch epoch (E.sync[0] + 1,
-// advanced by phase D), so they are never reset.  Producers have lower block
-// indices than their consumers and the grid fits one block per CU, so every
-// spin terminates; spins are still bounded and set E.sync[1] on a timeout.
+// advanced by phase C), so they are never reset.  Producers have lower block
+// indices than their consumers in every layout (phase A: pi(s') -> target
+// critics -> critics; phase C: critics -> pi; fused: update tiles first), so
+// in-order dispatch gives every spinning consumer resident producers; spins are
+// still bounded (E.spin_limit) and set E.sync[1] on a timeout, which the host
+// API turns into an error (sac_engine_read_status, SacEngine._poll_status).
 enum HandKind { HK_PI = 0, HK_T1 = 1, HK_T2 = 2, HK_C1 = 3, HK_C2 = 4, HK_COUNT = 5 };
 // SYNC_STAGED (u64 at words 4-5): step whose phase A last used a staged batch record
 enum SyncWord { SYNC_EPOCH = 0, SYNC_TIMEOUT = 1, SYNC_STAGED = 4, SYNC_DDONE = 16, SYNC_BDONE = 32, SYNC_CDONE = 64, SYNC_FLAGS = 128 };
@@ -1120,7 +1124,7 @@ __device__ __forceinline__ void hand_wait(const AS_C EngineDev& E, int kind, int
   if (threadIdx.x == 0) {
     uint32_t* f = (uint32_t*)hand_flag(E, kind, rbi);
     for (int it = 0; __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != ep; ++it) {
-      if (it > (1 << 22)) {  // ~0.3 s: a producer never ran; flag the error, do not hang the GPU
+      if (it > E.spin_limit) {  // ~0.3 s: a producer never ran; flag the error, do not hang the GPU
         __hip_atomic_store((uint32_t*)GP(uint32_t, E.sync) + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         break;
       }
@@ -1139,7 +1143,7 @@ __device__ __forceinline__ void hand_wait2(const AS_C EngineDev& E, int k1, int 
       const uint32_t a = __hip_atomic_load(f1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       const uint32_t b = __hip_atomic_load(f2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (a == ep && b == ep) break;
-      if (it > (1 << 22)) {
+      if (it > E.spin_limit) {
         __hip_atomic_store((uint32_t*)GP(uint32_t, E.sync) + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         break;
       }
@@ -1154,7 +1158,7 @@ __device__ __forceinline__ void count_wait(const AS_C EngineDev& E, int word, ui
   if (threadIdx.x == 0) {
     uint32_t* c = (uint32_t*)E.sync + word;
     for (int it = 0; __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target; ++it) {
-      if (it > (1 << 22)) {
+      if (it > E.spin_limit) {
         __hip_atomic_store((uint32_t*)GP(uint32_t, E.sync) + SYNC_TIMEOUT, 1u, __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
         break;
@@ -1189,7 +1193,7 @@ __device__ __forceinline__ float gran_get(const AS_C EngineDev& E, const AS_G ui
   for (int it = 0;; ++it) {
     x = __hip_atomic_load((uint64_t*)g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if ((uint32_t)(x >> 32) == ep) break;
-    if (it > (1 << 22)) {
+    if (it > E.spin_limit) {
       __hip_atomic_store((uint32_t*)GP(uint32_t, E.sync) + SYNC_TIMEOUT, 1u, __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_AGENT);
       break;
@@ -1277,6 +1281,7 @@ __device__ __forceinline__ void stage_next_batch(const AS_C EngineDev& E, const 
     hdr[1] = (uint64_t)rb_size;
     hdr[2] = (uint64_t)rb_pos;
     hdr[3] = (uint64_t)(uintptr_t)rb.obs;
+    hdr[4] = (uint64_t)GPC(int64_t, rb.state)[2];  // push generation: any push / clear() invalidates
   }
 }
 
@@ -1300,20 +1305,18 @@ __device__ __forceinline__ void target_critic_body(const EngineDev* __restrict__
   const int tid = threadIdx.x;
   int bid = blockIdx.x;
   if (WITH_D) {
-    // grid order = dispatch order: pi(s') roles first (the critical path), then
-    // the phase D blocks they wait for, then the other roles
-    if (bid >= E.nrt) {
-      if (bid <= E.nrt + E.nD) {
-        const int parD = (int)((*GPC(uint64_t, E.rng_step) - 1) & 1);  // the step phase C just closed
-        if (bid < E.nrt + E.nD)
-          dw_adam_tile<T, SAC_THREADS, true>(E, E.tilesD + (bid - E.nrt), false, parD, lds);
-        else
-          alpha_and_losses(E, parD, lds);
-        count_done((uint32_t*)E.sync + SYNC_DDONE);
-        return;
-      }
-      bid -= E.nD + 1;
+    // grid order = dispatch order: the phase D blocks (producers of pi's new
+    // weights) first, then the roles; the pi roles wait for D's count
+    if (bid <= E.nD) {
+      const int parD = (int)((*GPC(uint64_t, E.rng_step) - 1) & 1);  // the step phase C just closed
+      if (bid < E.nD)
+        dw_adam_tile<T, SAC_THREADS, true>(E, E.tilesD + bid, false, parD, lds);
+      else
+        alpha_and_losses(E, parD, lds);
+      count_done((uint32_t*)E.sync + SYNC_DDONE);
+      return;
     }
+    bid -= E.nD + 1;
   }
   int rbi, role;
   if (ROLES) {
@@ -1447,7 +1450,7 @@ __device__ __forceinline__ void target_critic_body(const EngineDev* __restrict__
       }
     }
     staged = hdr[0] == step && hdr[1] == (uint64_t)rb_size && hdr[2] == (uint64_t)rb_pos &&
-             hdr[3] == (uint64_t)(uintptr_t)rb.obs;
+             hdr[3] == (uint64_t)(uintptr_t)rb.obs && hdr[4] == (uint64_t)GPC(int64_t, rb.state)[2];
   }
   if (staged && rbi == 0 && (!ROLES || role == 0) && tid == 0)
     *(AS_G uint64_t*)(GP(uint32_t, E.sync) + 4) = step;  // SYNC_STAGED: the staged path ran (tests)
@@ -1740,8 +1743,12 @@ __device__ __forceinline__ void actor_body(const EngineDev* __restrict__ Ep, int
   const int tid = threadIdx.x;
   int rbi, role;
   if (ROLES) {
+    // producers first: block groups 0 / 1 are the critic roles (1 / 2), group
+    // 2 the pi role (0) that consumes their granules.  In-order dispatch then
+    // guarantees that a spinning consumer's producers already hold a CU.
     rbi = bid % E.nrt;
-    role = bid / E.nrt;
+    const int grp = bid / E.nrt;
+    role = grp == 2 ? 0 : grp + 1;
   } else {
     if (bid % E.xs) return;  // XCD placement: see EngineDev::xs
     rbi = bid / E.xs;

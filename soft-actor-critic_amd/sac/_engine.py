@@ -27,6 +27,11 @@ class EngineError(RuntimeError):
     pass
 
 
+class HandoffTimeout(EngineError):
+    """A workgroup hand-off inside a phase kernel gave up waiting: the affected
+    gradient steps computed on stale inputs and the learner state is invalid."""
+
+
 c_int32_p = ctypes.POINTER(ctypes.c_int32)
 
 
@@ -80,6 +85,10 @@ SIGNATURES = {
                           + [ctypes.c_void_p] * 6),
     "sac_replay_sample_indices": (ctypes.c_int, [ctypes.POINTER(ReplayDesc), ctypes.c_int32, ctypes.c_uint64,
                                                  ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p]),
+    "sac_replay_sample_gather": (ctypes.c_int, [ctypes.POINTER(ReplayDesc), ctypes.c_int32, ctypes.c_uint64,
+                                                ctypes.c_uint64] + [ctypes.c_void_p] * 7),
+    "sac_engine_read_status": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    "sac_engine_clear_status": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
     "sac_engine_time_phases": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ReplayDesc), ctypes.c_int32,
                                               ctypes.POINTER(ctypes.c_float), ctypes.c_void_p]),
     "sac_phase_kernel_name": (ctypes.c_char_p, [ctypes.c_int32]),

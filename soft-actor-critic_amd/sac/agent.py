@@ -10,7 +10,9 @@ the same attributes and methods.  What changes is underneath:
 * ``select_action`` (agent.py:149-156) runs the policy head in a HIP kernel.
 
 Extra (optional) config keys, all under ``train``:
-    precision: 'bf16' (default; bf16 MFMA products, fp32 accumulate/master) | 'fp32'
+    precision: 'fp32' (default; exact-fp32 MFMA products, the reference's arithmetic) |
+               'bf16' (opt-in: bf16 MFMA products, fp32 accumulate and master weights;
+               loss deviation from the fp32 reference up to ~2e-3 rel)
     rng:       'device' (default; Philox/Feistel on the GPU, graph-replayable) |
                'reference' (Python ``random.sample`` indices + torch eps draws,
                the reference's RNG consumption)
@@ -58,6 +60,21 @@ def due_updates(old_steps: int, new_steps: int, update_frequency: int, gradient_
     return (new_steps // update_frequency - old_steps // update_frequency) * gradient_steps
 
 
+def due_updates_gated(old_steps: int, new_steps: int, len_before: int, capacity: int, warming_steps: int,
+                      update_frequency: int, gradient_steps: int) -> int:
+    """``due_updates`` restricted to the env steps at which the reference's
+    ``can_update()`` already holds (agent.py:159-164, 361-362): env step t
+    (old_steps < t <= new_steps) pushes the (t - old_steps)-th of this vector
+    step's transitions, after which the buffer holds min(capacity, len_before +
+    t - old_steps) rows; it updates only if that is >= warming_steps."""
+    if warming_steps > capacity or new_steps <= old_steps:
+        return 0
+    first = old_steps + max(1, warming_steps - len_before)  # first env step with can_update() true
+    if first > new_steps:
+        return 0
+    return due_updates(first - 1, new_steps, update_frequency, gradient_steps)
+
+
 class SAC:
     def __init__(self, env, config: dict):
         self.env = env
@@ -76,7 +93,7 @@ class SAC:
         sac_cfg = config["sac"]
         self._auto = bool(sac_cfg["auto_entropy_tuning"])
         tr = config["train"]
-        self.precision = tr.get("precision", "bf16")
+        self.precision = tr.get("precision", "fp32")
         self.rng_mode = tr.get("rng", "device")
         self.graph_chunk = int(tr.get("graph_chunk", 32))
         self.engine: Optional[SacEngine] = None
@@ -323,6 +340,8 @@ class SAC:
             if print_rewards:
                 print(f"Episode {episode}, Return: {episode_return:.2f}, "
                       f"Average Return(last 100 episodes): {avg_return:.2f}")
+        if self.engine is not None:
+            self.engine.check()
         metrics = {"total_episodes": total_episodes, "best_avg_return": best_avg_return,
                    "final_avg_return": avg_return}
         if active_logger is not None:
@@ -382,11 +401,13 @@ class SAC:
             actions = self.select_actions(obs)
             next_obs, rewards, terminated, truncated, info = env.step(actions)
             dones = np.logical_or(terminated, truncated)
+            len_before = len(self.replay_buffer)
             self.store_transitions(obs, actions, rewards, info["final_obs"], dones)
             old = total_steps
             total_steps += N
-            due = due_updates(old, total_steps, update_every, n_grad)
-            if due and self.can_update():
+            due = due_updates_gated(old, total_steps, len_before, self.replay_buffer.capacity,
+                                    tr["warming_steps"], update_every, n_grad)
+            if self.can_update() and due:
                 self._run_updates(due)
                 grad_steps += due
             ep_ret += rewards
@@ -405,6 +426,8 @@ class SAC:
                 ep_ret[i] = 0.0
                 ep_len[i] = 0
             obs = next_obs
+        if self.engine is not None:
+            self.engine.check()  # a timed-out hand-off invalidates the run: raise, do not report it
         metrics = {"total_episodes": total_episodes, "best_avg_return": best_avg_return,
                    "final_avg_return": avg_return, "total_env_steps": total_steps, "gradient_steps": grad_steps}
         if active_logger is not None:
@@ -497,7 +520,10 @@ class SAC:
                 st["step"] = torch.tensor(float(steps[i]))
 
     def save_agent(self, filepath: str) -> None:
-        """Same checkpoint dict as the reference (agent.py:521-536)."""
+        """Same checkpoint dict as the reference (agent.py:521-536).  Raises
+        HandoffTimeout instead of saving a state an invalid step produced."""
+        if self.engine is not None:
+            self.engine.check()
         self._export_steps()
         ckpt = {
             "policy_net_state_dict": self.policy_net.state_dict(),

@@ -58,7 +58,7 @@ def _views(flat: torch.Tensor, like: Sequence[torch.Tensor]) -> List[torch.Tenso
 class SacEngine:
     def __init__(self, policy_net, q_net1, q_net2, q_net1_target, q_net2_target, *, batch_size: int,
                  gamma: float, tau: float, actor_lr: float, critic_lr: float, alpha_lr: float,
-                 alpha: float, auto_entropy_tuning: bool, device, precision: str = "bf16",
+                 alpha: float, auto_entropy_tuning: bool, device, precision: str = "fp32",
                  seed: int = 0, betas=(0.9, 0.999), eps: float = 1e-8):
         self.device = torch.device(device)
         E.require_gpu(self.device)
@@ -128,6 +128,12 @@ class SacEngine:
         E.check(self.lib.sac_engine_create(ctypes.byref(cfg), ctypes.byref(bufs), self._stream(), ctypes.byref(h)))
         self.handle = h
         self.steps_done = 0
+        # lazy hand-off status: an async D2H copy of the engine's status words
+        # into pinned memory every STATUS_EVERY train calls, checked when it has
+        # landed (never a per-step synchronisation); losses()/check() force it
+        self._status = torch.zeros(2, dtype=torch.int32, pin_memory=True)
+        self._status_ev: Optional[torch.cuda.Event] = None
+        self._calls = 0
         self.lib.sac_engine_uses_roles.argtypes = [ctypes.c_void_p]
         self.roles = bool(self.lib.sac_engine_uses_roles(h))
         self.fused = int(self.lib.sac_engine_phase_layout(h))  # 1: D in the next A's launch, 2: + B in C's
@@ -178,6 +184,46 @@ class SacEngine:
             v.copy_(snap[k])
         self.sync_params()
 
+    # ------------------------------------------------------------------ status
+    STATUS_EVERY = 16
+
+    def _raise_timeout(self) -> None:
+        raise E.HandoffTimeout(
+            "a workgroup hand-off of the SAC phase kernels timed out (the GPU was too contended for the "
+            "role-split step to make progress): the gradient steps since the last good status are invalid")
+
+    def _poll_status(self, block: bool = False) -> None:
+        """Check the last status copy if it has landed (block: wait for a fresh one)."""
+        if block:
+            self._issue_status()
+        ev = self._status_ev
+        if ev is None:
+            return
+        if block:
+            ev.synchronize()
+        elif not ev.query():
+            return
+        self._status_ev = None
+        if int(self._status[1]) != 0:
+            self._raise_timeout()
+
+    def _issue_status(self) -> None:
+        E.check(self.lib.sac_engine_read_status(self.handle, ctypes.c_void_p(self._status.data_ptr()),
+                                                self._stream()))
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(self.device))
+        self._status_ev = ev
+
+    def _after_launch(self) -> None:
+        self._calls += 1
+        if self._status_ev is None and self._calls % self.STATUS_EVERY == 0:
+            self._issue_status()
+
+    def clear_status(self) -> None:
+        """Reset the hand-off timeout flag (after handling a HandoffTimeout)."""
+        self._status_ev = None
+        E.check(self.lib.sac_engine_clear_status(self.handle, self._stream()))
+
     # ------------------------------------------------------------------ compute
     def train(self, replay, n_steps: int = 1, indices: Optional[torch.Tensor] = None,
               eps: Optional[torch.Tensor] = None) -> None:
@@ -189,18 +235,23 @@ class SacEngine:
             indices = indices.to(self.device, torch.int32).contiguous()
         if eps is not None:
             eps = eps.to(self.device, torch.float32).contiguous()
+        self._poll_status()
         E.check(self.lib.sac_engine_train(self.handle, ctypes.byref(desc), int(n_steps), E.ptr(indices),
                                           E.ptr(eps), self._stream()))
         self._keep = (indices, eps)
         self.steps_done += n_steps
+        self._after_launch()
 
     def train_graph(self, replay, n_steps: int, chunk: int = 32) -> None:
         if len(replay) < self.batch:
             replay._check(self.batch)
         desc = replay.desc
+        self._poll_status()
         E.check(self.lib.sac_engine_train_graph(self.handle, ctypes.byref(desc), int(n_steps), int(chunk),
                                                 self._stream()))
         self.steps_done += n_steps
+        if n_steps:
+            self._after_launch()
 
     def policy_act(self, obs: torch.Tensor, eps: Optional[torch.Tensor] = None, want_log_pi: bool = False):
         obs = obs.to(self.device, torch.float32).contiguous()
@@ -224,11 +275,13 @@ class SacEngine:
 
     # ------------------------------------------------------------------ readback (syncs)
     def check(self) -> None:
-        """Raise EngineError if an in-launch hand-off of the phase kernels timed out."""
-        E.check(self.lib.sac_engine_check(self.handle, self._stream()))
+        """Raise HandoffTimeout if an in-launch hand-off of the phase kernels timed out."""
+        self._poll_status(block=True)
 
     def losses(self) -> List[float]:
-        """[L_Q1, L_Q2, L_pi, L_alpha] of the last step (NaN L_alpha when fixed)."""
+        """[L_Q1, L_Q2, L_pi, L_alpha] of the last step (NaN L_alpha when fixed).
+        Raises HandoffTimeout if any step since the last check was invalid."""
+        self._poll_status(block=True)
         return self.stats[:4].double().cpu().tolist()
 
     def last_targets(self) -> torch.Tensor:

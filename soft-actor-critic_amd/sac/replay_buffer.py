@@ -61,7 +61,7 @@ class ReplayBuffer:
         self.rew = torch.zeros(cap, **f32)
         self.next_obs = torch.zeros(cap, self.obs_dim, **f32)
         self.done = torch.zeros(cap, **f32)
-        self.state = torch.zeros(2, dtype=torch.int64, device=dev)
+        self.state = torch.zeros(3, dtype=torch.int64, device=dev)  # size, next slot, push generation
         self.row_width = 2 * self.obs_dim + self.act_dim + 2
         self._desc = E.ReplayDesc(
             self.obs.data_ptr(), self.act.data_ptr(), self.rew.data_ptr(), self.next_obs.data_ptr(),
@@ -208,7 +208,10 @@ class ReplayBuffer:
         self._staged.clear()
         self._n_staged = 0
         if self._alloc_done:
-            self.state.zero_()
+            # size and write slot back to 0; the push generation moves on, so a
+            # batch the engine staged before the clear is never used after it
+            self.state[:2].zero_()
+            self.state[2:].add_(1)
 
 
 def ctypes_ref(desc):

@@ -106,3 +106,28 @@ def test_bench_flops_match_survey():
         assert total == pytest.approx(v, rel=1e-4), k
         # per-phase counts (roofline of each kernel) add up to the step's F_alg
         assert sum(phases) == total
+
+
+def test_due_updates_gated_matches_the_reference_per_step_loop():
+    """The vectorised driver's gradient-step count for one vector step of N
+    env steps equals the reference loop's (agent.py:355-369: push, then
+    can_update() and t % update_frequency) counted env step by env step,
+    including vector steps that cross the warm-up boundary, a full ring and
+    warming_steps > capacity (never updates)."""
+    import itertools
+
+    from sac.agent import due_updates_gated
+
+    for N, freq, grad, warm, cap in itertools.product((1, 3, 16), (1, 2, 5), (1, 3), (0, 7, 64, 100), (50, 1000)):
+        length = total = 0
+        for _ in range(40):
+            want = 0
+            ln = length
+            for t in range(total + 1, total + N + 1):
+                ln = min(cap, ln + 1)
+                if warm <= cap and ln >= warm and t % freq == 0:
+                    want += grad
+            got = due_updates_gated(total, total + N, length, cap, warm, freq, grad)
+            assert got == want, (N, freq, grad, warm, cap, total)
+            length = min(cap, length + N)
+            total += N

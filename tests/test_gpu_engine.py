@@ -91,7 +91,7 @@ def test_device_sampler_equals_host(lib, size, batch):
 
     f = lib.sac_debug_sample_indices_host
     f.argtypes = [ctypes.c_int64, ctypes.c_int32, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_void_p]
-    state = torch.tensor([size, 0], dtype=torch.int64, device=DEV)
+    state = torch.tensor([size, 0, 0], dtype=torch.int64, device=DEV)
     desc = E.ReplayDesc(0, 0, 0, 0, 0, size, 1, 1, state.data_ptr())
     out = torch.empty(batch, dtype=torch.int32, device=DEV)
     for step in (0, 5, 2**33 + 1):
@@ -309,3 +309,159 @@ def test_fused_launches_equal_four_launches(precision, layout, monkeypatch):
         out[fuse]["stats"] = eng.stats.clone()
     for k in out[layout]:
         assert torch.equal(out[layout][k], out["0"][k]), k
+
+
+# ---------------------------------------------------------------- hand-off status (round 2)
+def test_handoff_timeout_raises_through_the_api(lib):
+    """A hand-off spin bound of 0 polls makes every role-split consumer that
+    does not find its producer's granules at once give up: the step is invalid,
+    the device flag is set, and the Python API (losses(), check(), save_agent)
+    raises HandoffTimeout instead of returning the invalid state.  After
+    clear_status() and the default bound the engine trains normally again."""
+    from sac import _engine as E
+
+    eng, rb, c = _engine("c2", "fp32", capacity=5000)
+    assert eng.roles
+    eng.train(rb, 2)
+    eng.check()
+    f = lib.sac_engine_debug_set_spin_limit
+    f.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p]
+    E.check(f(eng.handle, 0, eng._stream()))
+    eng.train(rb, 4)
+    with pytest.raises(E.HandoffTimeout):
+        eng.losses()
+    with pytest.raises(RuntimeError):  # HandoffTimeout is a RuntimeError
+        eng.check()
+    E.check(f(eng.handle, 1 << 22, eng._stream()))
+    eng.clear_status()
+    eng.train(rb, 3)
+    eng.check()
+    assert all(np.isfinite(eng.losses()[:3]))
+
+
+def test_concurrent_engines_on_streams_match_serial():
+    """Two learners on two HIP streams at once (the multi-learner packing that
+    contends for CUs) give the same bits as each run alone, and no hand-off
+    times out (producer roles sit on the lowest block ids of every launch)."""
+    runs = {}
+    for mode in ("serial", "concurrent"):
+        e1, rb1, _ = _engine("c2", "fp32", seed=1, capacity=5000)
+        e2, rb2, _ = _engine("c2", "fp32", seed=2, capacity=5000)
+        s1, s2 = torch.cuda.Stream(DEV), torch.cuda.Stream(DEV)
+        torch.cuda.synchronize()
+        if mode == "serial":
+            with torch.cuda.stream(s1):
+                e1.train_graph(rb1, 40, chunk=10)
+            s1.synchronize()
+            with torch.cuda.stream(s2):
+                e2.train_graph(rb2, 40, chunk=10)
+            s2.synchronize()
+        else:
+            for _ in range(4):
+                with torch.cuda.stream(s1):
+                    e1.train_graph(rb1, 10, chunk=10)
+                with torch.cuda.stream(s2):
+                    e2.train_graph(rb2, 10, chunk=10)
+            torch.cuda.synchronize()
+        e1.check()
+        e2.check()
+        runs[mode] = [{k: v.clone() for k, v in e.state_tensors().items()} for e in (e1, e2)]
+    for i in range(2):
+        for k in runs["serial"][i]:
+            assert torch.equal(runs["serial"][i][k], runs["concurrent"][i][k]), (i, k)
+
+
+def test_clear_and_refill_invalidates_the_staged_batch(monkeypatch):
+    """ReplayBuffer.clear() followed by a refill to the same (size, write slot)
+    must not let phase A use the batch phase C staged from the old rows: the
+    push generation in the replay state differs, so phase A gathers the new
+    rows (same bits as a run with staging off)."""
+    out = {}
+    for stage in ("1", "0"):
+        monkeypatch.setenv("SAC_STAGE", stage)
+        eng, rb, c = _engine("c2", "fp32", capacity=4096)
+        eng.train(rb, 2)  # phase C of step 2 staged step 3's batch from the old rows
+        g = np.random.default_rng(9)
+        rb.clear()
+        n = 4096  # refill to the same size; the write slot wraps back to 0 as before
+        rb.push_batch(g.standard_normal((n, c["obs"]), dtype=np.float32), g.uniform(-1, 1, (n, c["act"])),
+                      g.standard_normal(n), g.standard_normal((n, c["obs"]), dtype=np.float32), g.random(n) < 0.1)
+        assert int(rb.state[0]) == 4096 and int(rb.state[1]) == 0
+        eng.train(rb, 2)
+        eng.check()
+        out[stage] = {k: v.clone() for k, v in eng.state_tensors().items()}
+    for k in out["1"]:
+        assert torch.equal(out["1"][k], out["0"][k]), k
+
+
+# ---------------------------------------------------------------- gather kernel (round 2)
+@pytest.mark.parametrize("obs,act", [(24, 4), (5, 2), (32, 2)])
+def test_sample_gather_equals_sampler_plus_gather(lib, obs, act):
+    """sac_replay_sample_gather (sampler + row-vectorised gather in one kernel)
+    returns the sampler's indices and exactly the rows sac_replay_gather
+    returns for them, for 16-B-aligned rows (obs 24/32) and scalar rows (5/2),
+    on a wrapped ring."""
+    from sac import _engine as E
+    from sac.replay_buffer import ReplayBuffer
+
+    cap = 3000
+    rb = ReplayBuffer(cap, device=DEV, obs_dim=obs, act_dim=act)
+    g = np.random.default_rng(0)
+    n = 4100  # wraps: the oldest row sits at slot 1100
+    rb.push_batch(g.standard_normal((n, obs), dtype=np.float32), g.uniform(-1, 1, (n, act)).astype(np.float32),
+                  g.standard_normal(n), g.standard_normal((n, obs), dtype=np.float32), g.random(n) < 0.1)
+    for B in (1, 64, 100, 2999):
+        f32 = dict(dtype=torch.float32, device=DEV)
+        out = [torch.empty(B, obs, **f32), torch.empty(B, act, **f32), torch.empty(B, **f32),
+               torch.empty(B, obs, **f32), torch.empty(B, **f32)]
+        idx = torch.empty(B, dtype=torch.int32, device=DEV)
+        desc = rb.desc
+        E.check(lib.sac_replay_sample_gather(ctypes.byref(desc), B, 5, 17, E.ptr(idx), *[E.ptr(t) for t in out],
+                                             E.stream_handle(DEV)))
+        ref_idx = torch.empty(B, dtype=torch.int32, device=DEV)
+        E.check(lib.sac_replay_sample_indices(ctypes.byref(desc), B, 5, 17, E.ptr(ref_idx), E.stream_handle(DEV)))
+        assert torch.equal(idx, ref_idx)
+        t = rb.gather(idx.cpu().numpy())
+        for a_, b_ in zip(out, t):
+            assert torch.equal(a_, b_)
+        # and against the host copy of the storage, by ring slot
+        li = idx.cpu().numpy().astype(np.int64)
+        slot = (int(rb.state[1]) + li) % cap
+        assert np.array_equal(out[0].cpu().numpy(), rb.obs.cpu().numpy()[slot])
+        assert np.array_equal(out[4].cpu().numpy(), rb.done.cpu().numpy()[slot])
+
+
+def test_gather_with_replacement_past_capacity(lib):
+    """The bandwidth leg of bench.py gathers B = 1,048,576 rows with replacement
+    (B > the 1e6-row buffer): the gather is exact at that size too."""
+    from sac import _engine as E
+    from sac.replay_buffer import ReplayBuffer
+
+    cap, obs, act = 1_000_000, 24, 4
+    rb = ReplayBuffer(cap, device=DEV, obs_dim=obs, act_dim=act)
+    n = cap + 12_345
+    gen = torch.Generator(device=DEV).manual_seed(0)
+    rows = torch.randn(n, 2 * obs + act + 2, device=DEV, generator=gen)
+    rb.push_batch(rows[:, :obs], rows[:, obs:obs + act], rows[:, obs + act], rows[:, obs + act + 1:2 * obs + act + 1],
+                  rows[:, -1] > 0)
+    B = 1 << 20
+    idx = torch.randint(0, cap, (B,), device=DEV, dtype=torch.int32, generator=gen)
+    t = rb.gather(idx)
+    slot = (idx.long() + int(rb.state[1])) % cap
+    assert torch.equal(t.state, rb.obs[slot]) and torch.equal(t.next_state, rb.next_obs[slot])
+    assert torch.equal(t.action, rb.act[slot]) and torch.equal(t.reward, rb.rew[slot])
+    assert torch.equal(t.done, rb.done[slot])
+
+
+def test_c3_full_size_properties():
+    """C3 at full size (1e6-row buffer, B = 4096, fp32 parity mode, device
+    sampler): 60 graph-replayed steps stay finite with no hand-off timeout, and
+    the in-step sampler draws the exported sampler's distinct rows."""
+    eng, rb, c = _engine("c3", "fp32")
+    assert len(rb) == 1_000_000
+    eng.train_graph(rb, 60, chunk=20)
+    eng.check()
+    losses = eng.losses()
+    assert all(np.isfinite(losses)), losses
+    assert np.all(np.isfinite(eng.last_targets().cpu().numpy()))
+    assert int(eng.rng_step.item()) == 60

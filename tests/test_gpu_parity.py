@@ -102,21 +102,32 @@ def test_constant_reward_y_is_r_on_gpu():
     assert np.array_equal(y, np.ones_like(y))
 
 
+BENCH_NETS = {"policy": "pi", "q1": "q1", "q2": "q2", "q1t": "q1t", "q2t": "q2t"}
+
+
 @pytest.mark.parametrize("precision", ["fp32", "bf16"])
-def test_wide_obs_donkey_matches_oracle(precision):
-    """C4' (the reference Donkey env's real observation width: 32-D latent + 2x20
-    command history, x3 frame stack = 216), act 2, [256,256], B=256.
-    No golden fixture exists at this width (parity unpinned by the reference), so
-    the engine is checked against the fixture-pinned oracle on seeded batches with
-    injected indices and eps, 3 steps, with the tolerances above."""
+@pytest.mark.parametrize("cfg,capacity,steps", [("c4", 4096, 3), ("c4w", 2048, 3), ("c3", 12_288, 2)])
+def test_baseline_config_matches_oracle(cfg, capacity, steps, precision):
+    """The BASELINE.json configs the fixtures do not cover, against the
+    fixture-pinned oracle on seeded batches with injected indices and eps:
+      c4  DonkeyVae as BASELINE.json states it: obs 32, act 2, [256,256], B 256;
+      c4w the reference Donkey env's real observation width (32-D latent + 2x20
+          command history, x3 frame stack = 216; SURVEY §7.8), act 2, B 256;
+      c3  BipedalWalker at B = 4096 (256 row tiles: the non-role-split phase
+          kernels and the 4-chunk update staging, a different code path).
+    No golden fixture exists at these shapes (parity unpinned by the reference
+    itself; the oracle is pinned by the 8 reference fixtures).  Checks, per
+    step: the four losses, y and log pi, every post-step parameter of the five
+    networks and log alpha, with this file's tolerances."""
     import bench
 
-    c = dict(bench.CONFIGS["c4w"])
-    bench.CONFIGS["c4w"] = dict(c, capacity=2048)
+    c = dict(bench.CONFIGS[cfg])
+    bench.CONFIGS[cfg] = dict(c, capacity=capacity)
     try:
-        eng, rb, cc = bench.build_engine("c4w", precision, 3, torch.device("cuda", 0))
+        eng, rb, cc = bench.build_engine(cfg, precision, 3, torch.device("cuda", 0))
     finally:
-        bench.CONFIGS["c4w"] = c
+        bench.CONFIGS[cfg] = c
+    assert eng.roles == (cfg != "c3")
     B, A = cc["batch"], cc["act"]
     sds = {k: {kk: v.detach().cpu().numpy().copy() for kk, v in m.state_dict().items()} for k, m in eng.nets.items()}
     hp = O.SacHyper(alpha=0.1, auto_entropy_tuning=True)  # bench.build_engine's hyper-parameters
@@ -125,7 +136,9 @@ def test_wide_obs_donkey_matches_oracle(precision):
     rows = {k: getattr(rb, k).cpu().numpy() for k in ("obs", "act", "rew", "next_obs", "done")}
     g = np.random.default_rng(11)
     rtol = 1e-4 if precision == "fp32" else 2e-3
-    for k in range(3):
+    lrs = {"policy": hp.actor_lr, "q1": hp.critic_lr, "q2": hp.critic_lr, "q1t": hp.critic_lr * hp.tau,
+           "q2t": hp.critic_lr * hp.tau}
+    for k in range(1, steps + 1):
         idx = g.choice(len(rb), size=B, replace=False).astype(np.int32)
         et = g.standard_normal((B, A)).astype(np.float32)
         ea = g.standard_normal((B, A)).astype(np.float32)
@@ -137,5 +150,29 @@ def test_wide_obs_donkey_matches_oracle(precision):
         got = eng.losses()
         floor = float(np.mean(np.abs(st.alpha * ref["log_pi"])) + np.mean(np.abs(ref["y"]))) + 1e-6
         for i, (gv, w) in enumerate(zip(got, ref["losses"])):
-            assert _loss_ok(gv, w, floor if i == 2 else 1e-3, rtol), (precision, k, i, gv, w)
+            assert _loss_ok(gv, w, floor if i == 2 else 1e-3, rtol), (cfg, precision, k, i, gv, w)
+        y = eng.last_targets().cpu().numpy()
+        lp = eng.last_log_pi().cpu().numpy()
+        if precision == "fp32":
+            np.testing.assert_allclose(y, ref["y"], rtol=1e-4, atol=1e-4)
+            np.testing.assert_allclose(lp, ref["log_pi"], rtol=1e-4, atol=1e-4)
+        else:
+            for gv, want in ((y, ref["y"]), (lp, ref["log_pi"])):
+                scale = np.abs(want).mean() + 1.0
+                assert np.abs(gv - want).mean() <= 1e-2 * scale, (cfg, k, np.abs(gv - want).mean(), scale)
+        for key, ek in BENCH_NETS.items():
+            mine = {kk: v.detach().cpu().numpy() for kk, v in eng.nets[ek].state_dict().items()}
+            lr = lrs[key] * (k if key in ("policy", "q1", "q2") else k * (k + 1) / 2)
+            ds = []
+            for pk, want in _oracle_net(st, key).state_dict().items():
+                d = np.abs(mine[pk] - want)
+                assert d.max() <= 2 * lr + 1e-5, (cfg, precision, k, key, pk, d.max())
+                if precision == "fp32":
+                    assert np.mean(d <= 1e-6) >= 0.995, (cfg, k, key, pk, np.mean(d <= 1e-6))
+                ds.append(d.ravel())
+            if precision == "bf16":
+                d = np.concatenate(ds)
+                assert d.mean() <= 0.05 * lr + 1e-7, (cfg, k, key, d.mean())
+        la = float(eng.alpha_state[0].item())
+        assert abs(la - st.log_alpha) <= (1e-7 if precision == "fp32" else 1e-5), (la, st.log_alpha)
     eng.check()

@@ -117,8 +117,12 @@ def test_vectorized_loop_many_envs_runs_and_counts():
     m = agent.run_vectorized_training_loop(16 * 20)
     torch.cuda.synchronize()
     assert m["total_env_steps"] == 320 and len(agent.replay_buffer) == 320
-    # updates only once the buffer holds warming_steps rows: from vector step 4 on (64 rows)
-    assert m["gradient_steps"] == sum(3 * 8 for _ in range(4, 21))
+    # the reference loop (agent.py:355-369) at env step t: push, then 3 gradient
+    # steps if len(buffer) >= 64 and t % 2 == 0 -- counted per env step, also
+    # inside the vector step that crosses the warm-up boundary (t = 49..64)
+    want = sum(3 for t in range(1, 321) if t >= 64 and t % 2 == 0)
+    assert want == 387
+    assert m["gradient_steps"] == want
     assert agent.engine.steps_done == m["gradient_steps"]
     agent.engine.check()
     assert all(np.isfinite(agent.engine.losses()[:3]))

@@ -49,14 +49,22 @@ def counter_avg(db: sqlite3.Connection, counter: str):
 
 
 def main():
-    rnd = sys.argv[1] if len(sys.argv) > 1 else "r01"
-    src = sys.argv[2] if len(sys.argv) > 2 else os.path.join(ROOT, "gpurun_out", "prof")
+    import argparse
+
+    ap = argparse.ArgumentParser()
+    ap.add_argument("round", nargs="?", default="r01")
+    ap.add_argument("src", nargs="?", default=os.path.join(ROOT, "gpurun_out", "prof"))
+    ap.add_argument("--tag", default="", help="suffix of the output files (e.g. _fp32, _gather)")
+    ap.add_argument("--config", default="c2", help="bench config the profile ran (or 'gather')")
+    ap.add_argument("--precision", default="bf16")
+    a = ap.parse_args()
+    rnd, src, tag = a.round, a.src, a.tag
     dst = os.path.join(ROOT, "profiles")
     os.makedirs(dst, exist_ok=True)
 
     kt = one_db(os.path.join(src, "kt", "*.db"))
     rows = list(kt.execute("select name, total_calls, total_duration, average, percentage from top_kernels"))
-    with open(os.path.join(dst, f"{rnd}_kernel_stats.csv"), "w", newline="") as f:
+    with open(os.path.join(dst, f"{rnd}_kernel_stats{tag}.csv"), "w", newline="") as f:
         w = csv.writer(f)
         w.writerow(["kernel", "calls", "total_us", "avg_us", "percent"])
         for name, calls, tot, avg, pct in rows:
@@ -65,7 +73,8 @@ def main():
     fetch = counter_avg(one_db(os.path.join(src, "fetch", "*.db")), "FETCH_SIZE")
     write = counter_avg(one_db(os.path.join(src, "write", "*.db")), "WRITE_SIZE")
     durations = {short(n): avg for n, _, _, avg, _ in rows}
-    summary = {"source": "rocprofv3 --kernel-trace --stats; separate --pmc FETCH_SIZE / --pmc WRITE_SIZE passes",
+    summary = {"config": a.config, "precision": a.precision,
+               "source": "rocprofv3 --kernel-trace --stats; separate --pmc FETCH_SIZE / --pmc WRITE_SIZE passes",
                "correction": "fetch_bytes = 2 x FETCH_SIZE KiB x 1024 (gfx950 wide-read undercount); "
                              "write_bytes = WRITE_SIZE KiB x 1024",
                "kernels": {}}
@@ -77,7 +86,7 @@ def main():
         summary["kernels"][k] = {"launches_sampled": fetch.get(k, (0, 0))[0], "fetch_bytes": round(fb),
                                  "write_bytes": round(wb), "hbm_bytes_per_launch": round(fb + wb),
                                  "avg_us_kernel_trace": durations.get(k)}
-    with open(os.path.join(dst, f"{rnd}_pmc.json"), "w") as f:
+    with open(os.path.join(dst, f"{rnd}_pmc{tag}.json"), "w") as f:
         json.dump(summary, f, indent=1)
     print(json.dumps(summary, indent=1))
 

@@ -72,7 +72,7 @@ names.update({33: "B waited", 20: "HC8 layer entry", 21: "HC8 MFMA done (wave 0)
 names.update({60: "END", 61: "END", 62: "END", 63: "END"})
 PH = {"A": list(range(0, 17)) + [20, 21, 22, 23, 56, 57, 59, 60],  # 20-23: free for DSTAMP probes
       "C": list(range(32, 40)) + [61], "B": [48, 49, 50, 62], "D": [52, 53, 54, 63]}
-ROLES = {"A": ["pi(s')", "Qt1", "Qt2", "Q1", "Q2", "pi(s)"], "C": ["pi", "Q1", "Q2"]}
+ROLES = {"A": ["pi(s')", "Qt1", "Qt2", "Q1", "Q2", "pi(s)"], "C": ["Q1", "Q2", "pi"]}  # block-group order
 # shader clock during phase A: s_memtime ticks (slots 40/41) per realtime tick (slots 0/60)
 clk = []
 for r in runs:
