@@ -51,6 +51,16 @@ def gemm_flops(obs, act, hidden, B):
     return [A, Bk, C, D], total_survey, Gq, Gp
 
 
+def soa_copy(rb):
+    """The same rows in a struct-of-arrays replay (layout comparison leg of the sweep)."""
+    from sac.replay_buffer import ReplayBuffer
+
+    soa = ReplayBuffer(rb.capacity, device=rb.device, obs_dim=rb.obs_dim, act_dim=rb.act_dim, layout="soa")
+    soa.push_batch(rb.obs, rb.act, rb.rew, rb.next_obs, rb.done)
+    torch.cuda.synchronize()
+    return soa
+
+
 def synthetic_replay(rb, cap, obs, act, seed):
     """s~N(0,1), a~U(-1,1), r~N(0,1), d~Bernoulli(.01), s' = next row's s."""
     rng = np.random.default_rng(seed)
@@ -320,6 +330,7 @@ def main():
 
     if rank == 0:
         sweep = {} if args.no_sweep else gather_sweep(rb, device)
+        sweep_soa = {} if args.no_sweep else gather_sweep(soa_copy(rb), device, sizes=(65536, 1_048_576))
         W = 2 * c["obs"] + c["act"] + 2
         sps = total_steps / elapsed
         line = {
@@ -361,11 +372,15 @@ def main():
         if sweep:
             line["replay_sample_GBps_sweep"] = sweep["sample_gather"]
             line["replay_gather_GBps_sweep"] = sweep["gather"]
+            line["replay_layout"] = f"transition records, row stride {rb.row_stride} floats"
+            line["replay_gather_GBps_sweep_soa_layout"] = sweep_soa["gather"]
             bmax = max(int(b) for b in sweep["gather"])
             ms = sweep["ms"][f"gather/{bmax}"]
-            gtr, gsrc = pmc_traffic("replay_gather_kernel", "gather", "fp32")
+            gk = ("replay_gather_records_kernel" if rb.layout == "records" and rb.row_stride in (16, 32, 64, 128, 256)
+                  and c["obs"] % 4 == 0 and c["act"] % 4 == 0 else "replay_gather_kernel")
+            gtr, gsrc = pmc_traffic(gk, "gather", "fp32")
             line["roofline_gather"] = {
-                "bound": "hbm", "kernel": "replay_gather_kernel", "batch": bmax,
+                "bound": "hbm", "kernel": gk, "batch": bmax,
                 "achieved": sweep["gather"][str(bmax)], "peak": PEAK_HBM_GBS, "unit": "GB/s",
                 "frac": round(sweep["gather"][str(bmax)] / PEAK_HBM_GBS, 5), "traffic": gtr,
                 "traffic_source": gsrc, "bytes_per_launch": bmax * W * 4, "avg_launch_ms": ms,

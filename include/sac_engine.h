@@ -25,9 +25,14 @@
  *     — i.e. the concatenation of reference state_dict() values
  *     (net.0.weight, net.0.bias, net.2.weight, ...; sac/models.py:141-149);
  *   - Adam exp_avg / exp_avg_sq buffers use the same flat layout;
- *   - replay storage is struct-of-arrays, fp32, ring-ordered:
- *     obs[cap][obs_dim], act[cap][act_dim], rew[cap], next_obs[cap][obs_dim],
- *     done[cap]; state[0] = number of valid rows, state[1] = next write slot
+ *   - replay storage is fp32, ring-ordered, in one of two layouts (row_stride):
+ *     struct-of-arrays obs[cap][obs_dim], act[cap][act_dim], rew[cap],
+ *     next_obs[cap][obs_dim], done[cap] (row_stride = 0), or transition
+ *     records [cap][row_stride] holding each row's fields at the field
+ *     pointers' offsets (the default of sac/replay_buffer.py: obs | next_obs |
+ *     act | rew | done, padded to whole 128-B lines, so a sampled row is 2
+ *     cache lines at C2 instead of ~6.5);
+ *     state[0] = number of valid rows, state[1] = next write slot
  *     (the oldest row once full), state[2] = push generation (incremented by
  *     every push and by ReplayBuffer.clear(); a batch the engine staged for
  *     the next step is used only while it matches).
@@ -98,6 +103,9 @@ typedef struct sac_replay {
   int64_t capacity;
   int32_t obs_dim, act_dim;
   int64_t *state;        /* device [3]: size, next write slot, push generation */
+  int64_t row_stride;    /* 0: struct-of-arrays (each field its own dense [cap][width] array);
+                            > 0: transition records -- every field is a column of ONE
+                            [cap][row_stride] fp32 table (floats between consecutive rows) */
 } sac_replay;
 
 typedef struct sac_engine sac_engine;

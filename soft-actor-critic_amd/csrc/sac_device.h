@@ -223,6 +223,21 @@ __host__ __device__ inline int64_t feistel_sample(const Feistel& f, int64_t b, i
   return (int64_t)y;
 }
 
+// ----------------------------------------------------------------------------- replay layout
+// Row strides (floats) of the replay fields (include/sac_engine.h sac_replay):
+// struct-of-arrays (row_stride == 0: each field's own width) or transition
+// records (every field a column of one [cap][row_stride] table).
+struct RowStrides {
+  int64_t obs, act, one;  // obs / next_obs, act, rew / done
+};
+__host__ __device__ inline RowStrides row_strides(int64_t row_stride, int obs_dim, int act_dim) {
+  RowStrides r;
+  r.obs = row_stride ? row_stride : obs_dim;
+  r.act = row_stride ? row_stride : act_dim;
+  r.one = row_stride ? row_stride : 1;
+  return r;
+}
+
 // ----------------------------------------------------------------------------- block reductions
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll

@@ -1238,11 +1238,13 @@ __device__ __forceinline__ void gather_rows(const sac_replay& rb, const AS_L int
   const AS_G float* ract = GPC(float, rb.act);
   const AS_G float* rrew = GPC(float, rb.rew);
   const AS_G float* rdone = GPC(float, rb.done);
+  const RowStrides rs = row_strides(rb.row_stride, O, A);
   const int nI = R * (O > A ? O : A);
   for (int i = threadIdx.x; i < nI; i += SAC_THREADS) {
     const int io = i < R * O ? i : R * O - 1, ia = i < R * A ? i : R * A - 1, ir = i < R ? i : R - 1;
     const int64_t so = slotB[io / O], sa = slotB[ia / A], sr = slotB[ir];
-    const int64_t po = (so < 0 ? 0 : so) * O + io % O, pa = (sa < 0 ? 0 : sa) * A + ia % A, pr = sr < 0 ? 0 : sr;
+    const int64_t po = (so < 0 ? 0 : so) * rs.obs + io % O, pa = (sa < 0 ? 0 : sa) * rs.act + ia % A,
+                  pr = (sr < 0 ? 0 : sr) * rs.one;
     const float vo = obs[po], vn = nobs[po], va = ract[pa], vr = rrew[pr], vd = rdone[pr];
     if (i < R * O) {
       s[i] = so >= 0 ? vo : 0.f;

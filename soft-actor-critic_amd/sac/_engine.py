@@ -61,7 +61,8 @@ class EngineBuffers(ctypes.Structure):
 class ReplayDesc(ctypes.Structure):
     _fields_ = [("obs", ctypes.c_void_p), ("act", ctypes.c_void_p), ("rew", ctypes.c_void_p),
                 ("next_obs", ctypes.c_void_p), ("done", ctypes.c_void_p), ("capacity", ctypes.c_int64),
-                ("obs_dim", ctypes.c_int32), ("act_dim", ctypes.c_int32), ("state", ctypes.c_void_p)]
+                ("obs_dim", ctypes.c_int32), ("act_dim", ctypes.c_int32), ("state", ctypes.c_void_p),
+                ("row_stride", ctypes.c_int64)]
 
 
 # name -> (restype, argtypes): every symbol include/sac_engine.h declares

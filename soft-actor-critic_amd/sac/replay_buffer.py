@@ -1,8 +1,19 @@
 """Replay buffer resident in HBM (API of reference ``sac/replay_buffer.py``).
 
-Storage is struct-of-arrays on the device:
-``obs[cap][O] | act[cap][A] | rew[cap] | next_obs[cap][O] | done[cap]`` (fp32),
-ring-ordered with ``(size, pos)`` mirrored on the host and on the device.
+Storage is fp32 on the device, ring-ordered with ``(size, pos)`` mirrored on
+the host and on the device, in one of two layouts (``layout=``):
+
+* ``"records"`` (default): one ``[cap][row_stride]`` table of transition
+  records ``obs | next_obs | act | rew | done | pad``, padded to whole 128-B
+  lines (C2: 54 floats -> 64 = 256 B).  A sampled row is 2 cache lines; the
+  replay-gather PMC profile measured 3.2x more bytes fetched than gathered for
+  the struct-of-arrays form (scattered 4-B rew/done lines, 96-B obs rows
+  straddling lines), DESIGN.md §2;
+* ``"soa"``: struct-of-arrays ``obs[cap][O] | act[cap][A] | rew[cap] |
+  next_obs[cap][O] | done[cap]``.
+
+``obs``, ``act``, ``rew``, ``next_obs``, ``done`` are tensor views of the
+fields in both layouts.
 
 * ``push`` (replay_buffer.py:21-30) stages rows in pinned host memory; staged rows
   are appended by one HIP kernel (``sac_replay_push``) before the next read, so an
@@ -32,11 +43,14 @@ Transition = namedtuple("Transition", ("state", "action", "reward", "next_state"
 
 class ReplayBuffer:
     def __init__(self, capacity: int, device=None, obs_dim: Optional[int] = None,
-                 act_dim: Optional[int] = None, stage_rows: int = 4096):
+                 act_dim: Optional[int] = None, stage_rows: int = 4096, layout: str = "records"):
         """Experience replay of at most ``capacity`` transitions (FIFO eviction)."""
         self.capacity = int(capacity)
         if self.capacity < 1:
             raise ValueError("capacity must be >= 1")
+        if layout not in ("records", "soa"):
+            raise ValueError("layout must be 'records' or 'soa'")
+        self.layout = layout
         self.device = torch.device(device) if device is not None else torch.device(
             "cuda" if torch.cuda.is_available() else "cpu")
         self._size = 0
@@ -55,17 +69,29 @@ class ReplayBuffer:
         E.require_gpu(self.device)
         self.obs_dim, self.act_dim = int(obs_dim), int(act_dim)
         cap, dev = self.capacity, self.device
+        O, A = self.obs_dim, self.act_dim
         f32 = dict(dtype=torch.float32, device=dev)
-        self.obs = torch.zeros(cap, self.obs_dim, **f32)
-        self.act = torch.zeros(cap, self.act_dim, **f32)
-        self.rew = torch.zeros(cap, **f32)
-        self.next_obs = torch.zeros(cap, self.obs_dim, **f32)
-        self.done = torch.zeros(cap, **f32)
+        self.row_width = 2 * O + A + 2
+        if self.layout == "records":
+            W = self.row_width
+            self.row_stride = 16 if W <= 16 else (W + 31) // 32 * 32  # whole 64-B / 128-B lines
+            self.records = torch.zeros(cap, self.row_stride, **f32)
+            self.obs = self.records[:, :O]
+            self.next_obs = self.records[:, O:2 * O]
+            self.act = self.records[:, 2 * O:2 * O + A]
+            self.rew = self.records[:, 2 * O + A]
+            self.done = self.records[:, 2 * O + A + 1]
+        else:
+            self.row_stride = 0
+            self.obs = torch.zeros(cap, O, **f32)
+            self.act = torch.zeros(cap, A, **f32)
+            self.rew = torch.zeros(cap, **f32)
+            self.next_obs = torch.zeros(cap, O, **f32)
+            self.done = torch.zeros(cap, **f32)
         self.state = torch.zeros(3, dtype=torch.int64, device=dev)  # size, next slot, push generation
-        self.row_width = 2 * self.obs_dim + self.act_dim + 2
         self._desc = E.ReplayDesc(
             self.obs.data_ptr(), self.act.data_ptr(), self.rew.data_ptr(), self.next_obs.data_ptr(),
-            self.done.data_ptr(), cap, self.obs_dim, self.act_dim, self.state.data_ptr())
+            self.done.data_ptr(), cap, O, A, self.state.data_ptr(), self.row_stride)
         self._alloc_done = True
 
     @property

@@ -56,7 +56,8 @@ def _c_layout(tmp_path):
                               "adam_eps", "auto_entropy", "target_entropy", "precision", "seed"],
         "sac_engine_buffers": ["pi", "q1", "q2", "q1t", "q2t", "pi_m", "pi_v", "q1_m", "q1_v", "q2_m", "q2_v",
                                "alpha_state", "opt_steps", "rng_step", "stats", "workspace", "workspace_bytes"],
-        "sac_replay": ["obs", "act", "rew", "next_obs", "done", "capacity", "obs_dim", "act_dim", "state"],
+        "sac_replay": ["obs", "act", "rew", "next_obs", "done", "capacity", "obs_dim", "act_dim", "state",
+                       "row_stride"],
     }
     src = ['#include <stdio.h>', '#include <stddef.h>', '#include "sac_engine.h"', "int main(void) {"]
     for st, fs in fields.items():

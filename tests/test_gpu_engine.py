@@ -34,14 +34,16 @@ def _engine(cfgname="c1", precision="fp32", seed=0, capacity=None):
 
 
 # ---------------------------------------------------------------- replay buffer
-def test_replay_push_gather_ring_exact():
+@pytest.mark.parametrize("layout", ["records", "soa"])
+def test_replay_push_gather_ring_exact(layout):
     """push (single rows, staged) + push_batch with wrap-around; gather by
-    logical position == the deque model of replay_buffer.py:12-30 bit-exactly."""
+    logical position == the deque model of replay_buffer.py:12-30 bit-exactly,
+    for both storage layouts."""
     from sac.replay_buffer import ReplayBuffer
 
     O, A, cap = 5, 2, 37
     rng = np.random.default_rng(0)
-    rb = ReplayBuffer(cap, device=DEV, stage_rows=8)
+    rb = ReplayBuffer(cap, device=DEV, stage_rows=8, layout=layout)
     model = []
     for it in range(6):
         n = int(rng.integers(1, 30))
@@ -395,8 +397,9 @@ def test_clear_and_refill_invalidates_the_staged_batch(monkeypatch):
 
 
 # ---------------------------------------------------------------- gather kernel (round 2)
+@pytest.mark.parametrize("layout", ["records", "soa"])
 @pytest.mark.parametrize("obs,act", [(24, 4), (5, 2), (32, 2)])
-def test_sample_gather_equals_sampler_plus_gather(lib, obs, act):
+def test_sample_gather_equals_sampler_plus_gather(lib, obs, act, layout):
     """sac_replay_sample_gather (sampler + row-vectorised gather in one kernel)
     returns the sampler's indices and exactly the rows sac_replay_gather
     returns for them, for 16-B-aligned rows (obs 24/32) and scalar rows (5/2),
@@ -405,7 +408,7 @@ def test_sample_gather_equals_sampler_plus_gather(lib, obs, act):
     from sac.replay_buffer import ReplayBuffer
 
     cap = 3000
-    rb = ReplayBuffer(cap, device=DEV, obs_dim=obs, act_dim=act)
+    rb = ReplayBuffer(cap, device=DEV, obs_dim=obs, act_dim=act, layout=layout)
     g = np.random.default_rng(0)
     n = 4100  # wraps: the oldest row sits at slot 1100
     rb.push_batch(g.standard_normal((n, obs), dtype=np.float32), g.uniform(-1, 1, (n, act)).astype(np.float32),
@@ -465,3 +468,25 @@ def test_c3_full_size_properties():
     assert all(np.isfinite(losses)), losses
     assert np.all(np.isfinite(eng.last_targets().cpu().numpy()))
     assert int(eng.rng_step.item()) == 60
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_training_is_layout_independent(precision):
+    """The fused step reads the replay through its field strides: the same rows
+    in transition records and in struct-of-arrays give the same bits (device
+    sampler, staged next-step batches and graph replay included)."""
+    import bench
+
+    out = {}
+    for layout in ("records", "soa"):
+        eng, rb, c = _engine("c2", precision, capacity=5000)
+        if layout == "soa":
+            rb = bench.soa_copy(rb)
+        assert rb.layout == layout
+        eng.train(rb, 3)
+        eng.train_graph(rb, 6, chunk=3)
+        eng.check()
+        out[layout] = {k: v.clone() for k, v in eng.state_tensors().items()}
+        out[layout]["stats"] = eng.stats.clone()
+    for k in out["records"]:
+        assert torch.equal(out["records"][k], out["soa"][k]), k
