@@ -22,6 +22,9 @@ int sac_engine_debug_staged_step(sac_engine* e, uint64_t* step_out, void* stream
 /* 1 if phases A/C run role-split (per-network workgroups with in-launch
  * hand-offs), 0 if one workgroup per row tile runs all networks. */
 int sac_engine_uses_roles(const sac_engine *e);
+/* 1 if phases A/C run the hidden-split role kernels (sac_split.h: two
+ * workgroups per role and row tile, each with half of the 256-wide layer 1). */
+int sac_engine_uses_split(const sac_engine *e);
 /* Host evaluation of the device sampler (the same inline code as the sampler
  * inside sac_engine_train and sac_replay_sample_indices): out[b] = b-th element
  * of the Philox-keyed Feistel permutation of [0, size) for RNG (seed, step). */

@@ -33,6 +33,7 @@
 #define SAC_VERSION "sac-mi355x 0.1.0"
 
 #include "sac_phases.h"
+#include "sac_split.h"
 
 // ============================================================================ params / replay
 template <typename T>
@@ -329,6 +330,15 @@ static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
   auto P = [&](size_t o) -> void* { return base ? (void*)(base + o) : nullptr; };
   int maxKp = 32, maxNo = 32;
   size_t xt_q0 = 0;
+  const int nrt0 = (B + SAC_ROWS - 1) / SAC_ROWS;
+  // hidden-split role kernels (sac_split.h): two hidden layers of width 256 in
+  // both nets, identity pi output, 2 act <= 32, and 12 * nrt co-resident blocks
+  int split = c->q_layers == 3 && c->pi_layers == 3 && c->q_dims[1] == SPLIT_H && c->q_dims[2] == SPLIT_H &&
+              c->pi_dims[1] == SPLIT_H && c->pi_dims[2] == SPLIT_H && c->pi_out_act == SAC_ACT_IDENTITY &&
+              2 * A <= 32 && 12 * nrt0 <= 256 && SAC_ROWS * (A + 1) <= SAC_HAND_STRIDE;
+  if (const char* v = getenv("SAC_SPLIT")) split = split && atoi(v) != 0;
+  if (const char* v = getenv("SAC_ROLES")) split = split && atoi(v) != 0;
+  const int bp0 = split ? 2 * Bp : Bp;  // batch columns of layer 0's GT / XT
   for (int ni = 0; ni < 5; ++ni) {
     const bool is_pi = ni == NET_PI;
     const bool trainable = ni <= NET_Q2;
@@ -354,19 +364,21 @@ static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
       else maxNo = std::max(maxNo, ly.Np);
       ly.Wc = P(lay.take((size_t)ly.Np * ly.Kp * esz));
       if (trainable) {
+        const int bpl = l == 0 ? bp0 : Bp;
         ly.WTc = P(lay.take((size_t)ly.Kp * ly.Np * esz));
         if (ni == NET_Q2 && l == 0) {
           ly.XT = P(xt_q0);
         } else {
           // pi: two copies by step parity (phase D of step k reads one while
           // phase A of step k + 1 writes the other when they share a launch)
-          const size_t o = lay.take((size_t)ly.Kp * Bp * esz * (is_pi ? 2 : 1));
+          const size_t o = lay.take((size_t)ly.Kp * bpl * esz * (is_pi ? 2 : 1));
           if (ni == NET_Q1 && l == 0) xt_q0 = o;
           ly.XT = P(o);
-          ly.xt_par = is_pi ? (long)ly.Kp * Bp : 0;
+          ly.xt_par = is_pi ? (long)ly.Kp * bpl : 0;
         }
-        ly.GT = P(lay.take((size_t)ly.Np * Bp * esz));
-        ly.dbp = (float*)P(lay.take((size_t)nrt * ly.N * 4));
+        ly.GT = P(lay.take((size_t)ly.Np * bpl * esz));
+        // bias-gradient partials: one row per row tile (split layer 0: per half and row tile)
+        ly.dbp = (float*)P(lay.take((size_t)(l == 0 && split ? 2 * Bp / SAC_ROWS : nrt) * ly.N * 4));
       }
       if (is_pi) ly.pstash = (float*)P(lay.take((size_t)Br * ly.Np * 4));
     }
@@ -384,6 +396,9 @@ static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
   h.gran = (uint64_t*)P(lay.take((size_t)G_COUNT * nrt * h.gstride * 8));
   h.stg_stride = (16 + 2 * SAC_ROWS * O + SAC_ROWS * A + 2 * SAC_ROWS + 15) / 16 * 16;
   h.stg = (float*)P(lay.take((size_t)nrt * h.stg_stride * 4));
+  h.split = split;
+  h.gs2 = SAC_ROWS * std::max(2 * A, A + 1);
+  h.gran2 = (uint64_t*)P(lay.take((size_t)GS_COUNT * nrt * 2 * h.gs2 * 8));
   int nB = 0, nD = 0;
   for (int ni = NET_PI; ni <= NET_Q2; ++ni)
     for (int l = 0; l < h.net[ni].L; ++l)
@@ -443,6 +458,7 @@ static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
   h.o_ga = lt(R * A);
   h.o_gout = lt(R * h.ldo);
   h.o_slot = lt(2 * R);  // int64[R]
+  h.o_red = split ? lt(SAC_NW * 256) : 0;
 
   if (e) {
     h.B = B;
@@ -521,8 +537,9 @@ static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
           for (int kt = 0; kt < ly.Kp / 32; ++kt) {
             TileDesc t;
             memset(&t, 0, sizeof(t));
-            t.GT = (const char*)ly.GT + (size_t)nt * 32 * Bp * esz2;
-            t.XT = (const char*)ly.XT + (size_t)kt * 32 * Bp * esz2;
+            const int bpl = (l == 0 && split) ? 2 * Bp : Bp;
+            t.GT = (const char*)ly.GT + (size_t)nt * 32 * bpl * esz2;
+            t.XT = (const char*)ly.XT + (size_t)kt * 32 * bpl * esz2;
             t.W = nd.P + ly.w_off;
             t.Wm = nd.M + ly.w_off;
             t.Wv = nd.V + ly.w_off;
@@ -538,6 +555,7 @@ static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
             }
             t.dbp = ly.dbp;
             t.xt_par = ly.xt_par;
+            t.bp = (l == 0 && split) ? 2 * Bp : Bp;
             t.K = ly.K;
             t.N = ly.N;
             t.Kp = ly.Kp;
@@ -545,7 +563,7 @@ static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
             t.n0 = nt * 32;
             t.k0 = kt * 32;
             t.opt = ni;
-            t.nrt = nrt;
+            t.nrt = (l == 0 && split) ? 2 * Bp / SAC_ROWS : nrt;
             (ni == NET_PI ? e->hostD : e->hostB).push_back(t);
           }
       }
@@ -557,7 +575,7 @@ static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
       // on C2: four launches stay the default; SAC_FUSE=1|2 opts in.
       int fuse = 0;
       if (const char* v = getenv("SAC_FUSE")) fuse = std::max(0, std::min(2, atoi(v)));
-      if (!e->h.roles || nD + 1 + 6 * nrt > 256) fuse = 0;
+      if (!e->h.roles || e->h.split || nD + 1 + 6 * nrt > 256) fuse = 0;
       if (fuse == 2 && nB + 3 * nrt > 256) fuse = 1;
       e->fused = fuse;
     }
@@ -576,6 +594,8 @@ static void set_lds_attrs(size_t bytes) {
   (void)hipFuncSetAttribute((const void*)sac_actor<T, true, false>, hipFuncAttributeMaxDynamicSharedMemorySize, b);
   (void)hipFuncSetAttribute((const void*)sac_actor<T, true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, b);
   (void)hipFuncSetAttribute((const void*)sac_policy_act_kernel<T>, hipFuncAttributeMaxDynamicSharedMemorySize, b);
+  (void)hipFuncSetAttribute((const void*)sac_target_critic_split<T>, hipFuncAttributeMaxDynamicSharedMemorySize, b);
+  (void)hipFuncSetAttribute((const void*)sac_actor_split<T>, hipFuncAttributeMaxDynamicSharedMemorySize, b);
   (void)hipFuncSetAttribute((const void*)sac_critic_update<T>, hipFuncAttributeMaxDynamicSharedMemorySize, b);
   (void)hipFuncSetAttribute((const void*)sac_actor_update<T>, hipFuncAttributeMaxDynamicSharedMemorySize, b);
 }
@@ -602,7 +622,9 @@ static void launch_kind(sac_engine* e, int kind, const sac_replay* rb, const int
   const int stg = e->h.stage ? e->nrt : 0;  // stager blocks of phase C
   switch (kind) {
     case L_A:
-      if (e->h.roles)
+      if (e->h.split)
+        sac_target_critic_split<T><<<e->nrt * 12, SAC_THREADS, lf, s>>>(e->d, *rb, idx, eps);
+      else if (e->h.roles)
         sac_target_critic<T, true, false><<<e->nrt * 6, SAC_THREADS, lf, s>>>(e->d, *rb, idx, eps);
       else
         sac_target_critic<T, false, false><<<e->nrt * e->h.xs, SAC_THREADS, lf, s>>>(e->d, *rb, idx, eps);
@@ -611,7 +633,9 @@ static void launch_kind(sac_engine* e, int kind, const sac_replay* rb, const int
       sac_critic_update<T><<<e->nB, SAC_UPD_THREADS, e->upd_lds, s>>>(e->d, e->tilesB);
       break;
     case L_C:
-      if (e->h.roles)
+      if (e->h.split)
+        sac_actor_split<T><<<e->nrt * 6 + stg, SAC_THREADS, lf, s>>>(e->d, *rb);
+      else if (e->h.roles)
         sac_actor<T, true, false><<<e->nrt * 3 + stg, SAC_THREADS, lf, s>>>(e->d, *rb);
       else
         sac_actor<T, false, false><<<e->nrt * e->h.xs + stg, SAC_THREADS, lf, s>>>(e->d, *rb);
@@ -932,6 +956,8 @@ int sac_debug_sample_indices_host(int64_t size, int32_t batch, uint64_t seed, ui
 }
 
 int sac_engine_uses_roles(const sac_engine* e) { return e && e->h.roles ? 1 : 0; }
+
+int sac_engine_uses_split(const sac_engine* e) { return e && e->h.split ? 1 : 0; }
 
 int sac_engine_phase_layout(const sac_engine* e) { return e ? e->fused : 0; }
 

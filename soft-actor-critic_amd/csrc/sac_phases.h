@@ -110,6 +110,11 @@ struct EngineDev {
   float* stg;
   int stg_stride;  // floats per row-tile record
   int stage;       // stager blocks launched with phase C
+  // hidden-split role kernels (sac_split.h): two workgroups per (role, row tile)
+  int split;
+  uint64_t* gran2;  // [GS_COUNT][nrt][2][gs2] split hand-off granules
+  int gs2;
+  int o_red;        // LDS: SAC_NW x 256 floats of k-split partial tiles
   int spin_limit;  // polls before a hand-off wait gives up and sets SYNC_TIMEOUT (~0.3 s at 1 << 22)
   // LDS layout (float offsets)
   int o_X, o_Y, o_P1[SAC_DEV_LAYERS], ldp1[SAC_DEV_LAYERS], o_P2[SAC_DEV_LAYERS], ldp2[SAC_DEV_LAYERS];
@@ -136,6 +141,8 @@ struct TileDesc {
   const float* dbp;
   long xt_par;     // element offset of the odd-step X^T copy (pi tiles), else 0
   int K, N, Kp, Np, n0, k0, opt, nrt;
+  int bp;          // batch columns of the GT / XT operands (Bp; 2 Bp for a hidden-split layer 0:
+                   // the two halves' partial dY side by side, X duplicated)
 };
 
 
@@ -207,15 +214,26 @@ __device__ __forceinline__ void prefetch_engine(const void* p) {
 // so the load latency overlaps the epilogue, the barrier and whatever non-GEMM
 // work sits between the two steps.
 struct GemmW {
-  const void* p;      // packed B matrix
-  int cols;           // reduction length (multiple of SAC_PAD)
+  const void* p;      // packed B matrix (first element of the step's first tile and chunk)
+  int cols;           // reduction length of the step (multiple of SAC_PAD)
   int NT;             // 16-row tiles of the packed matrix = output tiles of the step
   const float* bias;  // forward steps: bias [N], prefetched with the weights
   int N;
+  int tcols;          // column count of the whole packed matrix: a 16-row tile is 16 * tcols elements
 };
-__device__ __forceinline__ GemmW gw_fwd(const AS_C LayerDev& L) { return GemmW{L.Wc, L.Kp, L.Np >> 4, L.bias, L.N}; }
-__device__ __forceinline__ GemmW gw_bwd(const AS_C LayerDev& L) { return GemmW{L.WTc, L.Np, L.Kp >> 4, nullptr, 0}; }
-__device__ __forceinline__ GemmW gw_none() { return GemmW{nullptr, 0, 0, nullptr, 0}; }
+__device__ __forceinline__ GemmW gw_fwd(const AS_C LayerDev& L) { return GemmW{L.Wc, L.Kp, L.Np >> 4, L.bias, L.N, L.Kp}; }
+__device__ __forceinline__ GemmW gw_bwd(const AS_C LayerDev& L) { return GemmW{L.WTc, L.Np, L.Kp >> 4, nullptr, 0, L.Np}; }
+__device__ __forceinline__ GemmW gw_none() { return GemmW{nullptr, 0, 0, nullptr, 0, 0}; }
+// Sub-matrix view of a packed [rows][cols_full] operand: rows [row0, row0 + nrows)
+// (multiples of 16) and reduction columns [col0, col0 + ncols) (multiples of the
+// MFMA K chunk).  Tile t starts at t * 16 * cols_full elements and chunk ch of a
+// tile at ch * 64 * KL = ch * KC * 16 elements, so the view's origin is
+// row0 * cols_full + col0 * 16 (packed_off with KL / KC = 1/4 for both dtypes).
+template <typename T>
+__device__ __forceinline__ GemmW gw_sub(const void* p, int cols_full, int row0, int nrows, int col0, int ncols,
+                                        const float* bias, int N) {
+  return GemmW{(const T*)p + (size_t)row0 * cols_full + (size_t)col0 * 16, ncols, nrows >> 4, bias, N, cols_full};
+}
 
 #ifndef SAC_PF
 // Cross-step register prefetch of the weight stream: chunks per tile of the
@@ -243,8 +261,8 @@ __device__ __forceinline__ void pf_issue(Pf<T>& pf, const GemmW& w) {
   if (!w.p || wave >= w.NT) return;
   const int last = w.cols / KC - 1;
   const int nt1 = wave + SAC_NW < w.NT ? wave + SAC_NW : wave;
-  const AS_G T* b0 = GPC(T, w.p) + packed_lane<T>(wave, w.cols, lane);
-  const AS_G T* b1 = GPC(T, w.p) + packed_lane<T>(nt1, w.cols, lane);
+  const AS_G T* b0 = GPC(T, w.p) + packed_lane<T>(wave, w.tcols, lane);
+  const AS_G T* b1 = GPC(T, w.p) + packed_lane<T>(nt1, w.tcols, lane);
   if (w.bias) {  // same columns as layer_fwd's first pair: n0 = 16 wave + c, n1 = n0 + 16 SAC_NW
     const int n0 = wave * 16 + (lane & 15), n1 = n0 + 16 * SAC_NW;
     pf.b0 = GPC(float, w.bias)[n0 < w.N ? n0 : w.N - 1];
@@ -293,8 +311,8 @@ __device__ __forceinline__ void held_issue(Held<T, HC>& h, const GemmW& w) {
   const int last = w.cols / MM<T>::KC - 1;
   const int nt1 = wave + SAC_NW < w.NT ? wave + SAC_NW : wave;
   const __amdgpu_buffer_rsrc_t rs = coh_rsrc(w.p, 0xFFFFFFF0u);
-  const uint32_t o0 = (uint32_t)(packed_lane<T>(wave, w.cols, lane) * sizeof(T));
-  const uint32_t o1 = (uint32_t)(packed_lane<T>(nt1, w.cols, lane) * sizeof(T));
+  const uint32_t o0 = (uint32_t)(packed_lane<T>(wave, w.tcols, lane) * sizeof(T));
+  const uint32_t o1 = (uint32_t)(packed_lane<T>(nt1, w.tcols, lane) * sizeof(T));
   if (w.bias) {  // layer_fwd's first pair: n0 = 16 wave + c, n1 = n0 + 16 SAC_NW
     const int n0 = wave * 16 + (lane & 15), n1 = n0 + 16 * SAC_NW;
     h.b0 = ldf<COH>(w.bias + (n0 < w.N ? n0 : w.N - 1));
@@ -402,8 +420,8 @@ __device__ __forceinline__ void gemm_pair_fixed(const lf* __restrict__ arow, int
   }
   if (!have) {
     const __amdgpu_buffer_rsrc_t rs = coh_rsrc(w.p, 0xFFFFFFF0u);
-    const uint32_t o0 = (uint32_t)(packed_lane<T>(nt0, w.cols, lane) * sizeof(T));
-    const uint32_t o1 = (uint32_t)(packed_lane<T>(nt1, w.cols, lane) * sizeof(T));
+    const uint32_t o0 = (uint32_t)(packed_lane<T>(nt0, w.tcols, lane) * sizeof(T));
+    const uint32_t o1 = (uint32_t)(packed_lane<T>(nt1, w.tcols, lane) * sizeof(T));
     static_for<NCH>([&](auto uc) {
       constexpr int u = decltype(uc)::value;
       f0[u] = coh_frag<T, COH>(rs, o0 + u * FSB);
@@ -462,8 +480,8 @@ __device__ __forceinline__ void gemm_step(const lf* __restrict__ A, int lda, con
   auto pair = [&](int nt0, bool first) __attribute__((always_inline)) {
     const int nt1 = nt0 + SAC_NW;
     const bool has1 = nt1 < NT;
-    const uint32_t o0 = (uint32_t)(packed_lane<T>(nt0, w.cols, lane) * sizeof(T));
-    const uint32_t o1 = (uint32_t)(packed_lane<T>(has1 ? nt1 : nt0, w.cols, lane) * sizeof(T));
+    const uint32_t o0 = (uint32_t)(packed_lane<T>(nt0, w.tcols, lane) * sizeof(T));
+    const uint32_t o1 = (uint32_t)(packed_lane<T>(has1 ? nt1 : nt0, w.tcols, lane) * sizeof(T));
     f32x4 acc0[RT], acc1[RT];
 #pragma unroll
     for (int rt = 0; rt < RT; ++rt) acc0[rt] = acc1[rt] = (f32x4){0.f, 0.f, 0.f, 0.f};
@@ -627,7 +645,7 @@ __device__ __forceinline__ void layer_bwd(const lf* G, int ldg, const AS_C Layer
 template <typename T, int ROWS>
 __device__ __forceinline__ void store_T(const lf* __restrict__ src, int lds_ld, int Kp, int K, void* dst_,
                                                  int Bp, int col0, int nvalid, float* dbp_,
-                                                 const lf* __restrict__ rowscale = nullptr) {
+                                                 const lf* __restrict__ rowscale = nullptr, int dbp_ld = 0) {
   AS_G T* dst = GP(T, dst_);
   AS_G float* dbp = GP(float, dbp_);
   constexpr int CH = ROWS / 8;
@@ -666,7 +684,7 @@ __device__ __forceinline__ void store_T(const lf* __restrict__ src, int lds_ld, 
     if (dbp) {
 #pragma unroll
       for (int o = 1; o < CH; o <<= 1) s += __shfl_xor(s, o, 64);
-      if (live && ch == 0 && k < K) dbp[(size_t)(col0 / SAC_ROWS) * K + k] = s;
+      if (live && ch == 0 && k < K) dbp[(size_t)(col0 / SAC_ROWS) * (dbp_ld ? dbp_ld : K) + k] = s;
     }
   }
 }
@@ -818,7 +836,7 @@ __device__ __forceinline__ void dw_adam_tile(const AS_C EngineDev& E, const Tile
   const AS_C TileDesc& td = *(const AS_C TileDesc*)tdp_;  // scalar loads
   STAMP(polyak ? 48 : 52);
   const int tid = threadIdx.x;
-  const int Bp = E.Bp;
+  const int Bp = td.bp;
   // LDS: stage [64][SAC_UPD_BCH + pad] of T | acc / new params [32][33] f32 | targets [32][33] | bias reduce [32][17]
   const int lds_row = SAC_UPD_BCH + 16 / (int)sizeof(T);  // +16 B per row: rows start on different banks
   AS_L T* stage = (AS_L T*)lds;

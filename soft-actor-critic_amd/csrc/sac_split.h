@@ -1,0 +1,850 @@
+// sac_split.h — hidden-split role kernels of phases A and C.
+//
+// For nets with two hidden layers of width H = 256 (the reference's
+// BipedalWalker / Donkey configs, C2/C4), every role of the role split
+// (sac_phases.h "role hand-offs") runs as TWO workgroups per row tile, one per
+// half h of layer 1's H outputs:
+//
+//   layer 0  (K0 -> H)   computed in full by both halves (K0 is small);
+//   layer 1  (H -> H)    half h computes outputs [h H/2, (h+1) H/2): its half of
+//                        W1 (128 KB fp32) is register-held, issued at launch
+//                        start, so the layer runs at the MFMA rate;
+//   layer 2  (H -> out)  half h sums over ITS inputs only: a partial output;
+//                        consumers add the two partials (+ bias) themselves.
+//
+// Backward mirrors it: dY1 of a half is exact (elementwise in the seed for the
+// critics), dY0 = dY1_h W1[h] is a PARTIAL over the half's n; the partial is
+// masked (relu' is elementwise) and stored as its own batch columns of layer
+// 0's dY^T, so phase B/D's dW = sum over 2 Bp columns adds the halves, and
+// da (phase C) = the sum of the halves' partial dX0.
+//
+// No half waits for its peer on the critical path: a consumer reads both
+// halves' partial granules.  Bit-identical to the reference up to fp32
+// summation order (two partial sums instead of one), checked against the
+// oracle in tests/test_gpu_parity.py.
+//
+// Reference cross-walk: target agent.py:195-211, critic agent.py:213-236,
+// actor agent.py:238-260, policy head models.py:73-87.
+#pragma once
+#include "sac_phases.h"
+
+#define SPLIT_H 256
+#define SPLIT_HH 128
+
+// Split granule kinds: [GS_COUNT][nrt][2 halves][E.gs2] 8-B granules
+enum SplitGran {
+  GS_PI = 0,   // pi(s') layer-2 partial [R][2A]              -> target critics
+  GS_PS = 1,   // pi(s) layer-2 partial [R][2A]               -> the peer pi(s) half
+  GS_QT1 = 2,  // target critic 1 partial q [R]               -> critics
+  GS_QT2 = 3,  // target critic 2 partial q [R]               -> critics
+  GS_LP = 4,   // log pi(a~'|s') [R] (half 0 only)           -> critics
+  GS_QA1 = 5,  // critic 1 partial q [R]                      -> its peer half
+  GS_QA2 = 6,  // critic 2 partial q [R]
+  GS_C1 = 7,   // phase C critic 1: partial da [R][A], partial q [R] -> pi halves
+  GS_C2 = 8,
+  GS_COUNT = 9
+};
+__device__ __forceinline__ AS_G uint64_t* gs_at(const AS_C EngineDev& E, int kind, int rbi, int h) {
+  return GP(uint64_t, E.gran2) + ((size_t)(kind * E.nrt + rbi) * 2 + h) * E.gs2;
+}
+
+// ---------------------------------------------------------------------------- held GEMM
+// The fragments of a wave's NTW output tiles (t = wave + j * SAC_NW) over the
+// first HC reduction chunks of a packed B view, plus the bias of the lane's
+// column in each tile.  Issued early (before waits); consumed by gemm_hs.
+template <typename T, int NTW, int HC>
+struct HTiles {
+  typename MM<T>::Frag f[NTW][HC];
+  float b[NTW];
+};
+
+template <typename T, int NTW, int HC, bool COH = false>
+__device__ __forceinline__ void ht_issue(HTiles<T, NTW, HC>& ht, const GemmW& w) {
+  constexpr uint32_t FSB = 64 * MM<T>::KL * sizeof(T);
+  const int lane = threadIdx.x & 63, wave = wave_id();
+  const int nch = w.cols / MM<T>::KC;
+  const __amdgpu_buffer_rsrc_t rs = coh_rsrc(w.p, 0xFFFFFFF0u);
+  static_for<NTW>([&](auto jc) {
+    constexpr int j = decltype(jc)::value;
+    int t = wave + j * SAC_NW;
+    t = t < w.NT ? t : w.NT - 1;  // clamped: loads valid memory, the tile is skipped
+    const uint32_t o = (uint32_t)(((size_t)t * 16 * w.tcols + lane * MM<T>::KL) * sizeof(T));
+    static_for<HC>([&](auto uc) {
+      constexpr int u = decltype(uc)::value;
+      const uint32_t cu = u < nch ? u : nch - 1;
+      ht.f[j][u] = coh_frag<T, COH>(rs, o + cu * FSB);
+    });
+    if (w.bias) {
+      const int n = t * 16 + (lane & 15);
+      ht.b[j] = ldf<COH>(w.bias + (n < w.N ? n : w.N - 1));
+    }
+  });
+}
+
+// out tiles of A[16][cols] x B^T over the view's reduction: chunks [0, HC) from
+// the held fragments (when ht != null), the rest streamed in batches of 8.
+// Two accumulators per tile (even / odd chunk) cover the dependent-MFMA latency.
+// epi(j, col, acc, bias) for every valid tile j of the wave.
+template <typename T, int NTW, int HC, bool COH = false, typename Epi>
+__device__ __forceinline__ void gemm_hs(const lf* __restrict__ A, int lda, const GemmW& w,
+                                        const HTiles<T, NTW, HC>* ht, Epi&& epi) {
+  typedef typename MM<T>::Frag F;
+  constexpr int KC = MM<T>::KC, KL = MM<T>::KL;
+  constexpr uint32_t FSB = 64 * KL * sizeof(T);
+  const int lane = threadIdx.x & 63, wave = wave_id();
+  const int c = lane & 15, g = lane >> 4;
+  const int nch = w.cols / KC;
+  const lf* arow = A + c * lda + g * KL;
+  f32x4 acc[NTW][2];
+  static_for<NTW>([&](auto jc) {
+    constexpr int j = decltype(jc)::value;
+    acc[j][0] = acc[j][1] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  });
+  int ch0 = 0;
+  if (ht) {  // uniform
+    F a[HC];
+    static_for<HC>([&](auto uc) {
+      constexpr int u = decltype(uc)::value;
+      a[u] = MM<T>::from_lds(arow + (u < nch ? u : 0) * KC);
+    });
+    static_for<HC>([&](auto uc) {
+      constexpr int u = decltype(uc)::value;
+      if (u < nch)
+        static_for<NTW>([&](auto jc) {
+          constexpr int j = decltype(jc)::value;
+          MM<T>::mma(acc[j][u & 1], a[u], ht->f[j][u]);
+        });
+    });
+    ch0 = HC;
+  }
+  if (ch0 < nch) {
+    const __amdgpu_buffer_rsrc_t rs = coh_rsrc(w.p, 0xFFFFFFF0u);
+    uint32_t o[NTW];
+    static_for<NTW>([&](auto jc) {
+      constexpr int j = decltype(jc)::value;
+      int t = wave + j * SAC_NW;
+      t = t < w.NT ? t : w.NT - 1;
+      o[j] = (uint32_t)(((size_t)t * 16 * w.tcols + lane * KL) * sizeof(T));
+    });
+    for (int cb = ch0; cb < nch; cb += 8) {
+      const int rem = nch - cb < 8 ? nch - cb : 8;
+      F f[NTW][8], a[8];
+      static_for<8>([&](auto uc) {
+        constexpr int u = decltype(uc)::value;
+        const uint32_t cu = cb + (u < rem ? u : rem - 1);
+        static_for<NTW>([&](auto jc) {
+          constexpr int j = decltype(jc)::value;
+          f[j][u] = coh_frag<T, COH>(rs, o[j] + cu * FSB);
+        });
+      });
+      static_for<8>([&](auto uc) {
+        constexpr int u = decltype(uc)::value;
+        a[u] = MM<T>::from_lds(arow + (cb + (u < rem ? u : rem - 1)) * KC);
+      });
+      static_for<8>([&](auto uc) {
+        constexpr int u = decltype(uc)::value;
+        if (u < rem)
+          static_for<NTW>([&](auto jc) {
+            constexpr int j = decltype(jc)::value;
+            MM<T>::mma(acc[j][u & 1], a[u], f[j][u]);
+          });
+      });
+    }
+  }
+  static_for<NTW>([&](auto jc) {
+    constexpr int j = decltype(jc)::value;
+    const int t = wave + j * SAC_NW;
+    if (t < w.NT) epi(j, t * 16 + c, acc[j][0] + acc[j][1]);
+  });
+}
+
+// ---------------------------------------------------------------------------- k-split GEMM
+// Small-N steps (NT <= 2 output tiles, long reduction): the reduction is
+// split over the waves (SAC_NW / NT waves per tile, consecutive chunk slices),
+// partial tiles summed through LDS in slice order.  out[r][col] for col < 16 NT.
+template <typename T, bool COH = false>
+__device__ __forceinline__ void gemm_ksplit(const lf* __restrict__ A, int lda, const GemmW& w, lf* red, lf* out,
+                                            int ldo) {
+  typedef typename MM<T>::Frag F;
+  constexpr int KC = MM<T>::KC, KL = MM<T>::KL;
+  constexpr uint32_t FSB = 64 * KL * sizeof(T);
+  const int lane = threadIdx.x & 63, wave = wave_id();
+  const int c = lane & 15, g = lane >> 4;
+  const int NT = w.NT;  // 1 or 2
+  const int wpt = SAC_NW / NT;
+  const int t = wave % NT, sl = wave / NT;
+  const int nch = w.cols / KC;
+  const int per = (nch + wpt - 1) / wpt;
+  const int c0 = sl * per, c1 = c0 + per < nch ? c0 + per : nch;
+  const __amdgpu_buffer_rsrc_t rs = coh_rsrc(w.p, 0xFFFFFFF0u);
+  const uint32_t o = (uint32_t)(((size_t)t * 16 * w.tcols + lane * KL) * sizeof(T));
+  const lf* arow = A + c * lda + g * KL;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  for (int cb = c0; cb < c1; cb += 4) {
+    const int rem = c1 - cb < 4 ? c1 - cb : 4;
+    F f[4], a[4];
+    static_for<4>([&](auto uc) {
+      constexpr int u = decltype(uc)::value;
+      const int cu = cb + (u < rem ? u : rem - 1);
+      f[u] = coh_frag<T, COH>(rs, o + cu * FSB);
+      a[u] = MM<T>::from_lds(arow + cu * KC);
+    });
+    static_for<4>([&](auto uc) {
+      constexpr int u = decltype(uc)::value;
+      if (u < rem) MM<T>::mma(acc, a[u], f[u]);
+    });
+  }
+  // partial tile of (t, sl) -> red[wave][16][16]
+#pragma unroll
+  for (int i = 0; i < 4; ++i) red[wave * 256 + (g * 4 + i) * 16 + c] = acc[i];
+  __syncthreads();
+  for (int i = threadIdx.x; i < 256 * NT; i += SAC_THREADS) {
+    const int tt = i / 256, e = i % 256, r = e / 16, cc = e % 16;
+    float s = 0.f;
+    for (int q = 0; q < wpt; ++q) s += red[(q * NT + tt) * 256 + e];
+    out[r * ldo + tt * 16 + cc] = s;
+  }
+  __syncthreads();
+}
+
+// ---------------------------------------------------------------------------- phase A
+template <typename T>
+__device__ __forceinline__ void target_critic_split_body(const EngineDev* __restrict__ Ep, const sac_replay& rb,
+                                                         const int32_t* __restrict__ inj_idx_,
+                                                         const float* __restrict__ inj_eps_) {
+  PREFETCH_ARG(Ep);
+  const AS_C EngineDev& E = *(const AS_C EngineDev*)Ep;
+  extern __shared__ float lds_raw[];
+  lf* lds = (lf*)lds_raw;
+  constexpr int R = SAC_ROWS, HH = SPLIT_HH;
+  constexpr int KC = MM<T>::KC;
+  constexpr int HC0 = 64 / KC;         // layer 0: chunks held (the rest streams)
+  constexpr int NCH_H = SPLIT_H / KC;  // layer 1 reduction
+  constexpr int NCH_HH = HH / KC;      // layer 1 dX reduction of a half
+  const int tid = threadIdx.x;
+  const int n2 = 2 * E.nrt;
+  const int grp = (int)blockIdx.x / n2, idx = (int)blockIdx.x % n2;
+  const int h = idx & 1, rbi = idx >> 1;
+  // roles in producer-first order: 0 pi(s'), 1/2 target critics, 3/4 critics, 5 pi(s)
+  const int role = grp;
+  const bool is_pi = role == 0 || role == 5;
+  const int ni = is_pi ? NET_PI : role <= 2 ? NET_Q1T + role - 1 : NET_Q1 + role - 3;
+  const AS_C NetDev& net = E.net[ni];
+  const AS_C LayerDev& L0 = net.l[0];
+  const AS_C LayerDev& L1 = net.l[1];
+  const AS_C LayerDev& L2 = net.l[2];
+  STAMP(0);
+  // this role's weights, issued first: layer 0 (first HC0 chunks) and the half of layer 1
+  const GemmW w0 = gw_fwd(L0);
+  const GemmW w1 = gw_sub<T>(L1.Wc, L1.Kp, h * HH, HH, 0, L1.Kp, L1.bias + h * HH, HH);
+  HTiles<T, 2, HC0> h0;
+  HTiles<T, 1, NCH_H> h1;
+  ht_issue<T, 2, HC0>(h0, w0);
+  ht_issue<T, 1, NCH_H>(h1, w1);
+
+  const int B = E.B, Bp = E.Bp, O = E.O, A = E.A, ld = E.ld, ldo = E.ldo;
+  const int r0 = rbi * R;
+  const int nvalid = min(R, B - r0);
+  const uint32_t ep = *GPC(uint32_t, E.sync) + 1u;
+  const AS_G int32_t* inj_idx = GPC(int32_t, inj_idx_);
+  const AS_G float* inj_eps = GPC(float, inj_eps_);
+  lf* Xb = lds + E.o_X;           // layer-0 input [R][ld]; later dY0 partial
+  lf* H0 = lds + E.o_Y;           // h0 [R][ld]
+  lf* P0 = lds + E.o_P1[0];       // layer-0 pre-activation [R][ldp1[0]]
+  lf* P1 = lds + E.o_P1[1];       // layer-1 half pre-activation
+  lf* H1 = lds + E.o_P2[0];       // h1 half [R][ldp2[0]]
+  lf* U1 = lds + E.o_P2[1];       // critics: unit-seed dY1 half
+  const int ldp0 = E.ldp1[0], ldp1 = E.ldp1[1], ldh1 = E.ldp2[0], ldu1 = E.ldp2[1];
+  lf* outB = lds + E.o_out;       // layer-2 partial [R][ldo]
+  lf* red = lds + E.o_red;        // k-split partials
+  lf* sB = lds + E.o_s;
+  lf* s2B = lds + E.o_s2;
+  lf* aB = lds + E.o_a;
+  lf* a2B = lds + E.o_a2;
+  lf* rB = lds + E.o_r;
+  lf* dB = lds + E.o_d;
+  lf* epsB = lds + E.o_et;
+  lf* lpB = lds + E.o_lp;
+  lf* qtB = lds + E.o_qt;
+  AS_L int64_t* slotB = (AS_L int64_t*)(lds + E.o_slot);
+  AS_G float* stats = GP(float, E.stats);
+
+  const uint64_t step = *GPC(uint64_t, E.rng_step);
+  const int par = (int)(step & 1);
+  if (role == 0 && rbi == 0 && h == 0 && tid < 4 && (tid < 3 || E.auto_entropy)) {
+    // optimizer step counters and this step's Adam bias corrections (torch adam.py)
+    const double t = GP(double, E.opt_steps)[tid] + 1.0;
+    GP(double, E.opt_steps)[tid] = t;
+    if (tid < 3) {
+      const double lr = tid == 0 ? E.actor_lr : E.critic_lr;
+      GP(float, E.adam_sc)[par * 6 + tid * 2] = (float)(-(lr / (1.0 - pow((double)E.beta1, t))));
+      GP(float, E.adam_sc)[par * 6 + tid * 2 + 1] = (float)sqrt(1.0 - pow((double)E.beta2, t));
+    } else {
+      GP(double, E.alpha_sc)[par * 2] = 1.0 - pow((double)E.beta1, t);
+      GP(double, E.alpha_sc)[par * 2 + 1] = 1.0 - pow((double)E.beta2, t);
+    }
+  }
+  // ---- sample (replay_buffer.py:32-39) + gather (agent.py:166-193): the staged record or a gather
+  const int64_t rb_size = GPC(int64_t, rb.state)[0], rb_pos = GPC(int64_t, rb.state)[1];
+  bool staged = false;
+  if (E.stage && !inj_idx) {
+    const AS_G float* rec = GPC(float, E.stg) + (size_t)rbi * E.stg_stride;
+    const AS_C uint64_t* hdr = (const AS_C uint64_t*)rec;
+    const AS_G float* p = rec + 16;
+    for (int i = tid; i < R * O; i += SAC_THREADS) {
+      sB[i] = p[i];
+      s2B[i] = p[R * O + i];
+    }
+    for (int i = tid; i < R * A; i += SAC_THREADS) aB[i] = p[2 * R * O + i];
+    if (tid < R) {
+      rB[tid] = p[2 * R * O + R * A + tid];
+      dB[tid] = p[2 * R * O + R * A + R + tid];
+    }
+    staged = hdr[0] == step && hdr[1] == (uint64_t)rb_size && hdr[2] == (uint64_t)rb_pos &&
+             hdr[3] == (uint64_t)(uintptr_t)rb.obs && hdr[4] == (uint64_t)GPC(int64_t, rb.state)[2];
+  }
+  if (staged && rbi == 0 && role == 0 && h == 0 && tid == 0)
+    *(AS_G uint64_t*)(GP(uint32_t, E.sync) + 4) = step;  // SYNC_STAGED (tests)
+  if (!staged) {  // uniform
+    tile_slots(E, rb, step, rb_size, rb_pos, r0, inj_idx, slotB);
+    __syncthreads();
+    gather_rows<lf*>(rb, slotB, O, A, sB, s2B, aB, rB, dB);
+  }
+  // eps: the target draw (which = 0) for the roles that evaluate pi's head on s'
+  // (target critics), the actor draw (which = 1) for pi(s)
+  if (role == 1 || role == 2 || role == 5) {
+    const int which = role == 5 ? 1 : 0;
+    const int NP = (A + 1) / 2;
+    for (int i = tid; i < R * NP; i += SAC_THREADS) {
+      const int r = i / NP, pp = i % NP, b = r0 + r;
+      float e0 = 0.f, e1 = 0.f;
+      if (b < B) {
+        if (inj_eps) {
+          e0 = inj_eps[((size_t)which * B + b) * A + 2 * pp];
+          if (2 * pp + 1 < A) e1 = inj_eps[((size_t)which * B + b) * A + 2 * pp + 1];
+        } else {
+          philox_normal2(E.seed, step, (uint32_t)b, (uint32_t)which, (uint32_t)pp, e0, e1);
+        }
+      }
+      epsB[r * A + 2 * pp] = e0;
+      if (2 * pp + 1 < A) epsB[r * A + 2 * pp + 1] = e1;
+    }
+  }
+  __syncthreads();
+  STAMP(1);
+
+  // pi's squashed-Gaussian head (models.py:79-87) from two layer-2 partials:
+  // o = p0 + p1 + b2 (same order in every consumer), one lane per (row, dim)
+  auto head = [&](const AS_G uint64_t* g0, const AS_G uint64_t* g1, bool tgt, lf* actB, lf* lpOut, bool stash) {
+    const AS_C NetDev& pn = E.net[NET_PI];
+    const AS_G float* b2 = GPC(float, pn.l[2].bias);
+    const int AP = A <= 1 ? 1 : 1 << (32 - __builtin_clz(A - 1));
+    const int rpp = SAC_THREADS / AP;
+    for (int base = 0; base < R; base += rpp) {
+      const int r = base + tid / AP, j = tid % AP;
+      const bool live = r < R && j < A;
+      float lp = 0.f, corr = 0.f;
+      if (live) {
+        float mu, lsr;
+        if (tgt) {
+          mu = (gran_get(E, g0 + r * 2 * A + j, ep) + gran_get(E, g1 + r * 2 * A + j, ep)) + b2[j];
+          lsr = (gran_get(E, g0 + r * 2 * A + A + j, ep) + gran_get(E, g1 + r * 2 * A + A + j, ep)) + b2[A + j];
+        } else {  // g0 / g1 = this half's own partial (in outB) and the peer's granules, in half order
+          const float pown0 = outB[r * ldo + j], pown1 = outB[r * ldo + A + j];
+          const float ppe0 = gran_get(E, g1 + r * 2 * A + j, ep), ppe1 = gran_get(E, g1 + r * 2 * A + A + j, ep);
+          mu = (h == 0 ? pown0 + ppe0 : ppe0 + pown0) + b2[j];
+          lsr = (h == 0 ? pown1 + ppe1 : ppe1 + pown1) + b2[A + j];
+        }
+        const float e = epsB[r * A + j];
+        const float lo = E.ls_min, hi = E.ls_max;
+        const float ls = lsr < lo ? lo : (lsr > hi ? hi : lsr);
+        const float sd = expf(ls);
+        const float z = mu + e * sd;
+        const float act_v = tanhf(z) * E.scale;
+        const float diff = z - mu;
+        const float var = sd * sd;
+        lp = -(diff * diff) / (2.f * var) - logf(sd) - HALF_LOG_2PI;
+        corr = 2.f * ((LOG2F - z) - softplus20(-2.f * z));
+        actB[r * A + j] = act_v;
+        if (stash) {
+          const int b = r0 + r;
+          AS_G float* hs = GP(float, E.head_st) + (size_t)b * 4 * A;
+          hs[j] = mu;
+          hs[A + j] = lsr;
+          hs[2 * A + j] = z;
+          hs[3 * A + j] = e;
+          GP(float, E.a_st)[(size_t)b * A + j] = act_v;
+        }
+      }
+      for (int o = 1; o < AP; o <<= 1) {
+        lp += __shfl_xor(lp, o, 64);
+        corr += __shfl_xor(corr, o, 64);
+      }
+      if (live && j == 0) lpOut[r] = lp - corr;
+    }
+    __syncthreads();
+  };
+
+  // ---- layer 0 (full) and layer 1 (this half) forward: H0, H1 in LDS; P0 / P1 kept
+  auto forward01 = [&](bool keepP, bool stXT, bool pi_actor) {
+    // layer 0: X [R][Kp0] -> P0 / H0 [R][H]
+    const int act = net.hid_act;
+    gemm_hs<T, 2, HC0>(Xb, ld, w0, &h0, [&](int j, int col, const f32x4& acc) {
+      const bool nv = col < L0.N;
+      const float bn = h0.b[j];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int r = (((threadIdx.x & 63) >> 4) << 2) + i;
+        const float p = nv ? acc[i] + bn : 0.f;
+        if (keepP) P0[r * ldp0 + col] = p;
+        H0[r * ld + col] = act == ACT_RELU ? (p > 0.f ? p : 0.f) : p;
+      }
+    });
+    if (act != ACT_RELU && act != ACT_ID) act_pass_fwd<R>(H0, ld, L0.Np >> 4, act);
+    __syncthreads();
+    if (pi_actor && h == 0) {  // pi's layer-0 pre-activations for phase C's relu masks
+      AS_G float* ps = GP(float, L0.pstash) + (size_t)r0 * L0.Np;
+      for (int i = tid; i < R * L0.Np; i += SAC_THREADS) ps[i] = P0[(i / L0.Np) * ldp0 + i % L0.Np];
+    }
+    if (stXT && h == 0)
+      store_T<T, R>(H0, ld, L1.Kp, L1.K, (T*)L1.XT + (pi_actor ? par * L1.xt_par : 0), Bp, r0, nvalid, nullptr);
+    STAMP(2);
+    // layer 1, this half: H0 -> P1 / H1 [R][HH]
+    gemm_hs<T, 1, NCH_H>(H0, ld, w1, &h1, [&](int j, int col, const f32x4& acc) {
+      const float bn = h1.b[j];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int r = (((threadIdx.x & 63) >> 4) << 2) + i;
+        const float p = acc[i] + bn;
+        if (keepP) P1[r * ldp1 + col] = p;
+        H1[r * ldh1 + col] = act == ACT_RELU ? (p > 0.f ? p : 0.f) : p;
+      }
+    });
+    if (act != ACT_RELU && act != ACT_ID) act_pass_fwd<R>(H1, ldh1, HH >> 4, act);
+    __syncthreads();
+    if (pi_actor) {  // this half's layer-1 pre-activations
+      AS_G float* ps = GP(float, L1.pstash) + (size_t)r0 * L1.Np + h * HH;
+      for (int i = tid; i < R * HH; i += SAC_THREADS) ps[(i / HH) * L1.Np + i % HH] = P1[(i / HH) * ldp1 + i % HH];
+    }
+    if (stXT)  // layer 2's input, this half's rows of X^T
+      store_T<T, R>(H1, ldh1, HH, HH, (T*)L2.XT + (pi_actor ? par * L2.xt_par : 0) + (size_t)h * HH * Bp, Bp, r0,
+                    nvalid, nullptr);
+    STAMP(3);
+    // layer 2, this half's partial sum: outB [R][Np2]
+    const GemmW w2 = gw_sub<T>(L2.Wc, L2.Kp, 0, L2.Np, h * HH, HH, nullptr, 0);
+    GemmW w2n = w2;
+    w2n.NT = (L2.N + 15) >> 4;  // output tiles that hold data
+    gemm_ksplit<T>(H1, ldh1, w2n, red, outB, ldo);
+    STAMP(4);
+  };
+
+  // X = [s or s', a or a'] (zero padded to Kp0)
+  auto build_x = [&](const lf* st, const lf* ac, int na) {
+    const int Kp0 = L0.Kp;
+    for (int i = tid; i < R * Kp0; i += SAC_THREADS) {
+      const int r = i / Kp0, k = i % Kp0;
+      Xb[r * ld + k] = k < O ? st[r * O + k] : (k < O + na ? ac[r * A + (k - O)] : 0.f);
+    }
+    __syncthreads();
+  };
+
+  const float alpha32 = (float)*GPC(double, E.alpha_state + 1);
+  if (role == 0) {
+    // ---- pi(s'): the critical path's head
+    build_x(s2B, aB, 0);
+    forward01(false, false, false);
+    AS_G uint64_t* g = gs_at(E, GS_PI, rbi, h);
+    for (int i = tid; i < R * 2 * A; i += SAC_THREADS) gran_put(g + i, outB[(i / (2 * A)) * ldo + i % (2 * A)], ep);
+    STAMP(6);
+  } else if (role == 5) {
+    // ---- pi(s): the actor sample for phase C (stashes), X^T of pi's layers
+    if (h == 0)
+      for (int i = tid; i < R * O; i += SAC_THREADS) GP(float, E.s_st)[(size_t)r0 * O + i] = sB[i];
+    build_x(sB, aB, 0);
+    // layer-0 input X^T: both halves store it (columns h Bp + r0: the partial dW layout)
+    store_T<T, R>(Xb, ld, L0.Kp, L0.K, (T*)L0.XT + par * L0.xt_par, 2 * Bp, h * Bp + r0, nvalid, nullptr);
+    forward01(true, true, true);
+    AS_G uint64_t* g = gs_at(E, GS_PS, rbi, h);
+    for (int i = tid; i < R * 2 * A; i += SAC_THREADS) gran_put(g + i, outB[(i / (2 * A)) * ldo + i % (2 * A)], ep);
+    head(nullptr, gs_at(E, GS_PS, rbi, 1 - h), false, a2B, lpB, h == 0);
+    if (h == 0 && tid < nvalid) {
+      const int b = r0 + tid;
+      GP(float, E.lp_st)[par * E.Br + b] = lpB[tid];
+      stats[4 + B + b] = lpB[tid];
+    }
+    STAMP(6);
+  } else if (role == 1 || role == 2) {
+    // ---- target critic t (agent.py:195-211): a~', log pi' from pi(s')'s two partials
+    const int t = role - 1;
+    head(gs_at(E, GS_PI, rbi, 0), gs_at(E, GS_PI, rbi, 1), true, a2B, lpB, false);
+    if (t == 0 && h == 0 && tid < R) gran_put(gs_at(E, GS_LP, rbi, 0) + tid, lpB[tid], ep);
+    STAMP(7);
+    build_x(s2B, a2B, A);
+    forward01(false, false, false);
+    if (tid < R) gran_put(gs_at(E, t ? GS_QT2 : GS_QT1, rbi, h) + tid, outB[tid * ldo], ep);
+    STAMP(9);
+  } else {
+    // ---- critic qi (agent.py:213-236): forward, unit-seed backward, seed once y is known
+    const int qi = role - 3;
+    // layer 1's dX operand for this half (rows k all, reduction over this half's n), held
+    const GemmW wt1 = gw_sub<T>(L1.WTc, L1.Np, 0, L1.Kp, h * HH, HH, nullptr, 0);
+    HTiles<T, 2, NCH_HH> ht1;
+    build_x(sB, aB, A);
+    // layer-0 input X^T is shared by Q1 and Q2: Q1's halves store it (columns h Bp + r0)
+    if (qi == 0) store_T<T, R>(Xb, ld, L0.Kp, L0.K, L0.XT, 2 * Bp, h * Bp + r0, nvalid, nullptr);
+    forward01(true, true, false);
+    ht_issue<T, 2, NCH_HH>(ht1, wt1);  // h1's registers are free now
+    if (tid < R) gran_put(gs_at(E, qi ? GS_QA2 : GS_QA1, rbi, h) + tid, outB[tid * ldo], ep);
+    // unit-seed backward (every layer's dY is linear in the row's seed 2(q - y)/B):
+    // U1[r][n] = act'(P1[r][n]) * W2[0][h HH + n];  U0p = act'(P0) * (U1 W1[half])
+    {
+      const AS_G float* w2row = GPC(float, net.P + L2.w_off) + h * HH;  // W2 [1][H] fp32 master
+      for (int i = tid; i < R * HH; i += SAC_THREADS) {
+        const int r = i / HH, n = i % HH;
+        U1[r * ldu1 + n] = act_bwd(net.hid_act, P1[r * ldp1 + n], w2row[n]);
+      }
+      __syncthreads();
+      gemm_hs<T, 2, NCH_HH>(U1, ldu1, wt1, &ht1, [&](int j, int col, const f32x4& acc) {
+        const bool kv = col < L1.K;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int r = (((threadIdx.x & 63) >> 4) << 2) + i;
+          float v = kv ? acc[i] : 0.f;
+          if (net.hid_act == ACT_RELU && !(P0[r * ldp0 + col] > 0.f)) v = 0.f;
+          Xb[r * ld + col] = v;  // U0 partial
+        }
+      });
+      if (net.hid_act != ACT_RELU && net.hid_act != ACT_ID)
+        act_pass_bwd<R>(Xb, ld, P0, ldp0, L1.Kp >> 4, L1.K, net.hid_act);
+      __syncthreads();
+    }
+    STAMP(16);
+    if (tid < 64) {  // wave 0: q, y, loss partial, seed dL/dq = 2(q - y)/B  (mse_loss backward)
+      float sq = 0.f;
+      if (tid < R) {
+        const int b = r0 + tid;
+        const bool v = tid < nvalid;
+        const float b2 = GPC(float, L2.bias)[0];
+        const float mine = outB[tid * ldo];
+        const float peer = gran_get(E, gs_at(E, qi ? GS_QA2 : GS_QA1, rbi, 1 - h) + tid, ep);
+        const float qpre = (h == 0 ? mine + peer : peer + mine) + b2;
+        const float q = net.out_act == ACT_ID ? qpre : act_fwd(net.out_act, qpre);
+        const AS_C NetDev& t1 = E.net[NET_Q1T];
+        const AS_C NetDev& t2 = E.net[NET_Q2T];
+        const float q1tp = gran_get(E, gs_at(E, GS_QT1, rbi, 0) + tid, ep) +
+                           gran_get(E, gs_at(E, GS_QT1, rbi, 1) + tid, ep) + GPC(float, t1.l[2].bias)[0];
+        const float q2tp = gran_get(E, gs_at(E, GS_QT2, rbi, 0) + tid, ep) +
+                           gran_get(E, gs_at(E, GS_QT2, rbi, 1) + tid, ep) + GPC(float, t2.l[2].bias)[0];
+        const float q1t = t1.out_act == ACT_ID ? q1tp : act_fwd(t1.out_act, q1tp);
+        const float q2t = t2.out_act == ACT_ID ? q2tp : act_fwd(t2.out_act, q2tp);
+        const float lp2 = gran_get(E, gs_at(E, GS_LP, rbi, 0) + tid, ep);
+        const float y = rB[tid] + (E.gamma * (1.f - dB[tid])) * (fmin_nan(q1t, q2t) - alpha32 * lp2);
+        if (qi == 0 && h == 0 && b < B) stats[4 + b] = y;
+        const float d = q - y;
+        sq = v ? d * d : 0.f;
+        float seed = v ? (2.0f / (float)B) * d : 0.f;
+        if (net.out_act != ACT_ID) seed = act_bwd(net.out_act, qpre, seed);
+        qtB[tid] = seed;
+      }
+      sq = wave_sum(sq);
+      if (tid == 0 && h == 0) GP(float, E.lossp)[(par * E.nrt + rbi) * 4 + qi] = sq;
+    }
+    __syncthreads();
+    STAMP(15);
+    // dY^T of every layer (seed x unit dY) + bias partials for phase B
+    if (h == 0) {  // layer 2: dY2 = seed (N = 1)
+      lf* g2 = outB;
+      for (int i = tid; i < R * 32; i += SAC_THREADS) g2[(i / 32) * ldo + i % 32] = (i % 32) == 0 ? 1.f : 0.f;
+      __syncthreads();
+      store_T<T, R>(g2, ldo, L2.Np, L2.N, L2.GT, Bp, r0, nvalid, L2.dbp, qtB);
+    }
+    store_T<T, R>(U1, ldu1, HH, HH, (T*)L1.GT + (size_t)h * HH * Bp, Bp, r0, nvalid, L1.dbp + h * HH, qtB, L1.N);
+    store_T<T, R>(Xb, ld, L0.Np, L0.N, L0.GT, 2 * Bp, h * Bp + r0, nvalid, L0.dbp, qtB);
+    STAMP(11 + 2 * qi);
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(SAC_THREADS) sac_target_critic_split(const EngineDev* __restrict__ Ep, sac_replay rb,
+                                                                        const int32_t* __restrict__ inj_idx_,
+                                                                        const float* __restrict__ inj_eps_) {
+  target_critic_split_body<T>(Ep, rb, inj_idx_, inj_eps_);
+  const AS_C EngineDev& E = *(const AS_C EngineDev*)Ep;
+  (void)E;
+  END_STAMP(60);
+}
+
+// ---------------------------------------------------------------------------- phase C
+template <typename T>
+__device__ __forceinline__ void actor_split_body(const EngineDev* __restrict__ Ep, int bid) {
+  const AS_C EngineDev& E = *(const AS_C EngineDev*)Ep;
+  extern __shared__ float lds_raw[];
+  lf* lds = (lf*)lds_raw;
+  constexpr int R = SAC_ROWS, HH = SPLIT_HH;
+  constexpr int KC = MM<T>::KC;
+  constexpr int HC0 = 64 / KC;
+  constexpr int NCH_H = SPLIT_H / KC;
+  constexpr int NCH_HH = HH / KC;
+  constexpr int NCH_32 = 32 / KC;
+  const int tid = threadIdx.x;
+  const int n2 = 2 * E.nrt;
+  const int grp = bid / n2, idx = bid % n2;
+  const int h = idx & 1, rbi = idx >> 1;
+  // producers first: groups 0 / 1 the critics, group 2 pi
+  const bool is_pi = grp == 2;
+  const int qi = grp;  // critics
+  STAMP(32);
+  const int B = E.B, Bp = E.Bp, O = E.O, A = E.A, ld = E.ld, ldo = E.ldo;
+  const int r0 = rbi * R;
+  const int nvalid = min(R, B - r0);
+  const uint32_t ep = *GPC(uint32_t, E.sync) + 1u;
+  const int par = (int)(*GPC(uint64_t, E.rng_step) & 1);
+  lf* Xb = lds + E.o_X;
+  lf* H0 = lds + E.o_Y;
+  lf* P0 = lds + E.o_P1[0];
+  lf* P1 = lds + E.o_P1[1];
+  lf* H1 = lds + E.o_P2[0];
+  lf* U1 = lds + E.o_P2[1];
+  const int ldp0 = E.ldp1[0], ldp1 = E.ldp1[1], ldh1 = E.ldp2[0], ldu1 = E.ldp2[1];
+  lf* outB = lds + E.o_out;
+  lf* red = lds + E.o_red;
+  lf* sB = lds + E.o_s;
+  lf* aB = lds + E.o_a;
+  lf* lpB = lds + E.o_lp;
+  lf* gaB = lds + E.o_ga;
+  lf* goutB = lds + E.o_gout;
+  lf* g1B = lds + E.o_g;
+  lf* g2B = lds + E.o_g2;
+  const float alpha32 = (float)*GPC(double, E.alpha_state + 1);
+
+  if (!is_pi) {
+    // ---- critic qi on (s, a~) with the UPDATED weights (agent.py:244-248), then d Q / d a~
+    const AS_C NetDev& net = E.net[NET_Q1 + qi];
+    const AS_C LayerDev& L0 = net.l[0];
+    const AS_C LayerDev& L1 = net.l[1];
+    const AS_C LayerDev& L2 = net.l[2];
+    const GemmW w0 = gw_fwd(L0);
+    const GemmW w1 = gw_sub<T>(L1.Wc, L1.Kp, h * HH, HH, 0, L1.Kp, L1.bias + h * HH, HH);
+    HTiles<T, 2, HC0> h0;
+    HTiles<T, 1, NCH_H> h1;
+    ht_issue<T, 2, HC0>(h0, w0);
+    ht_issue<T, 1, NCH_H>(h1, w1);
+    for (int i = tid; i < R * O; i += SAC_THREADS) sB[i] = GPC(float, E.s_st)[(size_t)r0 * O + i];
+    for (int i = tid; i < R * A; i += SAC_THREADS) aB[i] = GPC(float, E.a_st)[(size_t)r0 * A + i];
+    __syncthreads();
+    const int Kp0 = L0.Kp;
+    for (int i = tid; i < R * Kp0; i += SAC_THREADS) {
+      const int r = i / Kp0, k = i % Kp0;
+      Xb[r * ld + k] = k < O ? sB[r * O + k] : (k < O + A ? aB[r * A + (k - O)] : 0.f);
+    }
+    __syncthreads();
+    STAMP(33);
+    const int act = net.hid_act;
+    gemm_hs<T, 2, HC0>(Xb, ld, w0, &h0, [&](int j, int col, const f32x4& acc) {
+      const bool nv = col < L0.N;
+      const float bn = h0.b[j];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int r = (((threadIdx.x & 63) >> 4) << 2) + i;
+        const float p = nv ? acc[i] + bn : 0.f;
+        P0[r * ldp0 + col] = p;
+        H0[r * ld + col] = act == ACT_RELU ? (p > 0.f ? p : 0.f) : p;
+      }
+    });
+    if (act != ACT_RELU && act != ACT_ID) act_pass_fwd<R>(H0, ld, L0.Np >> 4, act);
+    __syncthreads();
+    gemm_hs<T, 1, NCH_H>(H0, ld, w1, &h1, [&](int j, int col, const f32x4& acc) {
+      const float bn = h1.b[j];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int r = (((threadIdx.x & 63) >> 4) << 2) + i;
+        const float p = acc[i] + bn;
+        P1[r * ldp1 + col] = p;
+        H1[r * ldh1 + col] = act == ACT_RELU ? (p > 0.f ? p : 0.f) : p;
+      }
+    });
+    if (act != ACT_RELU && act != ACT_ID) act_pass_fwd<R>(H1, ldh1, HH >> 4, act);
+    __syncthreads();
+    // layer-1 dX operand of this half, issued now (h1's registers are free)
+    const GemmW wt1 = gw_sub<T>(L1.WTc, L1.Np, 0, L1.Kp, h * HH, HH, nullptr, 0);
+    HTiles<T, 2, NCH_HH> ht1;
+    ht_issue<T, 2, NCH_HH>(ht1, wt1);
+    {
+      GemmW w2 = gw_sub<T>(L2.Wc, L2.Kp, 0, L2.Np, h * HH, HH, nullptr, 0);
+      w2.NT = (L2.N + 15) >> 4;
+      gemm_ksplit<T>(H1, ldh1, w2, red, outB, ldo);  // partial q
+    }
+    STAMP(36 + qi);
+    // unit-seed backward down to a~ (the pi role applies the min-Q weights and act'(q))
+    {
+      const AS_G float* w2row = GPC(float, net.P + L2.w_off) + h * HH;
+      for (int i = tid; i < R * HH; i += SAC_THREADS) {
+        const int r = i / HH, n = i % HH;
+        U1[r * ldu1 + n] = act_bwd(act, P1[r * ldp1 + n], w2row[n]);
+      }
+      __syncthreads();
+      gemm_hs<T, 2, NCH_HH>(U1, ldu1, wt1, &ht1, [&](int j, int col, const f32x4& acc) {
+        const bool kv = col < L1.K;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int r = (((threadIdx.x & 63) >> 4) << 2) + i;
+          float v = kv ? acc[i] : 0.f;
+          if (act == ACT_RELU && !(P0[r * ldp0 + col] > 0.f)) v = 0.f;
+          Xb[r * ld + col] = v;
+        }
+      });
+      if (act != ACT_RELU && act != ACT_ID) act_pass_bwd<R>(Xb, ld, P0, ldp0, L1.Kp >> 4, L1.K, act);
+      __syncthreads();
+      // dX of layer 0 for the action columns: the 16-row tiles of W0^T holding [O, O + A)
+      const int k0 = (O >> 4) << 4, k1 = (O + A + 15) >> 4 << 4;
+      GemmW wt0 = gw_sub<T>(L0.WTc, L0.Np, k0, k1 - k0, 0, L0.Np, nullptr, 0);
+      gemm_ksplit<T>(Xb, ld, wt0, red, H0, ld);  // H0 [R][k1 - k0]: partial dX0
+      AS_G uint64_t* g = gs_at(E, GS_C1 + qi, rbi, h);
+      for (int i = tid; i < R * A; i += SAC_THREADS) gran_put(g + i, H0[(i / A) * ld + (O - k0) + i % A], ep);
+      if (tid < R) gran_put(g + R * A + tid, outB[tid * ldo], ep);
+    }
+    STAMP(38 + qi);
+    return;
+  }
+
+  // ---- pi half h: head backward + pi backward (agent.py:251-257)
+  const AS_C NetDev& pi = E.net[NET_PI];
+  const AS_C LayerDev& L0 = pi.l[0];
+  const AS_C LayerDev& L1 = pi.l[1];
+  const AS_C LayerDev& L2 = pi.l[2];
+  // operands: layer 2's dX (rows = this half's n, reduction over 2A -> 32),
+  // layer 1's dX (rows k all, reduction over this half's n), both held
+  const GemmW wt2 = gw_sub<T>(L2.WTc, L2.Np, h * HH, HH, 0, L2.Np, nullptr, 0);
+  const GemmW wt1 = gw_sub<T>(L1.WTc, L1.Np, 0, L1.Kp, h * HH, HH, nullptr, 0);
+  HTiles<T, 1, NCH_32> ht2;
+  HTiles<T, 2, NCH_HH> ht1;
+  ht_issue<T, 1, NCH_32>(ht2, wt2);
+  ht_issue<T, 2, NCH_HH>(ht1, wt1);
+  {  // relu masks: pi's pre-activations stashed by phase A's pi(s) role
+    const AS_G float* p0 = GPC(float, L0.pstash) + (size_t)r0 * L0.Np;
+    for (int i = tid; i < R * L0.Np; i += SAC_THREADS) P0[(i / L0.Np) * ldp0 + i % L0.Np] = p0[i];
+    const AS_G float* p1 = GPC(float, L1.pstash) + (size_t)r0 * L1.Np + h * HH;
+    for (int i = tid; i < R * HH; i += SAC_THREADS) P1[(i / HH) * ldp1 + i % HH] = p1[(i / HH) * L1.Np + i % HH];
+    if (tid < R) lpB[tid] = GPC(float, E.lp_st)[par * E.Br + r0 + tid];
+  }
+  __syncthreads();
+  STAMP(34);
+  // combine the critics' unit-seed partials with the min-Q weights (L_pi = mean(alpha logpi - min Q))
+  const AS_G uint64_t* c10 = gs_at(E, GS_C1, rbi, 0);
+  const AS_G uint64_t* c11 = gs_at(E, GS_C1, rbi, 1);
+  const AS_G uint64_t* c20 = gs_at(E, GS_C2, rbi, 0);
+  const AS_G uint64_t* c21 = gs_at(E, GS_C2, rbi, 1);
+  if (tid < 64) {
+    float term = 0.f;
+    if (tid < R) {
+      const bool v = tid < nvalid;
+      const AS_C NetDev& q1n = E.net[NET_Q1];
+      const AS_C NetDev& q2n = E.net[NET_Q2];
+      const float q1p = gran_get(E, c10 + R * A + tid, ep) + gran_get(E, c11 + R * A + tid, ep) +
+                        GPC(float, q1n.l[2].bias)[0];
+      const float q2p = gran_get(E, c20 + R * A + tid, ep) + gran_get(E, c21 + R * A + tid, ep) +
+                        GPC(float, q2n.l[2].bias)[0];
+      const float q1 = q1n.out_act == ACT_ID ? q1p : act_fwd(q1n.out_act, q1p);
+      const float q2 = q2n.out_act == ACT_ID ? q2p : act_fwd(q2n.out_act, q2p);
+      const float m = fmin_nan(q1, q2);
+      term = v ? alpha32 * lpB[tid] - m : 0.f;
+      const float gm = v ? -1.0f / (float)B : 0.f;
+      float w1 = (q1 == q2) ? gm * 0.5f : (q1 > q2 ? 0.f : gm);
+      float w2 = (q1 == q2) ? gm * 0.5f : (q1 < q2 ? 0.f : gm);
+      if (q1n.out_act != ACT_ID) w1 = act_bwd(q1n.out_act, q1p, w1);
+      if (q2n.out_act != ACT_ID) w2 = act_bwd(q2n.out_act, q2p, w2);
+      g1B[tid] = w1;
+      g2B[tid] = w2;
+    }
+    term = wave_sum(term);
+    if (tid == 0 && h == 0) GP(float, E.lossp)[(par * E.nrt + rbi) * 4 + 2] = term;
+  }
+  __syncthreads();
+  for (int i = tid; i < R * A; i += SAC_THREADS) {
+    const int r = i / A;
+    const float da1 = gran_get(E, c10 + i, ep) + gran_get(E, c11 + i, ep);
+    const float da2 = gran_get(E, c20 + i, ep) + gran_get(E, c21 + i, ep);
+    gaB[i] = g1B[r] * da1 + g2B[r] * da2;
+  }
+  __syncthreads();
+  STAMP(39);
+  // squashed-Gaussian head backward (models.py:79-87), one lane per (row, action dim)
+  for (int i = tid; i < R * A; i += SAC_THREADS) {
+    const int r = i / A, j = i % A, b = r0 + r;
+    const bool v = r < nvalid;
+    const float gl = v ? alpha32 * (1.0f / (float)B) : 0.f;
+    const AS_G float* hs = GPC(float, E.head_st) + (size_t)b * 4 * A;
+    const float lo = E.ls_min, hi = E.ls_max, scale = E.scale;
+    const float mu = hs[j], lsr = hs[A + j], z = hs[2 * A + j], e = hs[3 * A + j];
+    const float ls = lsr < lo ? lo : (lsr > hi ? hi : lsr);
+    const float sd = expf(ls);
+    const float t = tanhf(z);
+    const float diff = z - mu, var = sd * sd;
+    float g_z = (gaB[r * A + j] * scale) * (1.f - t * t);
+    g_z = g_z + (-gl) * 2.f * (-1.f + 2.f * softplus20_grad(-2.f * z));
+    const float two_var = 2.f * var;
+    const float g_sq = -gl / two_var;
+    const float g_twovar = gl * (diff * diff) / (two_var * two_var);
+    const float g_var = 2.f * g_twovar;
+    float g_std = 2.f * sd * g_var - gl / sd;
+    const float g_diff = 2.f * diff * g_sq;
+    g_z = g_z + g_diff;
+    const float g_mu = -g_diff + g_z;
+    g_std = g_std + g_z * e;
+    const float g_ls = g_std * sd;
+    const bool in_range = (lsr >= lo) && (lsr <= hi);
+    goutB[r * ldo + j] = v ? g_mu : 0.f;
+    goutB[r * ldo + A + j] = (v && in_range) ? g_ls : 0.f;
+  }
+  {
+    const int NOp = L2.Np, pad = NOp - 2 * A;
+    for (int i = tid; i < R * pad; i += SAC_THREADS) goutB[(i / pad) * ldo + 2 * A + i % pad] = 0.f;
+  }
+  __syncthreads();
+  // layer 2 dY^T (= dOut) + bias partials: half 0
+  if (h == 0) store_T<T, R>(goutB, ldo, L2.Np, L2.N, L2.GT, Bp, r0, nvalid, L2.dbp);
+  // dY1 (this half) = act'(P1) * (dOut W2[:, half])
+  const int act = pi.hid_act;
+  gemm_hs<T, 1, NCH_32>(goutB, ldo, wt2, &ht2, [&](int j, int col, const f32x4& acc) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r = (((threadIdx.x & 63) >> 4) << 2) + i;
+      float v = acc[i];
+      if (act == ACT_RELU && !(P1[r * ldp1 + col] > 0.f)) v = 0.f;
+      U1[r * ldu1 + col] = v;
+    }
+  });
+  if (act != ACT_RELU && act != ACT_ID) act_pass_bwd<R>(U1, ldu1, P1, ldp1, HH >> 4, HH, act);
+  __syncthreads();
+  store_T<T, R>(U1, ldu1, HH, HH, (T*)L1.GT + (size_t)h * HH * Bp, Bp, r0, nvalid, L1.dbp + h * HH, nullptr, L1.N);
+  // dY0 partial = act'(P0) * (dY1 W1[half])
+  gemm_hs<T, 2, NCH_HH>(U1, ldu1, wt1, &ht1, [&](int j, int col, const f32x4& acc) {
+    const bool kv = col < L1.K;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r = (((threadIdx.x & 63) >> 4) << 2) + i;
+      float v = kv ? acc[i] : 0.f;
+      if (act == ACT_RELU && !(P0[r * ldp0 + col] > 0.f)) v = 0.f;
+      Xb[r * ld + col] = v;
+    }
+  });
+  if (act != ACT_RELU && act != ACT_ID) act_pass_bwd<R>(Xb, ld, P0, ldp0, L1.Kp >> 4, L1.K, act);
+  __syncthreads();
+  store_T<T, R>(Xb, ld, L0.Np, L0.N, L0.GT, 2 * Bp, h * Bp + r0, nvalid, L0.dbp);
+  STAMP(35);
+}
+
+template <typename T>
+__global__ void __launch_bounds__(SAC_THREADS) sac_actor_split(const EngineDev* __restrict__ Ep, sac_replay rb) {
+  PREFETCH_ARG(Ep);
+  const AS_C EngineDev& E = *(const AS_C EngineDev*)Ep;
+  extern __shared__ float lds_raw[];
+  const int bid = (int)blockIdx.x;
+  const int nrole = 6 * E.nrt;  // 3 roles x 2 halves x nrt
+  if (bid >= nrole)
+    stage_next_batch(E, rb, bid - nrole, (lf*)lds_raw);
+  else
+    actor_split_body<T>(Ep, bid);
+  phase_c_done(E);
+  END_STAMP(61);
+}

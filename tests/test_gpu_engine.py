@@ -232,6 +232,7 @@ def test_role_split_equals_fused(precision, monkeypatch):
     """Phases A/C split into per-network workgroups with in-launch hand-offs give
     the same bits as the one-workgroup-per-row-tile kernels (power-of-two batch:
     the min-Q weights are applied after a unit-seed backward, exactly)."""
+    monkeypatch.setenv("SAC_SPLIT", "0")  # the hidden-split kernels sum in another order (tested vs the oracle)
     out = {}
     for roles in ("1", "0"):
         monkeypatch.setenv("SAC_ROLES", roles)
@@ -266,6 +267,8 @@ def test_staged_batch_equals_in_step_gather(cfg, precision, fuse, monkeypatch):
     from sac import _engine as E
 
     monkeypatch.setenv("SAC_FUSE", fuse)
+    if fuse != "0":
+        monkeypatch.setenv("SAC_SPLIT", "0")  # fused layouts run the one-workgroup-per-role kernels
     out = {}
     for stage in ("1", "0"):
         monkeypatch.setenv("SAC_STAGE", stage)
@@ -298,6 +301,7 @@ def test_fused_launches_equal_four_launches(precision, layout, monkeypatch):
     """Two launches per step (phase D inside the next phase A launch, phase B
     inside the phase C launch, in-launch completion counters) give the same
     bits as four launches per step."""
+    monkeypatch.setenv("SAC_SPLIT", "0")  # fused layouts run the one-workgroup-per-role kernels
     out = {}
     for fuse in (layout, "0"):
         monkeypatch.setenv("SAC_FUSE", fuse)
@@ -490,3 +494,26 @@ def test_training_is_layout_independent(precision):
         out[layout]["stats"] = eng.stats.clone()
     for k in out["records"]:
         assert torch.equal(out["records"][k], out["soa"][k]), k
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_hidden_split_is_used_and_close_to_unsplit(lib, precision, monkeypatch):
+    """C2 runs the hidden-split role kernels (two workgroups per role and row
+    tile); 5 device-sampled steps agree with the unsplit role kernels to
+    rounding (the split only changes the summation order of layers 1-2 and of
+    layer 0's dW; both paths are checked against the oracle elsewhere)."""
+    lib.sac_engine_uses_split.argtypes = [ctypes.c_void_p]
+    out = {}
+    for split in ("1", "0"):
+        monkeypatch.setenv("SAC_SPLIT", split)
+        eng, rb, c = _engine("c2", precision, capacity=5000)
+        assert lib.sac_engine_uses_split(eng.handle) == int(split)
+        eng.train(rb, 2)
+        eng.train_graph(rb, 3, chunk=3)
+        eng.check()
+        out[split] = {k: v.clone() for k, v in eng.state_tensors().items()}
+        out[split]["losses"] = torch.tensor(eng.losses())
+    tol = 2e-5 if precision == "fp32" else 2e-3
+    for k in out["1"]:
+        a, b = out["1"][k].double(), out["0"][k].double()
+        assert torch.allclose(a, b, rtol=tol, atol=tol), (k, (a - b).abs().max().item())

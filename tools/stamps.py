@@ -37,6 +37,9 @@ n_b = 2 * _tiles([O_ + A_] + H_ + [1])
 n_d = _tiles([O_] + H_ + [2 * A_])
 # role blocks start after the update tiles in the fused launches
 OFF = {"A": n_d + 1, "C": n_b} if eng.fused else {"A": 0, "C": 0}
+lib.sac_engine_uses_split.argtypes = [ctypes.c_void_p]
+SPLIT = bool(lib.sac_engine_uses_split(eng.handle))
+GROUP = 2 * nrt if SPLIT else nrt  # blocks per role group (hidden split: two halves per row tile)
 buf = torch.zeros(nblk * 64, dtype=torch.int64, device=dev)
 E.check(lib.sac_engine_debug_stamps(eng.handle, E.ptr(buf), eng._stream()))
 eng.train(rb, 20)
@@ -70,6 +73,10 @@ names = {58: "D done", 59: "D waited",
 names.update({33: "B waited", 20: "HC8 layer entry", 21: "HC8 MFMA done (wave 0)", 22: "HC8 epilogue done",
               23: "HC8 layer end"})
 names.update({60: "END", 61: "END", 62: "END", 63: "END"})
+if SPLIT:  # sac_split.h stamps
+    names.update({2: "L0", 3: "L1 half", 4: "L2 partial", 6: "partials published", 7: "pi head (s')",
+                  9: "Qt partial published", 33: "inputs", 34: "pi inputs", 36: "Q1 fwd", 37: "Q2 fwd",
+                  38: "Q1 da partial", 39: "pi: critics combined", 35: "pi bwd + GT"})
 PH = {"A": list(range(0, 17)) + [20, 21, 22, 23, 56, 57, 59, 60],  # 20-23: free for DSTAMP probes
       "C": list(range(32, 40)) + [61], "B": [48, 49, 50, 62], "D": [52, 53, 54, 63]}
 ROLES = {"A": ["pi(s')", "Qt1", "Qt2", "Q1", "Q2", "pi(s)"], "C": ["Q1", "Q2", "pi"]}  # block-group order
@@ -89,7 +96,7 @@ for ph, ids in PH.items():
     groups = {"all": np.ones(len(blk), bool)}
     if ph in ROLES and eng.roles:
         rb_ = blk - OFF[ph]
-        groups = {nm: (rb_ >= 0) & ((rb_ // nrt) == k) for k, nm in enumerate(ROLES[ph])}
+        groups = {nm: (rb_ >= 0) & ((rb_ // GROUP) == k) for k, nm in enumerate(ROLES[ph])}
         if OFF[ph]:
             groups["upd"] = rb_ < 0
     print(f"=== phase {ph}")
@@ -128,7 +135,7 @@ for ph, ids in PH.items():
                 if ph in ROLES and eng.roles:
                     rb2 = blk_r - OFF[ph]
                     k = list(groups).index(g) if g in ROLES.get(ph, []) else -1
-                    gm = (rb2 >= 0) & ((rb2 // nrt) == k) if k >= 0 else (rb2 < 0)
+                    gm = (rb2 >= 0) & ((rb2 // GROUP) == k) if k >= 0 else (rb2 < 0)
                 v = sel_r[gm, i]
                 v = v[v > 0]
                 if v.size:
