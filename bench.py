@@ -383,9 +383,14 @@ def main():
                 "bound": "hbm", "kernel": gk, "batch": bmax,
                 "achieved": sweep["gather"][str(bmax)], "peak": PEAK_HBM_GBS, "unit": "GB/s",
                 "frac": round(sweep["gather"][str(bmax)] / PEAK_HBM_GBS, 5), "traffic": gtr,
+                "achieved_read_write": round(2 * sweep["gather"][str(bmax)], 3),
+                "frac_read_write": round(2 * sweep["gather"][str(bmax)] / PEAK_HBM_GBS, 5),
                 "traffic_source": gsrc, "bytes_per_launch": bmax * W * 4, "avg_launch_ms": ms,
                 "note": "B_gather = 4 B (2 obs + act + 2) bytes read per launch (SURVEY §8d); the kernel writes "
-                        "as many again; rows uniform with replacement over the 1e6-row buffer"}
+                        "as many again (the minibatch it returns), counted in achieved_read_write; traffic = PMC "
+                        "FETCH (x2, gfx950) + WRITE per launch: reads exceed B_gather by the record padding "
+                        "(2O+A+2 floats stored in whole 128-B lines); rows uniform with replacement over the "
+                        "1e6-row buffer"}
         if not args.no_bf16 and args.precision == "fp32" and world == 1:  # single-process leg: no barriers
             eb, rbb, _, elb, lsb = timed("bf16")
             line["value_bf16"] = round(total_steps / elb, 2)

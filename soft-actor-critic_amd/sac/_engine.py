@@ -16,6 +16,7 @@ MAX_LAYERS = 8
 PREC_FP32, PREC_BF16 = 0, 1
 
 _LIB_NAME = "libsac_engine.so"
+_OPS_NAME = "libsac_torch_ops.so"
 _PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
@@ -121,6 +122,32 @@ def load_library() -> ctypes.CDLL:
         fn.argtypes = args
     _lib = lib
     return lib
+
+
+_ops_loaded = False
+
+
+def ops_library_path() -> str:
+    return os.path.join(os.path.dirname(library_path()), _OPS_NAME)
+
+
+def ops():
+    """``torch.ops.sac_hip``: the PyTorch custom ops over the C ABI
+    (csrc/sac_torch_ops.cpp: replay_push, replay_gather, replay_sample,
+    replay_sample_gather, train_step, train_graph, policy_act).  The op library
+    links libsac_engine.so (one instance with the ctypes handle: same file, same
+    soname).  Raises EngineUnavailable when it is not built."""
+    global _ops_loaded
+    if not _ops_loaded:
+        load_library()
+        path = ops_library_path()
+        if not os.path.exists(path):
+            raise EngineUnavailable(
+                f"{path} not found: build it with `make -C soft-actor-critic_amd/csrc` "
+                "(or __graft_entry__.build()); there is no CPU fallback")
+        torch.ops.load_library(path)
+        _ops_loaded = True
+    return torch.ops.sac_hip
 
 
 def check(rc: int) -> None:

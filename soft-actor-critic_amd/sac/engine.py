@@ -127,6 +127,12 @@ class SacEngine:
         h = ctypes.c_void_p()
         E.check(self.lib.sac_engine_create(ctypes.byref(cfg), ctypes.byref(bufs), self._stream(), ctypes.byref(h)))
         self.handle = h
+        self.ops = E.ops()
+        # the caller-owned tensors the step reads and writes, sac_engine_buffers
+        # order: the mutated arguments of torch.ops.sac_hip.train_step / train_graph
+        self.state_list = [self.flat[k] for k in ("pi", "q1", "q2", "q1t", "q2t")] + [
+            t for k in ("pi", "q1", "q2") for t in (self.m[k], self.v[k])] + [
+            self.alpha_state, self.opt_steps, self.rng_step, self.stats, self.workspace]
         self.steps_done = 0
         # lazy hand-off status: an async D2H copy of the engine's status words
         # into pinned memory every STATUS_EVERY train calls, checked when it has
@@ -230,14 +236,15 @@ class SacEngine:
         """n gradient steps.  indices: [n][B] int32 logical rows; eps: [n][2][B][A]."""
         if len(replay) < self.batch:
             replay._check(self.batch)
-        desc = replay.desc
+        replay.flush()
         if indices is not None:
             indices = indices.to(self.device, torch.int32).contiguous()
         if eps is not None:
             eps = eps.to(self.device, torch.float32).contiguous()
         self._poll_status()
-        E.check(self.lib.sac_engine_train(self.handle, ctypes.byref(desc), int(n_steps), E.ptr(indices),
-                                          E.ptr(eps), self._stream()))
+        with torch.cuda.device(self.device):
+            self.ops.train_step(self.handle.value, self.state_list, replay.storage, replay.state,
+                                replay.layout_spec, int(n_steps), indices, eps)
         self._keep = (indices, eps)
         self.steps_done += n_steps
         self._after_launch()
@@ -245,24 +252,23 @@ class SacEngine:
     def train_graph(self, replay, n_steps: int, chunk: int = 32) -> None:
         if len(replay) < self.batch:
             replay._check(self.batch)
-        desc = replay.desc
+        replay.flush()
         self._poll_status()
-        E.check(self.lib.sac_engine_train_graph(self.handle, ctypes.byref(desc), int(n_steps), int(chunk),
-                                                self._stream()))
+        with torch.cuda.device(self.device):
+            self.ops.train_graph(self.handle.value, self.state_list, replay.storage, replay.state,
+                                 replay.layout_spec, int(n_steps), int(chunk))
         self.steps_done += n_steps
         if n_steps:
             self._after_launch()
 
     def policy_act(self, obs: torch.Tensor, eps: Optional[torch.Tensor] = None, want_log_pi: bool = False):
         obs = obs.to(self.device, torch.float32).contiguous()
-        n = obs.shape[0]
-        act = torch.empty(n, self.cfg.act_dim, dtype=torch.float32, device=self.device)
-        lp = torch.empty(n, dtype=torch.float32, device=self.device) if (want_log_pi and eps is not None) else None
         if eps is not None:
             eps = eps.to(self.device, torch.float32).contiguous()
-        E.check(self.lib.sac_policy_act(self.handle, E.ptr(obs), n, E.ptr(eps), E.ptr(act), E.ptr(lp),
-                                        self._stream()))
-        return (act, lp) if want_log_pi else act
+        with torch.cuda.device(self.device):
+            act, lp = self.ops.policy_act(self.handle.value, obs, eps, int(self.cfg.act_dim),
+                                          bool(want_log_pi and eps is not None))
+        return (act, lp if lp.numel() else None) if want_log_pi else act
 
     def time_phases(self, replay, n_steps: int) -> List[float]:
         """[A, B, C, D, gap]: mean hipEvent interval per phase launch (ms) and

@@ -16,12 +16,12 @@ the host and on the device, in one of two layouts (``layout=``):
 fields in both layouts.
 
 * ``push`` (replay_buffer.py:21-30) stages rows in pinned host memory; staged rows
-  are appended by one HIP kernel (``sac_replay_push``) before the next read, so an
+  are appended by one HIP kernel (``torch.ops.sac_hip.replay_push``) before the next read, so an
   env loop pays one small H2D copy per flush, not per field.
 * ``sample`` (replay_buffer.py:32-39) keeps the reference's RNG stream: indices
   come from Python ``random.sample`` over positions (oldest = 0, the deque order)
   so a seeded run selects exactly the rows the reference would; rows are gathered
-  on the device (``sac_replay_gather``) and returned as ``Transition``s.
+  on the device (``torch.ops.sac_hip.replay_gather``) and returned as ``Transition``s.
 * ``sample_tensors`` is the batched form used by ``SAC.sample_batch``: one
   Transition of device tensors.
 * The fused engine path samples on the device itself (Feistel permutation keyed
@@ -37,6 +37,7 @@ import numpy as np
 import torch
 
 from . import _engine as E
+from ._engine import ops
 
 Transition = namedtuple("Transition", ("state", "action", "reward", "next_state", "done"))
 
@@ -76,19 +77,26 @@ class ReplayBuffer:
             W = self.row_width
             self.row_stride = 16 if W <= 16 else (W + 31) // 32 * 32  # whole 64-B / 128-B lines
             self.records = torch.zeros(cap, self.row_stride, **f32)
+            self.storage = self.records.view(-1)
+            offs = [0, 2 * O, 2 * O + A, O, 2 * O + A + 1]  # obs, act, rew, next_obs, done
             self.obs = self.records[:, :O]
             self.next_obs = self.records[:, O:2 * O]
             self.act = self.records[:, 2 * O:2 * O + A]
             self.rew = self.records[:, 2 * O + A]
             self.done = self.records[:, 2 * O + A + 1]
         else:
+            # one allocation, field-major: obs[cap][O] | act[cap][A] | rew[cap] | next_obs[cap][O] | done[cap]
             self.row_stride = 0
-            self.obs = torch.zeros(cap, O, **f32)
-            self.act = torch.zeros(cap, A, **f32)
-            self.rew = torch.zeros(cap, **f32)
-            self.next_obs = torch.zeros(cap, O, **f32)
-            self.done = torch.zeros(cap, **f32)
+            self.storage = torch.zeros(cap * self.row_width, **f32)
+            offs = [0, cap * O, cap * (O + A), cap * (O + A + 1), cap * (2 * O + A + 1)]
+            self.obs = self.storage[offs[0]:offs[1]].view(cap, O)
+            self.act = self.storage[offs[1]:offs[2]].view(cap, A)
+            self.rew = self.storage[offs[2]:offs[3]]
+            self.next_obs = self.storage[offs[3]:offs[4]].view(cap, O)
+            self.done = self.storage[offs[4]:]
         self.state = torch.zeros(3, dtype=torch.int64, device=dev)  # size, next slot, push generation
+        # the sac_hip custom ops' replay descriptor (csrc/sac_torch_ops.cpp)
+        self.layout_spec = [cap, O, A, self.row_stride] + offs
         self._desc = E.ReplayDesc(
             self.obs.data_ptr(), self.act.data_ptr(), self.rew.data_ptr(), self.next_obs.data_ptr(),
             self.done.data_ptr(), cap, O, A, self.state.data_ptr(), self.row_stride)
@@ -166,9 +174,8 @@ class ReplayBuffer:
 
     def _push_device_rows(self, rows: torch.Tensor) -> None:
         n = rows.shape[0]
-        lib = E.load_library()
-        E.check(lib.sac_replay_push(ctypes_ref(self._desc), E.ptr(rows), n, self._size, self._pos,
-                                    E.stream_handle(self.device)))
+        with torch.cuda.device(self.device):
+            ops().replay_push(self.storage, self.state, self.layout_spec, rows, self._size, self._pos)
         self._size = min(self.capacity, self._size + n)
         self._pos = (self._pos + n) % self.capacity
         self._keep = rows  # keep alive until the kernel has consumed it
@@ -203,19 +210,19 @@ class ReplayBuffer:
     def gather(self, logical_idx) -> Transition:
         """Device gather of the given logical positions -> Transition of tensors."""
         self.flush()
-        idx = torch.as_tensor(logical_idx, dtype=torch.int32)
-        B = idx.numel()
+        idx = torch.as_tensor(logical_idx, dtype=torch.int32).reshape(-1)
         idx = idx.to(self.device, non_blocking=True)
-        f32 = dict(dtype=torch.float32, device=self.device)
-        s = torch.empty(B, self.obs_dim, **f32)
-        a = torch.empty(B, self.act_dim, **f32)
-        r = torch.empty(B, **f32)
-        s2 = torch.empty(B, self.obs_dim, **f32)
-        d = torch.empty(B, **f32)
-        lib = E.load_library()
-        E.check(lib.sac_replay_gather(ctypes_ref(self._desc), E.ptr(idx), B, E.ptr(s), E.ptr(a), E.ptr(r),
-                                      E.ptr(s2), E.ptr(d), E.stream_handle(self.device)))
-        return Transition(s, a, r, s2, d)
+        with torch.cuda.device(self.device):
+            return Transition(*ops().replay_gather(self.storage, self.state, self.layout_spec, idx))
+
+    def sample_gather_device(self, batch_size: int, seed: int, step: int):
+        """Device sampler + gather in one kernel: (indices, Transition) of
+        ``batch_size`` distinct rows for RNG (seed, step)."""
+        self._check(batch_size)
+        self.flush()
+        with torch.cuda.device(self.device):
+            idx, *t = ops().replay_sample_gather(self.storage, self.state, self.layout_spec, batch_size, seed, step)
+        return idx, Transition(*t)
 
     def sample_tensors(self, batch_size: int) -> Transition:
         return self.gather(self.sample_indices(batch_size))
@@ -239,8 +246,3 @@ class ReplayBuffer:
             self.state[:2].zero_()
             self.state[2:].add_(1)
 
-
-def ctypes_ref(desc):
-    import ctypes
-
-    return ctypes.byref(desc)

@@ -14,7 +14,7 @@ for name in sys.argv[1:]:
     res = {}
     for k, c, n, v in db.execute("select kernel_name, counter_name, count(*), avg(value) from counters_collection "
                                  "group by kernel_name, counter_name"):
-        if short(k) in PHASE_KERNELS[:4]:
+        if short(k) in PHASE_KERNELS:
             res.setdefault(short(k), {})[c] = v
     for k, d in res.items():
         print(name, k, {c: round(v) for c, v in sorted(d.items())})

@@ -58,9 +58,10 @@ def main():
     ap.add_argument("--tag", default="", help="suffix of the output files (e.g. _fp32, _gather)")
     ap.add_argument("--config", default="c2", help="bench config the profile ran (or 'gather')")
     ap.add_argument("--precision", default="bf16")
+    ap.add_argument("--dst", default=os.path.join(ROOT, "profiles"), help="output directory")
     a = ap.parse_args()
     rnd, src, tag = a.round, a.src, a.tag
-    dst = os.path.join(ROOT, "profiles")
+    dst = a.dst
     os.makedirs(dst, exist_ok=True)
 
     kt = one_db(os.path.join(src, "kt", "*.db"))
