@@ -319,6 +319,8 @@ static int validate(const sac_engine_config* c) {
 }
 
 // Lays out everything; when e != nullptr also fills e->h pointers (base = workspace).
+static void xcd_order(std::vector<TileDesc>& tiles);
+
 static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
   const int esz = c->precision == SAC_PREC_BF16 ? 2 : 4;
   const int B = c->batch, Bp = rup(B, 32), nrt = (B + SAC_ROWS - 1) / SAC_ROWS, Br = nrt * SAC_ROWS;
@@ -519,8 +521,10 @@ static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
     e->h.nD = nD;
     e->lds_bytes = (size_t)lo * 4;
     {  // update tiles stage up to 4 batch chunks of 512 B per operand row per round
+       // (enough for the longest operand row, the split layer 0's 2 Bp columns)
       const int bch = 512 / esz;
-      e->h.upd_slots = std::min(4, (Bp + bch - 1) / bch);
+      const int bp_max = split ? 2 * Bp : Bp;
+      e->h.upd_slots = std::min(4, (bp_max + bch - 1) / bch);
       e->upd_lds = SAC_UPD_LDS_FOR(e->h.upd_slots);
     }
     e->nrt = nrt;
@@ -568,6 +572,8 @@ static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
           }
       }
     }
+    xcd_order(e->hostB);
+    xcd_order(e->hostD);
     e->h.nBq[0] = e->h.nBq[1] = 0;
     for (const TileDesc& t : e->hostB) ++e->h.nBq[t.opt - 1];
     {
@@ -581,6 +587,46 @@ static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
     }
   }
   return total + 256;
+}
+
+// Update-tile order for the XCDs (speed only; any order gives the same bits).
+// Blocks are dealt round-robin to the 8 XCDs (block b on XCD b % 8), and the
+// dW operands come from other XCDs' L2s (fetched through the Infinity Fabric
+// at ~11 B/cycle per CU). A layer's tile (nt, kt) reads dY^T rows nt and X^T
+// rows kt; tiles sharing them on one XCD fetch them once into that L2. So each
+// net's tiles are bucketed by XCD -- a 256x256 layer's 8x8 tiles as 2 nt x 4 kt
+// blocks per XCD (6 row groups fetched per XCD instead of 16), one-column /
+// one-row layers dealt across the XCDs -- and emitted so that position p holds
+// a tile of bucket p % 8.
+static void xcd_order(std::vector<TileDesc>& tiles) {
+  std::vector<TileDesc> out;
+  out.reserve(tiles.size());
+  size_t i = 0;
+  while (i < tiles.size()) {
+    size_t j = i;  // one net: consecutive tiles of the same optimizer
+    while (j < tiles.size() && tiles[j].opt == tiles[i].opt) ++j;
+    std::vector<TileDesc> bucket[8];
+    for (size_t t = i; t < j; ++t) {
+      const TileDesc& d = tiles[t];
+      const int NT = d.Np / 32, KT = d.Kp / 32, nt = d.n0 / 32, kt = d.k0 / 32;
+      int x;
+      if (KT == 1) x = nt % 8;
+      else if (NT == 1) x = kt % 8;
+      else if (NT >= 4 && KT >= 2) x = (nt * 4 / NT) * 2 + (kt * 2 / KT);
+      else x = (nt * KT + kt) % 8;
+      bucket[x].push_back(d);
+    }
+    size_t taken[8] = {0};
+    for (size_t left = j - i; left;) {
+      for (int x = 0; x < 8; ++x)
+        if (taken[x] < bucket[x].size()) {
+          out.push_back(bucket[x][taken[x]++]);
+          --left;
+        }
+    }
+    i = j;
+  }
+  tiles.swap(out);
 }
 
 template <typename T>

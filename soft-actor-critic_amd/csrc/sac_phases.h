@@ -811,8 +811,11 @@ __device__ __forceinline__ void count_done(uint32_t* counter) {
 //   1. all threads stage the tile's 32 dY^T rows and 32 X^T rows (the dW GEMM's
 //      operands, K = batch) into LDS and fetch their elements' master weight,
 //      Adam moments, target weight and bias state, all in one round trip;
-//   2. waves 0-3 run the dW MFMAs (one 16x16 sub-tile each, batch chunks in
-//      order: the same summation order as before the staging);
+//   2. the dW MFMAs run as 16 (sub-tile, K-quarter) pairs spread over the
+//      waves (one pair per wave at 16 waves): pair p owns 16x16 sub-tile p & 3
+//      and the MFMA K-steps ch = p >> 2 (mod 4) of every staged chunk; the four
+//      K-quarter partials are summed in LDS in quarter order (the same bits for
+//      any block size);
 //   3. every thread updates 1024 / UT elements: Adam (torch single-tensor op
 //      order), Polyak, master weights; the packed compute copies are written
 //      from LDS as whole 16-B fragment pieces with sc1 stores, so a phase that
@@ -906,8 +909,11 @@ __device__ __forceinline__ void dw_adam_tile(const AS_C EngineDev& E, const Tile
   // sub-tile each, chunks in batch order
   const int lane = tid & 63, wave = wave_id();
   const int c = lane & 15, g = lane >> 4;
-  const int ns = (wave >> 1) * 16, ks = (wave & 1) * 16;
-  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  constexpr int KQ = 4, NWV = UT / 64, PPW = 16 / NWV;  // K-quarters, waves, pairs per wave
+  static_assert(UT % 64 == 0 && 16 % NWV == 0, "16 (sub-tile, K-quarter) pairs over whole waves");
+  f32x4 acc[PPW];
+#pragma unroll
+  for (int j = 0; j < PPW; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
   constexpr int MAXS = 4, PPT = 64 * (SAC_UPD_BCH / EPR) / UT;  // slots, pieces per thread per full chunk
   for (int r0 = 0; r0 < Bp; r0 += nslot * SAC_UPD_BCH) {
     u32x4 rg[MAXS][PPT];
@@ -942,14 +948,19 @@ __device__ __forceinline__ void dw_adam_tile(const AS_C EngineDev& E, const Tile
       }
     }
     __syncthreads();
-    if (wave < 4) {
+    if (r0 == 0) STAMP(polyak ? 51 : 55);
+    {
       for (int sl = 0; sl < nslot; ++sl) {
         const int b0 = r0 + sl * SAC_UPD_BCH;
         if (b0 >= Bp) break;
         const int bch = Bp - b0 < SAC_UPD_BCH ? Bp - b0 : SAC_UPD_BCH;
+#pragma unroll
+        for (int j = 0; j < PPW; ++j) {
+        const int pr = wave + j * NWV, kq = pr >> 2;
+        const int ns = ((pr & 3) >> 1) * 16, ks = (pr & 1) * 16;
         const AS_L T* arow = stage + sl * slot_el + (ns + c) * lds_row + g * KL;
         const AS_L T* brow = stage + sl * slot_el + (32 + ks + c) * lds_row + g * KL;
-        for (int ch = 0; ch < bch / KC; ++ch) {
+        for (int ch = kq; ch < bch / KC; ch += KQ) {
           typename MM<T>::Frag a, b;
           if constexpr (sizeof(T) == 2) {
             a = *(const AS_L bf16x8*)(arow + ch * KC);
@@ -958,16 +969,32 @@ __device__ __forceinline__ void dw_adam_tile(const AS_C EngineDev& E, const Tile
             a = *(const AS_L f32x4*)(arow + ch * KC);
             b = *(const AS_L f32x4*)(brow + ch * KC);
           }
-          MM<T>::mma(acc, a, b);
+          MM<T>::mma(acc[j], a, b);
+        }
         }
       }
     }
     __syncthreads();  // the stage is refilled by the next round
   }
   STAMP(polyak ? 49 : 53);
-  if (wave < 4) {
+  {  // K-quarter partials -> the (free) stage area, summed in quarter order below
 #pragma unroll
-    for (int i = 0; i < 4; ++i) accs[(ns + g * 4 + i) * 33 + ks + c] = acc[i];
+    for (int j = 0; j < PPW; ++j) {
+      const int pr = wave + j * NWV;
+      const int ns = ((pr & 3) >> 1) * 16, ks = (pr & 1) * 16;
+      lf* part = (lf*)stage + (pr >> 2) * (32 * 33);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) part[(ns + g * 4 + i) * 33 + ks + c] = acc[j][i];
+    }
+  }
+  __syncthreads();
+  for (int el = tid; el < 1024; el += UT) {
+    const int o = (el >> 5) * 33 + (el & 31);
+    const lf* part = (const lf*)stage;
+    float sum = part[o];
+#pragma unroll
+    for (int q = 1; q < KQ; ++q) sum += part[q * (32 * 33) + o];
+    accs[o] = sum;
   }
 #pragma unroll
   for (int j = 0; j < BPT; ++j) {

@@ -22,6 +22,13 @@
 // Engine state: `engine` is the sac_engine* handle (int64) from
 // sac_engine_create; `state` lists the 16 caller-owned tensors the step reads
 // and writes (sac_engine_buffers order) so the op's mutation is declared.
+//
+// The ops do not link libsac_engine.so: bind_engine_library(path) dlopens the
+// library the Python side loaded (the same file, hence the same instance as the
+// ctypes handle's owner, also for the diagnostic -DSAC_STAMPS build) and
+// resolves the entry points once.
+#include <dlfcn.h>
+
 #include <ATen/ATen.h>
 #include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
 #include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
@@ -34,14 +41,59 @@ namespace {
 constexpr int64_t kStateTensors = 16;
 using Guard = c10::hip::HIPGuardMasqueradingAsCUDA;
 
+// the C ABI entry points the ops call, resolved by bind_engine_library
+struct EngineApi {
+  decltype(&sac_last_error) last_error = nullptr;
+  decltype(&sac_replay_push) replay_push = nullptr;
+  decltype(&sac_replay_gather) replay_gather = nullptr;
+  decltype(&sac_replay_sample_indices) replay_sample_indices = nullptr;
+  decltype(&sac_replay_sample_gather) replay_sample_gather = nullptr;
+  decltype(&sac_engine_train) engine_train = nullptr;
+  decltype(&sac_engine_train_graph) engine_train_graph = nullptr;
+  decltype(&sac_policy_act) policy_act = nullptr;
+};
+EngineApi g_api;
+std::string g_bound_path;
+
+template <typename F>
+void resolve(void* h, const char* name, F& f) {
+  f = reinterpret_cast<F>(dlsym(h, name));
+  TORCH_CHECK(f != nullptr, "libsac_engine lacks ", name);
+}
+
+void bind_engine_library(c10::string_view path_) {
+  const std::string path(path_.data(), path_.size());
+  if (g_api.engine_train && path == g_bound_path) return;
+  void* h = dlopen(path.c_str(), RTLD_NOW | RTLD_LOCAL);
+  TORCH_CHECK(h != nullptr, "cannot load ", path, ": ", dlerror());
+  EngineApi a;
+  resolve(h, "sac_last_error", a.last_error);
+  resolve(h, "sac_replay_push", a.replay_push);
+  resolve(h, "sac_replay_gather", a.replay_gather);
+  resolve(h, "sac_replay_sample_indices", a.replay_sample_indices);
+  resolve(h, "sac_replay_sample_gather", a.replay_sample_gather);
+  resolve(h, "sac_engine_train", a.engine_train);
+  resolve(h, "sac_engine_train_graph", a.engine_train_graph);
+  resolve(h, "sac_policy_act", a.policy_act);
+  g_api = a;
+  g_bound_path = path;
+}
+
+const EngineApi& api() {
+  TORCH_CHECK(g_api.engine_train != nullptr,
+              "torch.ops.sac_hip: engine library not bound (call sac._engine.ops(), which binds libsac_engine.so)");
+  return g_api;
+}
+
 void* stream_of(const at::Tensor& t) {
   return static_cast<void*>(c10::hip::getCurrentHIPStreamMasqueradingAsCUDA(t.device().index()).stream());
 }
 
 void check_rc(int rc) {
   // SAC_E_NOT_ENOUGH is the reference's ValueError (replay_buffer.py:35-38)
-  TORCH_CHECK_VALUE(rc != SAC_E_NOT_ENOUGH, sac_last_error());
-  TORCH_CHECK(rc == SAC_OK, "libsac_engine error ", rc, ": ", sac_last_error());
+  if (rc == SAC_OK) return;
+  TORCH_CHECK_VALUE(rc != SAC_E_NOT_ENOUGH, api().last_error());
+  TORCH_CHECK(false, "libsac_engine error ", rc, ": ", api().last_error());
 }
 
 void check_f32(const at::Tensor& t, const char* what) {
@@ -106,7 +158,7 @@ void replay_push(at::Tensor& storage, at::Tensor& state, at::IntArrayRef layout,
   TORCH_CHECK(rows.device() == storage.device(), "rows on a different device");
   if (rows.size(0) == 0) return;
   Guard g(storage.device());
-  check_rc(sac_replay_push(&r.d, rows.data_ptr<float>(), rows.size(0), size, pos, stream_of(storage)));
+  check_rc(api().replay_push(&r.d, rows.data_ptr<float>(), rows.size(0), size, pos, stream_of(storage)));
 }
 
 std::vector<at::Tensor> empty_batch(const at::Tensor& like, int64_t B, int64_t O, int64_t A) {
@@ -123,7 +175,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor> replay_ga
   auto out = empty_batch(storage, B, r.obs, r.act);
   if (B) {
     Guard g(storage.device());
-    check_rc(sac_replay_gather(&r.d, indices.data_ptr<int32_t>(), static_cast<int32_t>(B), out[0].data_ptr<float>(),
+    check_rc(api().replay_gather(&r.d, indices.data_ptr<int32_t>(), static_cast<int32_t>(B), out[0].data_ptr<float>(),
                                out[1].data_ptr<float>(), out[2].data_ptr<float>(), out[3].data_ptr<float>(),
                                out[4].data_ptr<float>(), stream_of(storage)));
   }
@@ -136,7 +188,7 @@ at::Tensor replay_sample(const at::Tensor& storage, const at::Tensor& state, at:
   TORCH_CHECK(batch >= 1 && batch <= r.d.capacity, "batch must be in [1, capacity]");
   auto idx = at::empty({batch}, storage.options().dtype(at::kInt));
   Guard g(storage.device());
-  check_rc(sac_replay_sample_indices(&r.d, static_cast<int32_t>(batch), static_cast<uint64_t>(seed),
+  check_rc(api().replay_sample_indices(&r.d, static_cast<int32_t>(batch), static_cast<uint64_t>(seed),
                                      static_cast<uint64_t>(step), idx.data_ptr<int32_t>(), stream_of(storage)));
   return idx;
 }
@@ -149,7 +201,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tenso
   auto idx = at::empty({batch}, storage.options().dtype(at::kInt));
   auto out = empty_batch(storage, batch, r.obs, r.act);
   Guard g(storage.device());
-  check_rc(sac_replay_sample_gather(&r.d, static_cast<int32_t>(batch), static_cast<uint64_t>(seed),
+  check_rc(api().replay_sample_gather(&r.d, static_cast<int32_t>(batch), static_cast<uint64_t>(seed),
                                     static_cast<uint64_t>(step), idx.data_ptr<int32_t>(), out[0].data_ptr<float>(),
                                     out[1].data_ptr<float>(), out[2].data_ptr<float>(), out[3].data_ptr<float>(),
                                     out[4].data_ptr<float>(), stream_of(storage)));
@@ -181,7 +233,7 @@ void train_step(int64_t engine, at::TensorList state, const at::Tensor& storage,
   }
   if (!n_steps) return;
   Guard g(storage.device());
-  check_rc(sac_engine_train(e, &r.d, static_cast<int32_t>(n_steps), ip, ep, stream_of(storage)));
+  check_rc(api().engine_train(e, &r.d, static_cast<int32_t>(n_steps), ip, ep, stream_of(storage)));
 }
 
 void train_graph(int64_t engine, at::TensorList state, const at::Tensor& storage, const at::Tensor& rstate,
@@ -190,7 +242,7 @@ void train_graph(int64_t engine, at::TensorList state, const at::Tensor& storage
   sac_engine* e = engine_of(engine, state, storage);
   TORCH_CHECK(n_steps >= 0 && chunk >= 1, "n_steps >= 0 and chunk >= 1");
   Guard g(storage.device());
-  check_rc(sac_engine_train_graph(e, &r.d, static_cast<int32_t>(n_steps), static_cast<int32_t>(chunk),
+  check_rc(api().engine_train_graph(e, &r.d, static_cast<int32_t>(n_steps), static_cast<int32_t>(chunk),
                                   stream_of(storage)));
 }
 
@@ -211,7 +263,7 @@ std::tuple<at::Tensor, at::Tensor> policy_act(int64_t engine, const at::Tensor& 
   at::Tensor lp = at::empty({(want_log_pi && ep) ? n : 0}, o);
   if (n) {
     Guard g(obs.device());
-    check_rc(sac_policy_act(reinterpret_cast<sac_engine*>(engine), obs.data_ptr<float>(), static_cast<int32_t>(n), ep,
+    check_rc(api().policy_act(reinterpret_cast<sac_engine*>(engine), obs.data_ptr<float>(), static_cast<int32_t>(n), ep,
                             act.data_ptr<float>(), lp.numel() ? lp.data_ptr<float>() : nullptr, stream_of(obs)));
   }
   return {act, lp};
@@ -253,6 +305,7 @@ std::tuple<at::Tensor, at::Tensor> policy_act_meta(int64_t, const at::Tensor& ob
 }  // namespace
 
 TORCH_LIBRARY(sac_hip, m) {
+  m.def("bind_engine_library(str path) -> ()", &bind_engine_library);
   m.def("replay_push(Tensor(a!) storage, Tensor(b!) state, int[] layout, Tensor rows, int size, int pos) -> ()");
   m.def("replay_gather(Tensor storage, Tensor state, int[] layout, Tensor indices) "
         "-> (Tensor, Tensor, Tensor, Tensor, Tensor)");

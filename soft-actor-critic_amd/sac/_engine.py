@@ -135,8 +135,9 @@ def ops():
     """``torch.ops.sac_hip``: the PyTorch custom ops over the C ABI
     (csrc/sac_torch_ops.cpp: replay_push, replay_gather, replay_sample,
     replay_sample_gather, train_step, train_graph, policy_act).  The op library
-    links libsac_engine.so (one instance with the ctypes handle: same file, same
-    soname).  Raises EngineUnavailable when it is not built."""
+    dlopens the engine library ctypes loaded (bind_engine_library: the same file,
+    so the same instance owns the engine handles).  Raises EngineUnavailable
+    when it is not built."""
     global _ops_loaded
     if not _ops_loaded:
         load_library()
@@ -146,6 +147,7 @@ def ops():
                 f"{path} not found: build it with `make -C soft-actor-critic_amd/csrc` "
                 "(or __graft_entry__.build()); there is no CPU fallback")
         torch.ops.load_library(path)
+        torch.ops.sac_hip.bind_engine_library(os.path.abspath(library_path()))
         _ops_loaded = True
     return torch.ops.sac_hip
 

@@ -14,7 +14,7 @@ import torch
 
 from conftest import PKG
 
-OPS = ("replay_push", "replay_gather", "replay_sample", "replay_sample_gather", "train_step", "train_graph",
+OPS = ("bind_engine_library", "replay_push", "replay_gather", "replay_sample", "replay_sample_gather", "train_step", "train_graph",
        "policy_act")
 
 

@@ -69,7 +69,7 @@ names = {58: "D done", 59: "D waited",
          5: "pi L3", 6: "head+publish", 7: "Qt1", 8: "Qt2", 9: "Qt published", 10: "Q1 fwd", 12: "Q2 fwd",
          16: "unit bwd", 14: "y inputs in", 15: "seed", 11: "Q1 GT stored", 13: "Q2 GT stored",
          32: "start", 36: "Q1 fwd", 37: "Q2 fwd", 38: "Q1 bwd->da", 39: "Q2 bwd->da / combined", 35: "pi bwd",
-         48: "start", 49: "dW", 50: "adam", 52: "start", 53: "dW", 54: "adam"}
+         48: "start", 49: "dW", 50: "adam", 52: "start", 53: "dW", 54: "adam", 51: "staged", 55: "staged"}
 names.update({33: "B waited", 20: "HC8 layer entry", 21: "HC8 MFMA done (wave 0)", 22: "HC8 epilogue done",
               23: "HC8 layer end"})
 names.update({60: "END", 61: "END", 62: "END", 63: "END"})
@@ -78,7 +78,7 @@ if SPLIT:  # sac_split.h stamps
                   9: "Qt partial published", 33: "inputs", 34: "pi inputs", 36: "Q1 fwd", 37: "Q2 fwd",
                   38: "Q1 da partial", 39: "pi: critics combined", 35: "pi bwd + GT"})
 PH = {"A": list(range(0, 17)) + [20, 21, 22, 23, 56, 57, 59, 60],  # 20-23: free for DSTAMP probes
-      "C": list(range(32, 40)) + [61], "B": [48, 49, 50, 62], "D": [52, 53, 54, 63]}
+      "C": list(range(32, 40)) + [61], "B": [48, 51, 49, 50, 62], "D": [52, 55, 53, 54, 63]}
 ROLES = {"A": ["pi(s')", "Qt1", "Qt2", "Q1", "Q2", "pi(s)"], "C": ["Q1", "Q2", "pi"]}  # block-group order
 # shader clock during phase A: s_memtime ticks (slots 40/41) per realtime tick (slots 0/60)
 clk = []
@@ -108,6 +108,28 @@ for ph, ids in PH.items():
             spans.append(r[live, endc].max() - r[live, base].min())
     if spans:
         print(f"  launch span (first block start -> last block end, stores drained): {np.median(spans) / 100:.2f} us")
+        st_, en_ = [], []
+        for r in runs:
+            live = r[:, base] > 0
+            if live.any() and (r[live, endc] > 0).all():
+                t0 = r[live, base].min()
+                st_.append(r[live, base] - t0)
+                en_.append(r[live, endc] - t0)
+        if st_:
+            st_, en_ = np.concatenate(st_) / 100, np.concatenate(en_) / 100
+            q = lambda x: " ".join(f"{v:.2f}" for v in np.percentile(x, [0, 25, 50, 75, 90, 100]))  # noqa: E731
+            print(f"  block start (us, p0 p25 p50 p75 p90 p100): {q(st_)}")
+            print(f"  block end   (us, p0 p25 p50 p75 p90 p100): {q(en_)}")
+            r = runs[-1]
+            live = np.nonzero(r[:, base] > 0)[0]
+            t0 = r[live, base].min()
+            late = sorted(live, key=lambda b: -r[b, endc])[:12]
+            print("  latest blocks (id: start/end us): " + ", ".join(
+                f"{b}: {(r[b, base] - t0) / 100:.2f}/{(r[b, endc] - t0) / 100:.2f}" for b in late))
+            if ph in ("B", "D"):
+                for b in list(late[:3]) + [int(np.median(live))]:
+                    print(f"    block {b}: " + " | ".join(f"{names.get(i, i)} {(r[b, i] - t0) / 100:.2f}"
+                                                      for i in ids if r[b, i] > 0))
     for g, m in groups.items():
         if not m.any():
             continue
