@@ -198,6 +198,14 @@ int sac_replay_sample_gather(const sac_replay *rb, int32_t batch, uint64_t seed,
 int sac_engine_time_phases(sac_engine *e, const sac_replay *rb, int32_t n_steps,
                            float *ms_host, void *stream);
 
+/* Temperature updates on (default) or off.  Off reproduces the reference
+ * after SAC.load_agent with auto_entropy_tuning: it rebinds log_alpha to the
+ * checkpoint's tensor but leaves alpha_optimizer bound to the old one
+ * (sac/agent.py:550-554), so later steps still compute and report L_alpha while
+ * log_alpha, alpha, its Adam moments and step count stay as loaded.  Takes
+ * effect for launches (and graph replays) after this point on `stream`. */
+int sac_engine_set_alpha_update(sac_engine *e, int32_t enabled, void *stream);
+
 /* Health check (synchronises the stream): SAC_E_HIP if an in-launch
  * workgroup hand-off of the role-split phase kernels gave up waiting (the
  * affected steps are invalid), else 0.  Replaces: nothing (diagnostic). */

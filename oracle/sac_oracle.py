@@ -304,6 +304,10 @@ class SacState:
     opt_alpha_m: float = 0.0
     opt_alpha_v: float = 0.0
     opt_alpha_step: float = 0.0
+    # True after the reference's load_agent with auto-tuning: log_alpha is the
+    # checkpoint's tensor while alpha_optimizer still holds the old one
+    # (sac/agent.py:550-554), so L_alpha is computed but nothing updates alpha
+    alpha_orphaned: bool = False
 
     @staticmethod
     def fresh(pi: MLP, q1: MLP, q2: MLP, hp: SacHyper, act_dim: int) -> "SacState":
@@ -379,6 +383,7 @@ def training_step(st: SacState, hp: SacHyper, batch: Batch, eps_t: np.ndarray, e
         la32 = F32(st.log_alpha)
         term = (lp + H).astype(F32)
         losses.append(float(-np.mean(la32 * term, dtype=F32)))
+    if hp.auto_entropy_tuning and not st.alpha_orphaned:
         g = float(np.sum(F32(-1.0 / B) * term, dtype=F32))
         st.opt_alpha_step += 1.0
         b1, b2, e = 0.9, 0.999, 1e-8
@@ -389,7 +394,7 @@ def training_step(st: SacState, hp: SacHyper, batch: Batch, eps_t: np.ndarray, e
         denom = math.sqrt(st.opt_alpha_v) / math.sqrt(bc2) + e
         st.log_alpha = st.log_alpha + (-hp.alpha_lr / bc1) * st.opt_alpha_m / denom
         st.alpha = math.exp(st.log_alpha)
-    else:
+    elif not hp.auto_entropy_tuning:
         losses.append(float("nan"))
 
     # ---- Polyak (agent.py:282-300)
@@ -449,4 +454,45 @@ def state_from_fixture(fx, prefix: str, hp: SacHyper, cfg: dict, act_dim: int) -
     st = SacState.fresh(pi, q1, q2, hp, act_dim)
     st.q1t, st.q2t = net("q1t", qa), net("q2t", qa)
     st.q1t.out_act = st.q2t.out_act = qo
+    return st
+
+
+# ----------------------------------------------------------------------------- checkpoints
+def load_checkpoint(ckpt: dict, hp: SacHyper, act_dim: int, q_act: str = "relu", pi_act: str = "relu") -> SacState:
+    """The reference's ``load_agent`` (sac/agent.py:538-554) on a checkpoint dict
+    as ``save_agent`` writes it (agent.py:521-536; tensors as numpy arrays):
+    five state_dicts, three torch Adam state_dicts, and with auto-tuning
+    ``log_alpha`` + the alpha optimizer's state_dict.  The alpha optimizer state
+    is loaded into an optimizer that no longer owns ``log_alpha``: the returned
+    state has ``alpha_orphaned`` set and alpha = exp(log_alpha)."""
+    def sd(key):
+        return {k: np.asarray(v, F32) for k, v in ckpt[key].items()}
+
+    st = SacState(MLP.from_state_dict(sd("policy_net_state_dict"), pi_act),
+                  MLP.from_state_dict(sd("q_net1_state_dict"), q_act), MLP.from_state_dict(sd("q_net2_state_dict"), q_act),
+                  MLP.from_state_dict(sd("q_net1_target_state_dict"), q_act),
+                  MLP.from_state_dict(sd("q_net2_target_state_dict"), q_act), None, None, None, act_dim)
+    for name, net in (("policy_optimizer_state_dict", st.pi), ("q1_optimizer_state_dict", st.q1),
+                      ("q2_optimizer_state_dict", st.q2)):
+        o = ckpt[name]["state"]
+        ps = net.params()
+        ad = AdamState.zeros_like(ps)
+        for i in range(len(ps)):
+            if i in o:
+                ad.m[i][...] = np.asarray(o[i]["exp_avg"], F32).reshape(ps[i].shape)
+                ad.v[i][...] = np.asarray(o[i]["exp_avg_sq"], F32).reshape(ps[i].shape)
+                ad.step = float(o[i]["step"])
+        setattr(st, {"policy_optimizer_state_dict": "opt_pi", "q1_optimizer_state_dict": "opt_q1",
+                     "q2_optimizer_state_dict": "opt_q2"}[name], ad)
+    if hp.auto_entropy_tuning:
+        st.log_alpha = float(np.asarray(ckpt["log_alpha"], np.float64))
+        st.alpha = math.exp(st.log_alpha)
+        ao = ckpt["alpha_optimizer_state_dict"]["state"].get(0)
+        if ao is not None:
+            st.opt_alpha_m = float(np.asarray(ao["exp_avg"], np.float64))
+            st.opt_alpha_v = float(np.asarray(ao["exp_avg_sq"], np.float64))
+            st.opt_alpha_step = float(ao["step"])
+        st.alpha_orphaned = True
+    else:
+        st.alpha = float(F32(hp.alpha))
     return st

@@ -482,6 +482,7 @@ static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
       h.stage = stage;
     }
     h.auto_entropy = c->auto_entropy;
+    h.alpha_update = 1;
     h.gamma = c->gamma;
     h.tau = c->tau;
     h.ls_min = c->log_std_min;
@@ -826,6 +827,14 @@ int sac_engine_create(const sac_engine_config* cfg, const sac_engine_buffers* bu
     return rc;
   }
   *out = e;
+  return SAC_OK;
+}
+
+int sac_engine_set_alpha_update(sac_engine* e, int32_t enabled, void* stream) {
+  if (!e) return fail(SAC_E_INVALID, "null engine");
+  e->h.alpha_update = enabled ? 1 : 0;
+  HIPCHK(hipMemcpyAsync((char*)e->d + offsetof(EngineDev, alpha_update), &e->h.alpha_update, sizeof(int),
+                        hipMemcpyHostToDevice, (hipStream_t)stream));
   return SAC_OK;
 }
 

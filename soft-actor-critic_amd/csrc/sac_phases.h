@@ -81,6 +81,10 @@ struct EngineDev {
   const TileDesc* tilesD;
   int nB, nD, nBq[2];
   int auto_entropy;
+  // 0 after a reference-style load_agent: the reference rebinds log_alpha but
+  // not its optimizer (sac/agent.py:550-554), so L_alpha is still computed and
+  // reported while log_alpha, its Adam moments and step count stay as loaded
+  int alpha_update;
   float gamma, tau, ls_min, ls_max, scale, beta1, beta2, adam_eps, target_entropy;
   double actor_lr, critic_lr, alpha_lr;
   uint64_t seed;
@@ -1106,8 +1110,8 @@ __device__ __forceinline__ void alpha_and_losses(const AS_C EngineDev& E, int pa
     stats[0] = red[2 * NT] / (float)B;
     stats[1] = red[3 * NT] / (float)B;
     stats[2] = red[4 * NT] / (float)B;
-    if (E.auto_entropy) {
-      stats[3] = -(red[1 * NT] / (float)B);
+    stats[3] = E.auto_entropy ? -(red[1 * NT] / (float)B) : __builtin_nanf("");
+    if (E.auto_entropy && E.alpha_update) {
       const double gr = (double)red[0];
       const double b1 = (double)E.beta1, b2 = (double)E.beta2;
       const double m = st[2] + (1.0 - b1) * (gr - st[2]);
@@ -1120,8 +1124,6 @@ __device__ __forceinline__ void alpha_and_losses(const AS_C EngineDev& E, int pa
       __hip_atomic_store(sd + 1, exp(la), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(sd + 2, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(sd + 3, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    } else {
-      stats[3] = __builtin_nanf("");
     }
   }
 }
@@ -1432,7 +1434,7 @@ __device__ __forceinline__ void target_critic_body(const EngineDev* __restrict__
     GP(uint32_t, E.sync)[SYNC_BDONE] = 0u;
     GP(uint32_t, E.sync)[SYNC_BDONE + 16] = 0u;
   }
-  if ((!ROLES || role == 0) && rbi == 0 && tid < 4 && (tid < 3 || E.auto_entropy)) {
+  if ((!ROLES || role == 0) && rbi == 0 && tid < 4 && (tid < 3 || (E.auto_entropy && E.alpha_update))) {
     const double t = GP(double, E.opt_steps)[tid] + 1.0;
     GP(double, E.opt_steps)[tid] = t;
     if (tid < 3) {

@@ -271,7 +271,7 @@ __device__ __forceinline__ void target_critic_split_body(const EngineDev* __rest
 
   const uint64_t step = *GPC(uint64_t, E.rng_step);
   const int par = (int)(step & 1);
-  if (role == 0 && rbi == 0 && h == 0 && tid < 4 && (tid < 3 || E.auto_entropy)) {
+  if (role == 0 && rbi == 0 && h == 0 && tid < 4 && (tid < 3 || (E.auto_entropy && E.alpha_update))) {
     // optimizer step counters and this step's Adam bias corrections (torch adam.py)
     const double t = GP(double, E.opt_steps)[tid] + 1.0;
     GP(double, E.opt_steps)[tid] = t;

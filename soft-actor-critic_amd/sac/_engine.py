@@ -95,6 +95,7 @@ SIGNATURES = {
                                               ctypes.POINTER(ctypes.c_float), ctypes.c_void_p]),
     "sac_phase_kernel_name": (ctypes.c_char_p, [ctypes.c_int32]),
     "sac_engine_check": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
+    "sac_engine_set_alpha_update": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p]),
     "sac_engine_phase_layout": (ctypes.c_int, [ctypes.c_void_p]),
 }
 

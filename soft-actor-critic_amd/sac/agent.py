@@ -587,4 +587,14 @@ class SAC:
             self.engine.alpha_state[1] = la.exp()
             if "alpha_optimizer_state_dict" in ckpt:
                 self._import_opt(self.alpha_optimizer, ckpt["alpha_optimizer_state_dict"], None, 3)
+            # The reference rebinds self.log_alpha to the checkpoint's tensor but
+            # leaves alpha_optimizer bound to the old one (agent.py:550-554): from
+            # here on its steps still compute L_alpha, but log_alpha, alpha and the
+            # alpha optimizer state stay as loaded.  Reproduced by default
+            # (pinned by tests/golden/ref_ckpt_*.npz); train.alpha_after_load:
+            # "tune" keeps tuning the loaded log_alpha instead.
+            mode = self.config["train"].get("alpha_after_load", "reference")
+            if mode not in ("reference", "tune"):
+                raise ValueError("train.alpha_after_load must be 'reference' or 'tune'")
+            self.engine.set_alpha_update(mode == "tune")
         self.engine.sync_params()

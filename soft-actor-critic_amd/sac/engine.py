@@ -160,6 +160,10 @@ class SacEngine:
         except Exception:
             pass
 
+    def set_alpha_update(self, enabled: bool) -> None:
+        """Temperature (log alpha) Adam updates on/off (see sac_engine.h)."""
+        E.check(self.lib.sac_engine_set_alpha_update(self.handle, int(bool(enabled)), self._stream()))
+
     def sync_params(self) -> None:
         """Re-pack the MFMA compute copies after host-side parameter changes."""
         E.check(self.lib.sac_engine_sync_params(self.handle, self._stream()))

@@ -203,6 +203,75 @@ def _state(agent, want_full: bool, prefix: str, out: dict) -> None:
     out[f"{prefix}/alpha"] = np.array(float(agent.alpha.item()), np.float64)
 
 
+def _draw_inputs(rng, c) -> dict:
+    """One step's injected batch + eps (the fixtures' seeded draw order)."""
+    B, O, A = c["batch"], c["obs"], c["act"]
+    s = rng.standard_normal((B, O)).astype(np.float32)
+    a = rng.uniform(-1, 1, (B, A)).astype(np.float32)
+    r = rng.standard_normal(B).astype(np.float32)
+    s2 = rng.standard_normal((B, O)).astype(np.float32)
+    d = (rng.random(B) < 0.05).astype(np.float32)
+    if "force_done" in c:
+        d[:] = c["force_done"]
+    if "force_reward" in c:
+        r[:] = c["force_reward"]
+    eps_t = rng.standard_normal((B, A)).astype(np.float32)
+    eps_a = rng.standard_normal((B, A)).astype(np.float32)
+    return dict(s=s, a=a, r=r, s2=s2, d=d, eps_t=eps_t, eps_a=eps_a)
+
+
+def _inject_step(agent, inputs: dict):
+    """One reference training_step() (sac/agent.py:302-327) on the given batch
+    and eps; returns (losses [4] float64, y, log_pi)."""
+    import torch.distributions.normal as tdn
+    from collections import namedtuple
+
+    T = namedtuple("Transition", ("state", "action", "reward", "next_state", "done"))
+    batch = T(*(torch.from_numpy(inputs[k]) for k in ("s", "a", "r", "s2", "d")))
+    agent.sample_batch = lambda b=batch: b
+    queue = [torch.from_numpy(inputs["eps_t"].copy()), torch.from_numpy(inputs["eps_a"].copy())]
+
+    def fake_sn(shape, dtype, device, q=queue):
+        e = q.pop(0)
+        assert tuple(e.shape) == tuple(shape), (e.shape, shape)
+        return e.to(dtype=dtype, device=device)
+
+    recorded: list = []
+    orig_backward = torch.Tensor.backward
+
+    def rec_backward(self, *a, **k):
+        recorded.append(float(self.detach().double().item()))
+        return orig_backward(self, *a, **k)
+
+    cap = {}
+    orig_ctq = type(agent).compute_target_q_values
+    orig_upn = type(agent).update_policy_network
+
+    def ctq(self, *a_, **k_):
+        y = orig_ctq(self, *a_, **k_)
+        cap["y"] = y.detach().numpy().copy()
+        return y
+
+    def upn(self, *a_, **k_):
+        lp = orig_upn(self, *a_, **k_)
+        cap["log_pi"] = lp.detach().numpy().copy()
+        return lp
+
+    agent.compute_target_q_values = types.MethodType(ctq, agent)
+    agent.update_policy_network = types.MethodType(upn, agent)
+    orig_sn = tdn._standard_normal
+    tdn._standard_normal = fake_sn
+    torch.Tensor.backward = rec_backward
+    try:
+        agent.training_step()
+    finally:
+        torch.Tensor.backward = orig_backward
+        tdn._standard_normal = orig_sn
+    assert not queue, "eps queue not fully consumed"
+    losses = recorded + ([np.nan] if len(recorded) == 3 else [])
+    return np.array(losses, np.float64), cap["y"], cap["log_pi"]
+
+
 def capture(name: str, c: dict) -> dict:
     from sac.agent import SAC  # reference, imported after stubs
     import sac.models  # noqa: F401
@@ -214,72 +283,14 @@ def capture(name: str, c: dict) -> dict:
     _state(agent, bool(c.get("full")) or 0 in full_steps, "init", out)
 
     rng = np.random.default_rng(123 + sum(map(ord, name)))
-    B, O, A = c["batch"], c["obs"], c["act"]
-    recorded: list = []
-    orig_backward = torch.Tensor.backward
-
-    def rec_backward(self, *a, **k):
-        recorded.append(float(self.detach().double().item()))
-        return orig_backward(self, *a, **k)
-
-    import torch.distributions.normal as tdn
-    orig_sn = tdn._standard_normal
     for step in range(1, c["steps"] + 1):
-        s = rng.standard_normal((B, O)).astype(np.float32)
-        a = rng.uniform(-1, 1, (B, A)).astype(np.float32)
-        r = rng.standard_normal(B).astype(np.float32)
-        s2 = rng.standard_normal((B, O)).astype(np.float32)
-        d = (rng.random(B) < 0.05).astype(np.float32)
-        if "force_done" in c:
-            d[:] = c["force_done"]
-        if "force_reward" in c:
-            r[:] = c["force_reward"]
-        eps_t = rng.standard_normal((B, A)).astype(np.float32)
-        eps_a = rng.standard_normal((B, A)).astype(np.float32)
-        for k_, v_ in dict(s=s, a=a, r=r, s2=s2, d=d, eps_t=eps_t, eps_a=eps_a).items():
+        inputs = _draw_inputs(rng, c)
+        for k_, v_ in inputs.items():
             out[f"step{step}/in/{k_}"] = v_
-
-        from collections import namedtuple
-        T = namedtuple("Transition", ("state", "action", "reward", "next_state", "done"))
-        batch = T(torch.from_numpy(s), torch.from_numpy(a), torch.from_numpy(r),
-                  torch.from_numpy(s2), torch.from_numpy(d))
-        agent.sample_batch = lambda b=batch: b
-        queue = [torch.from_numpy(eps_t.copy()), torch.from_numpy(eps_a.copy())]
-
-        def fake_sn(shape, dtype, device, q=queue):
-            e = q.pop(0)
-            assert tuple(e.shape) == tuple(shape), (e.shape, shape)
-            return e.to(dtype=dtype, device=device)
-
-        tdn._standard_normal = fake_sn
-        cap = {}
-        orig_ctq = type(agent).compute_target_q_values
-        orig_upn = type(agent).update_policy_network
-
-        def ctq(self, *a_, **k_):
-            y = orig_ctq(self, *a_, **k_)
-            cap["y"] = y.detach().numpy().copy()
-            return y
-
-        def upn(self, *a_, **k_):
-            lp = orig_upn(self, *a_, **k_)
-            cap["log_pi"] = lp.detach().numpy().copy()
-            return lp
-
-        agent.compute_target_q_values = types.MethodType(ctq, agent)
-        agent.update_policy_network = types.MethodType(upn, agent)
-        recorded.clear()
-        torch.Tensor.backward = rec_backward
-        try:
-            agent.training_step()
-        finally:
-            torch.Tensor.backward = orig_backward
-            tdn._standard_normal = orig_sn
-        assert not queue, "eps queue not fully consumed"
-        losses = recorded + ([np.nan] if len(recorded) == 3 else [])
-        out[f"step{step}/out/losses"] = np.array(losses, np.float64)
-        out[f"step{step}/out/y"] = cap["y"]
-        out[f"step{step}/out/log_pi"] = cap["log_pi"]
+        losses, y, log_pi = _inject_step(agent, inputs)
+        out[f"step{step}/out/losses"] = losses
+        out[f"step{step}/out/y"] = y
+        out[f"step{step}/out/log_pi"] = log_pi
         _state(agent, step in full_steps, f"step{step}/post", out)
     return out
 
@@ -302,6 +313,100 @@ def capture_replay_sample() -> dict:
     return out
 
 
+def capture_checkpoint() -> dict:
+    """the reference's own checkpoint round trip (agent.py:521-554).
+
+    Agent A (c1_auto config, seed 0) runs 2 injected steps and writes
+    ``ref_ckpt_c1_auto.pth`` with the reference's save_agent (committed next to
+    this script: a file the reference itself wrote, loaded by the tests with
+    torch.load(weights_only=True)).  Then
+      cont/: A continues with steps 3 and 4 (no reload);
+      load/: a FRESH agent B (seed 5: different init) runs the reference's
+             load_agent on that file and steps 3 and 4 on the same inputs.
+    B's log_alpha stays at the loaded value: load_agent rebinds log_alpha but
+    not alpha_optimizer (agent.py:550-554), so B's alpha steps update an orphan.
+    Full post-step state is stored for both."""
+    from sac.agent import SAC
+
+    c = dict(CONFIGS["c1_auto"])
+    out = {"config": np.array(json.dumps({"name": "ref_ckpt", **c, "cfg": _cfg(c)}))}
+    rng = np.random.default_rng(2024)
+    inputs = [_draw_inputs(rng, c) for _ in range(4)]
+    for k, inp in enumerate(inputs, 1):
+        for kk, v in inp.items():
+            out[f"step{k}/in/{kk}"] = v
+    a = SAC(FakeEnv(c["obs"], c["act"]), _cfg(c))
+    _state(a, True, "init", out)
+    for k in (1, 2):
+        out[f"step{k}/out/losses"] = _inject_step(a, inputs[k - 1])[0]
+    _state(a, True, "step2/post", out)
+    path = os.path.join(OUT, "ref_ckpt_c1_auto.pth")
+    a.save_agent(path)
+    b = SAC(FakeEnv(c["obs"], c["act"]), _cfg(dict(c, seed=5)))
+    _state(b, True, "fresh_init", out)
+    b.load_agent(path)
+    for k in (3, 4):
+        for tag, ag in (("cont", a), ("load", b)):
+            losses, y, lp = _inject_step(ag, inputs[k - 1])
+            out[f"{tag}/step{k}/out/losses"] = losses
+            out[f"{tag}/step{k}/out/y"] = y
+            _state(ag, True, f"{tag}/step{k}/post", out)
+    return out
+
+
+LOOP_CASES = {
+    # tag: (warming_steps, update_frequency, gradient_steps_per_update, capacity, episodes)
+    "w10_u1_g1": (10, 1, 1, 1000, 9),
+    "w13_u3_g2": (13, 3, 2, 1000, 9),
+    "w20_u2_g3_cap32": (20, 2, 3, 32, 10),
+    "w50_u1_g1_cap40": (50, 1, 1, 40, 8),  # warming_steps > capacity: never updates
+}
+
+
+def capture_loop() -> dict:
+    """the reference's run_training_loop (agent.py:329-418) on the
+    deterministic DetEnv (tests/golden/det_env.py: observations, rewards and
+    episode ends depend only on counters, not on actions).  training_step is
+    replaced by a recorder: for every call, the number of transitions pushed so
+    far (= the loop's total_steps) and len(replay_buffer).  Also stored: the
+    final deque content (state, reward, next_state, done; actions are the
+    policy's random draws and are not compared) and the episode count."""
+    from sac.agent import SAC
+
+    sys.path.insert(0, OUT)
+    from det_env import DetEnv
+
+    out = {}
+    c = dict(obs=3, act=2, q_hidden=[16, 16], pi_hidden=[16, 16], batch=8, auto=True)
+    for tag, (W, u, g, cap, n_ep) in LOOP_CASES.items():
+        cfg = _cfg(c)
+        cfg["buffer"]["capacity"] = cap
+        cfg["train"].update(warming_steps=W, update_frequency=u, gradient_steps_per_update=g)
+        agent = SAC(DetEnv(c["obs"], c["act"]), cfg)
+        pushed = [0]
+        calls = []
+        orig_store = agent.store_transition
+
+        def store(*a_, _o=orig_store, _p=pushed):
+            _p[0] += 1
+            return _o(*a_)
+
+        agent.store_transition = store
+        agent.training_step = lambda _c=calls, _p=pushed, _a=agent: _c.append((_p[0], len(_a.replay_buffer)))
+        metrics = agent.run_training_loop(n_ep, tqdm_disable=True)
+        mem = list(agent.replay_buffer.memory)
+        out[f"{tag}/calls"] = np.array(calls, np.int64).reshape(-1, 2)
+        out[f"{tag}/total_steps"] = np.array(pushed[0], np.int64)
+        out[f"{tag}/episodes"] = np.array(metrics["total_episodes"], np.int64)
+        out[f"{tag}/final_avg_return"] = np.array(metrics["final_avg_return"], np.float64)
+        out[f"{tag}/mem_state"] = np.stack([np.asarray(t.state, np.float32) for t in mem])
+        out[f"{tag}/mem_reward"] = np.array([t.reward for t in mem], np.float64)
+        out[f"{tag}/mem_next_state"] = np.stack([np.asarray(t.next_state, np.float32) for t in mem])
+        out[f"{tag}/mem_done"] = np.array([t.done for t in mem], bool)
+        out[f"{tag}/config"] = np.array([W, u, g, cap, n_ep], np.int64)
+    return out
+
+
 def main() -> None:
     _install_stubs()
     sys.path.insert(0, REF)
@@ -316,6 +421,12 @@ def main() -> None:
     if not only or "replay" in only:
         np.savez_compressed(os.path.join(OUT, "replay_sample.npz"), **capture_replay_sample())
         print("replay_sample written")
+    if not only or "ckpt" in only:
+        np.savez_compressed(os.path.join(OUT, "ref_ckpt_c1_auto.npz"), **capture_checkpoint())
+        print("ref_ckpt_c1_auto written (+ ref_ckpt_c1_auto.pth from the reference's save_agent)")
+    if not only or "loop" in only:
+        np.savez_compressed(os.path.join(OUT, "ref_loop.npz"), **capture_loop())
+        print("ref_loop written")
 
 
 if __name__ == "__main__":
