@@ -27,6 +27,7 @@ from __future__ import annotations
 import os
 import pprint
 import random
+import time
 from collections import deque
 from copy import deepcopy
 from typing import Any, Dict, Optional
@@ -73,6 +74,63 @@ def due_updates_gated(old_steps: int, new_steps: int, len_before: int, capacity:
     if first > new_steps:
         return 0
     return due_updates(first - 1, new_steps, update_frequency, gradient_steps)
+
+
+class LossLog:
+    """Loss and throughput scalars for the logger without per-step host syncs
+    (the reference logs none: agent.py:324 drops the alpha
+    dict and the losses are never read).  Every ``every`` gradient steps it
+    queues an async device->pinned copy of the last step's [L_Q1, L_Q2, L_pi,
+    L_alpha, alpha] behind the training launches and logs the previous
+    snapshot once its event has completed; ``finish`` waits for the last one.
+    Tags: Loss/Q1, Loss/Q2, Loss/Policy, Loss/Alpha (auto-tuning only), Alpha,
+    Perf/GradientStepsPerSec, Perf/EnvStepsPerSec (host wall clock between
+    snapshots), all at the gradient-step count of the snapshot."""
+
+    TAGS = ("Loss/Q1", "Loss/Q2", "Loss/Policy", "Loss/Alpha", "Alpha")
+
+    def __init__(self, engine: SacEngine, logger, every: int):
+        self.engine, self.logger, self.every = engine, logger, max(1, int(every))
+        self.buf = torch.zeros(5, dtype=torch.float64, pin_memory=torch.cuda.is_available())
+        self.ev: Optional[torch.cuda.Event] = None
+        self.pending_step = 0
+        self.next_at = self.every
+        self.t0 = time.perf_counter()
+        self.grad0 = engine.steps_done
+        self.env0 = 0
+
+    def _emit(self) -> None:
+        vals = self.buf.tolist()
+        for tag, v in zip(self.TAGS, vals):
+            if not (tag == "Loss/Alpha" and v != v):  # NaN L_alpha: fixed temperature
+                self.logger.log_scalar(tag, v, self.pending_step)
+        self.ev = None
+
+    def after_updates(self, env_steps: int) -> None:
+        eng = self.engine
+        if eng.steps_done < self.next_at:
+            return
+        if self.ev is not None:
+            if not self.ev.query():
+                return  # the previous snapshot has not landed: skip this one, never block
+            self._emit()
+        now = time.perf_counter()
+        dt = max(now - self.t0, 1e-9)
+        self.logger.log_scalar("Perf/GradientStepsPerSec", (eng.steps_done - self.grad0) / dt, eng.steps_done)
+        self.logger.log_scalar("Perf/EnvStepsPerSec", (env_steps - self.env0) / dt, eng.steps_done)
+        self.t0, self.grad0, self.env0 = now, eng.steps_done, env_steps
+        with torch.cuda.device(eng.device):
+            snap = torch.cat([eng.stats[:4].double(), eng.alpha_state[1:2]])
+            self.buf.copy_(snap, non_blocking=True)
+            self.ev = torch.cuda.Event()
+            self.ev.record()
+        self.pending_step = eng.steps_done
+        self.next_at = (eng.steps_done // self.every + 1) * self.every
+
+    def finish(self) -> None:
+        if self.ev is not None:
+            self.ev.synchronize()
+            self._emit()
 
 
 class SAC:
@@ -272,6 +330,13 @@ class SAC:
             self.replay_buffer._check(self.config["train"]["batch_size"])
             eng.train_graph(self.replay_buffer, n, self.graph_chunk)
 
+    def _loss_log(self, active_logger) -> Optional[LossLog]:
+        """logger.log_losses_every (default 1000 gradient steps; 0 = off)."""
+        every = int(self.config["logger"].get("log_losses_every", 1000))
+        if active_logger is None or self.engine is None or every <= 0 or not hasattr(active_logger, "log_scalar"):
+            return None
+        return LossLog(self.engine, active_logger, every)
+
     def last_losses(self) -> Dict[str, float]:
         """Losses of the last step (reads device memory: synchronises)."""
         l = self._engine().losses()
@@ -310,6 +375,7 @@ class SAC:
         tr = self.config["train"]
         update_every = tr.get("update_frequency", 1)
         n_grad = tr.get("gradient_steps_per_update", 1)
+        loss_log = self._loss_log(active_logger)
         for episode in _tqdm(range(num_episodes), disable=tqdm_disable):
             state, _ = self.env.reset()
             done = False
@@ -327,6 +393,8 @@ class SAC:
                 total_steps += 1
                 if self.can_update() and total_steps % update_every == 0:
                     self._run_updates(n_grad)
+                    if loss_log is not None:
+                        loss_log.after_updates(total_steps)
                 if active_logger is not None and self.config["logger"]["log_q_values"]:
                     self._log_q_values(
                         states=torch.FloatTensor(np.asarray(state)).unsqueeze(0).to(self.device),
@@ -342,6 +410,8 @@ class SAC:
                       f"Average Return(last 100 episodes): {avg_return:.2f}")
         if self.engine is not None:
             self.engine.check()
+        if loss_log is not None:
+            loss_log.finish()
         metrics = {"total_episodes": total_episodes, "best_avg_return": best_avg_return,
                    "final_avg_return": avg_return}
         if active_logger is not None:
@@ -396,6 +466,7 @@ class SAC:
         avg_return = float("nan")
         total_steps = total_episodes = grad_steps = 0
         log_episodes = active_logger is not None and self.config["logger"]["log_episode_stats"]
+        loss_log = self._loss_log(active_logger)
         pbar = _tqdm(range((int(total_env_steps) + N - 1) // N), disable=tqdm_disable)
         for _ in pbar:
             actions = self.select_actions(obs)
@@ -410,6 +481,8 @@ class SAC:
             if self.can_update() and due:
                 self._run_updates(due)
                 grad_steps += due
+                if loss_log is not None:
+                    loss_log.after_updates(total_steps)
             ep_ret += rewards
             ep_len += 1
             for i in np.nonzero(dones)[0]:
@@ -428,6 +501,8 @@ class SAC:
             obs = next_obs
         if self.engine is not None:
             self.engine.check()  # a timed-out hand-off invalidates the run: raise, do not report it
+        if loss_log is not None:
+            loss_log.finish()
         metrics = {"total_episodes": total_episodes, "best_avg_return": best_avg_return,
                    "final_avg_return": avg_return, "total_env_steps": total_steps, "gradient_steps": grad_steps}
         if active_logger is not None:

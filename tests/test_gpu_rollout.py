@@ -126,3 +126,48 @@ def test_vectorized_loop_many_envs_runs_and_counts():
     assert agent.engine.steps_done == m["gradient_steps"]
     agent.engine.check()
     assert all(np.isfinite(agent.engine.losses()[:3]))
+
+
+def test_loss_and_throughput_scalars_are_logged(tmp_path):
+    """the training loops log Loss/Q1, Loss/Q2, Loss/Policy,
+    Loss/Alpha, Alpha and Perf/* scalars every logger.log_losses_every gradient
+    steps from async snapshots (no per-step host sync); the snapshot values are
+    the engine's own losses."""
+    from sac.agent import SAC
+    from sac.utils.experiment_logger import ExperimentLogger
+    from sac.vector_env import SyncVectorEnv
+
+    cfg = _cfg(batch=16, warming=32, precision="fp32")
+    cfg["logger"].update(enabled=False, log_dir=str(tmp_path), run_name="t", use_timestamp=False,
+                         log_losses_every=8)
+    agent = SAC(SyncVectorEnv([_env] * 4), cfg)
+    logger = ExperimentLogger(cfg["logger"], env_name="probe", agent_name="SAC")
+    m = agent.run_vectorized_training_loop(4 * 40, logger=logger)
+    torch.cuda.synchronize()
+    rec = {}
+    for tag, v, step in logger.metrics_writer.scalars:
+        rec.setdefault(tag, []).append((step, v))
+    for tag in ("Loss/Q1", "Loss/Q2", "Loss/Policy", "Loss/Alpha", "Alpha", "Perf/GradientStepsPerSec",
+                "Perf/EnvStepsPerSec"):
+        assert tag in rec and len(rec[tag]) >= 2, (tag, rec.keys())
+        assert all(np.isfinite(v) for _, v in rec[tag]), tag
+        steps = [s for s, _ in rec[tag]]
+        assert steps == sorted(steps) and steps[-1] <= m["gradient_steps"]
+    assert all(v > 0 for _, v in rec["Perf/GradientStepsPerSec"])
+    # a snapshot is exactly the engine's stats at that step: re-snapshot now and compare
+    from sac.agent import LossLog
+
+    ll = LossLog(agent.engine, logger, 1)
+    ll.after_updates(m["total_env_steps"])
+    ll.finish()
+    l = agent.engine.losses()
+    last = {tag: rec2[-1][1] for tag, rec2 in _group(logger.metrics_writer.scalars).items()}
+    assert last["Loss/Q1"] == pytest.approx(l[0], rel=1e-6) and last["Loss/Policy"] == pytest.approx(l[2], rel=1e-6)
+    assert last["Alpha"] == pytest.approx(float(agent.engine.alpha_state[1]), rel=1e-12)
+
+
+def _group(scalars):
+    out = {}
+    for tag, v, step in scalars:
+        out.setdefault(tag, []).append((step, v))
+    return out
