@@ -401,12 +401,17 @@ static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
   h.split = split;
   h.gs2 = SAC_ROWS * std::max(2 * A, A + 1);
   h.gran2 = (uint64_t*)P(lay.take((size_t)GS_COUNT * nrt * 2 * h.gs2 * 8));
-  int nB = 0, nD = 0;
+  int nB = 0, nD = 0, nhalf = 0;
   for (int ni = NET_PI; ni <= NET_Q2; ++ni)
-    for (int l = 0; l < h.net[ni].L; ++l)
-      (ni == NET_PI ? nD : nB) += (h.net[ni].l[l].Np / 32) * (h.net[ni].l[l].Kp / 32);
+    for (int l = 0; l < h.net[ni].L; ++l) {
+      const int t = (h.net[ni].l[l].Np / 32) * (h.net[ni].l[l].Kp / 32);
+      const int halves = (l == 0 && split) ? 2 : 1;  // split layer 0: one block per batch half
+      (ni == NET_PI ? nD : nB) += t * halves;
+      if (halves == 2) nhalf += t;
+    }
   const size_t o_tB = lay.take((size_t)nB * sizeof(TileDesc));
   const size_t o_tD = lay.take((size_t)nD * sizeof(TileDesc));
+  const size_t o_part = lay.take((size_t)nhalf * 1024 * 8);  // batch-half partial dW granules of split tiles
   const size_t total = lay.take(0);
 
   // LDS layout (floats)
@@ -522,10 +527,9 @@ static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
     e->h.nD = nD;
     e->lds_bytes = (size_t)lo * 4;
     {  // update tiles stage up to 4 batch chunks of 512 B per operand row per round
-       // (enough for the longest operand row, the split layer 0's 2 Bp columns)
+       // (every tile reduces over at most Bp columns: split layer 0 is two half tiles)
       const int bch = 512 / esz;
-      const int bp_max = split ? 2 * Bp : Bp;
-      e->h.upd_slots = std::min(4, (bp_max + bch - 1) / bch);
+      e->h.upd_slots = std::min(4, (Bp + bch - 1) / bch);
       e->upd_lds = SAC_UPD_LDS_FOR(e->h.upd_slots);
     }
     e->nrt = nrt;
@@ -533,6 +537,8 @@ static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
     const int esz2 = esz;
     e->hostB.clear();
     e->hostD.clear();
+    std::vector<TileDesc> halvesB, halvesD;
+    int ihalf = 0;
     for (int ni = NET_PI; ni <= NET_Q2; ++ni) {
       const NetDev& nd = h.net[ni];
       const NetDev& tn = h.net[ni == NET_PI ? NET_PI : ni + 2];
@@ -569,12 +575,28 @@ static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
             t.k0 = kt * 32;
             t.opt = ni;
             t.nrt = (l == 0 && split) ? 2 * Bp / SAC_ROWS : nrt;
+            t.ld = t.bp;
+            t.khalf = 0;
+            if (l == 0 && split) {  // consumer half (columns [0, Bp)) + producer half ([Bp, 2 Bp))
+              t.bp = Bp;
+              t.khalf = 1;
+              t.part = (uint64_t*)(base + o_part) + (size_t)ihalf * 1024;
+              ++ihalf;
+              TileDesc pt = t;
+              pt.khalf = 2;
+              pt.GT = (const char*)t.GT + (size_t)Bp * esz2;
+              pt.XT = (const char*)t.XT + (size_t)Bp * esz2;
+              (ni == NET_PI ? halvesD : halvesB).push_back(pt);
+            }
             (ni == NET_PI ? e->hostD : e->hostB).push_back(t);
           }
       }
     }
     xcd_order(e->hostB);
     xcd_order(e->hostD);
+    // producer halves first: in-order dispatch starts every producer before its consumer
+    e->hostB.insert(e->hostB.begin(), halvesB.begin(), halvesB.end());
+    e->hostD.insert(e->hostD.begin(), halvesD.begin(), halvesD.end());
     e->h.nBq[0] = e->h.nBq[1] = 0;
     for (const TileDesc& t : e->hostB) ++e->h.nBq[t.opt - 1];
     {

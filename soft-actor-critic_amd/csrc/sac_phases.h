@@ -145,8 +145,16 @@ struct TileDesc {
   const float* dbp;
   long xt_par;     // element offset of the odd-step X^T copy (pi tiles), else 0
   int K, N, Kp, Np, n0, k0, opt, nrt;
-  int bp;          // batch columns of the GT / XT operands (Bp; 2 Bp for a hidden-split layer 0:
-                   // the two halves' partial dY side by side, X duplicated)
+  int bp;          // batch columns this tile reduces over
+  int ld;          // row stride of the GT / XT operands in elements (Bp; 2 Bp for a hidden-split
+                   // layer 0: the two halves' partial dY side by side, X duplicated)
+  // A hidden-split layer-0 tile is two blocks, one per batch half (bp = Bp each,
+  // so no block streams more operand bytes than a plain tile): khalf 2 publishes
+  // its partial dW as 1024 data-tagged granules (part: {value, launch epoch},
+  // one 8-B sc1 store each, no drain or flag); khalf 1 polls them, adds them to
+  // its own half (own + peer: fixed order) and runs Adam.  0: a whole tile.
+  int khalf;
+  uint64_t* part;
 };
 
 
@@ -874,7 +882,7 @@ __device__ __forceinline__ void dw_adam_tile(const AS_C EngineDev& E, const Tile
     v[e] = Wv[idx[e]];
     tp[e] = polyak ? tW[idx[e]] : 0.f;
   }
-  const bool do_bias = td.k0 == 0;
+  const bool do_bias = td.k0 == 0 && td.khalf != 2;
   float pb = 0.f, mb = 0.f, vb = 0.f, tbv = 0.f;
   if (do_bias && tid < 32 && td.n0 + tid < td.N) {
     pb = GPC(float, td.b)[td.n0 + tid];
@@ -931,8 +939,8 @@ __device__ __forceinline__ void dw_adam_tile(const AS_C EngineDev& E, const Tile
         for (int pi = 0; pi < PPT; ++pi) {
           const int i = tid + pi * UT;
           const int row = i / per_row, pc = i % per_row;
-          const AS_G T* src = row < 32 ? GPC(T, td.GT) + (size_t)row * Bp
-                                       : GPC(T, td.XT) + par * td.xt_par + (size_t)(row - 32) * Bp;
+          const AS_G T* src = row < 32 ? GPC(T, td.GT) + (size_t)row * td.ld
+                                       : GPC(T, td.XT) + par * td.xt_par + (size_t)(row - 32) * td.ld;
           if (i < 64 * per_row) rg[sl][pi] = *(const AS_G u32x4*)(src + b0 + pc * EPR);
         }
       }
@@ -1006,6 +1014,32 @@ __device__ __forceinline__ void dw_adam_tile(const AS_C EngineDev& E, const Tile
     if (do_bias && t < 512) red[(t >> 4) * 17 + (t & 15)] = bsum[j];
   }
   __syncthreads();
+  if (td.khalf) {  // hidden-split layer 0: the two batch halves of this tile meet here
+    const uint32_t ep = *GPC(uint32_t, E.sync) + 1u;  // per launch (B and D have their own granules)
+    if (td.khalf == 2) {
+      for (int el = tid; el < 1024; el += UT) {
+        const uint64_t x = (uint64_t)__float_as_uint(accs[(el >> 5) * 33 + (el & 31)]) | ((uint64_t)ep << 32);
+        __hip_atomic_store(td.part + el, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      return;  // uniform: the peer block runs Adam on the sum
+    }
+    for (int el = tid; el < 1024; el += UT) {
+      uint64_t x = 0;
+      for (int it = 0;; ++it) {
+        x = __hip_atomic_load(td.part + el, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if ((uint32_t)(x >> 32) == ep) break;
+        if (it > E.spin_limit) {  // the producer half never ran: flag the error, do not hang
+          __hip_atomic_store((uint32_t*)GP(uint32_t, E.sync) + 1 /* SYNC_TIMEOUT */, 1u, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      const int o = (el >> 5) * 33 + (el & 31);
+      accs[o] = accs[o] + __uint_as_float((uint32_t)x);
+    }
+    __syncthreads();
+  }
   STAMP(polyak ? 50 : 54);
   // ---- 3. elements: Adam + Polyak on the masters; new values -> LDS
   const float w1 = (float)(1.0 - (double)E.beta1), b2 = E.beta2, w2 = (float)(1.0 - (double)E.beta2);
