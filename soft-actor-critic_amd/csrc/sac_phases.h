@@ -1284,6 +1284,30 @@ __device__ __forceinline__ float gran_get(const AS_C EngineDev& E, const AS_G ui
   return __uint_as_float((uint32_t)x);
 }
 
+// one lane: N granules polled together (every load of a poll in flight at once:
+// one round trip once the producers have stored, not N in sequence)
+template <int N>
+__device__ __forceinline__ void gran_getn(const AS_C EngineDev& E, const AS_G uint64_t* const (&g)[N], uint32_t ep,
+                                          float (&out)[N]) {
+  uint64_t x[N];
+  for (int it = 0;; ++it) {
+#pragma unroll
+    for (int i = 0; i < N; ++i) x[i] = __hip_atomic_load((uint64_t*)g[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    bool all = true;
+#pragma unroll
+    for (int i = 0; i < N; ++i) all = all && (uint32_t)(x[i] >> 32) == ep;
+    if (all) break;
+    if (it > E.spin_limit) {
+      __hip_atomic_store((uint32_t*)GP(uint32_t, E.sync) + SYNC_TIMEOUT, 1u, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+      break;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+#pragma unroll
+  for (int i = 0; i < N; ++i) out[i] = __uint_as_float((uint32_t)x[i]);
+}
+
 // ============================================================================ sample + gather
 // Row tile r0's replay slots for `step` (replay_buffer.py:32-39: distinct
 // uniform logical rows, 0 = oldest; -1 for padding rows): threads tid < R.

@@ -234,13 +234,14 @@ __device__ __forceinline__ void target_critic_split_body(const EngineDev* __rest
   const AS_C LayerDev& L1 = net.l[1];
   const AS_C LayerDev& L2 = net.l[2];
   STAMP(0);
-  // this role's weights, issued first: layer 0 (first HC0 chunks) and the half of layer 1
+  // this role's weights: layer 0 (first HC0 chunks) first; the half of layer 1
+  // (the bulk of the bytes) after the batch record's loads, so the waits for
+  // the record do not include it (loads complete in issue order)
   const GemmW w0 = gw_fwd(L0);
   const GemmW w1 = gw_sub<T>(L1.Wc, L1.Kp, h * HH, HH, 0, L1.Kp, L1.bias + h * HH, HH);
   HTiles<T, 2, HC0> h0;
   HTiles<T, 1, NCH_H> h1;
   ht_issue<T, 2, HC0>(h0, w0);
-  ht_issue<T, 1, NCH_H>(h1, w1);
 
   const int B = E.B, Bp = E.Bp, O = E.O, A = E.A, ld = E.ld, ldo = E.ldo;
   const int r0 = rbi * R;
@@ -287,22 +288,55 @@ __device__ __forceinline__ void target_critic_split_body(const EngineDev* __rest
   // ---- sample (replay_buffer.py:32-39) + gather (agent.py:166-193): the staged record or a gather
   const int64_t rb_size = GPC(int64_t, rb.state)[0], rb_pos = GPC(int64_t, rb.state)[1];
   bool staged = false;
+  bool h1_issued = false;
   if (E.stage && !inj_idx) {
     const AS_G float* rec = GPC(float, E.stg) + (size_t)rbi * E.stg_stride;
     const AS_C uint64_t* hdr = (const AS_C uint64_t*)rec;
     const AS_G float* p = rec + 16;
-    for (int i = tid; i < R * O; i += SAC_THREADS) {
-      sB[i] = p[i];
-      s2B[i] = p[R * O + i];
-    }
-    for (int i = tid; i < R * A; i += SAC_THREADS) aB[i] = p[2 * R * O + i];
-    if (tid < R) {
-      rB[tid] = p[2 * R * O + R * A + tid];
-      dB[tid] = p[2 * R * O + R * A + R + tid];
+    constexpr int NS = (R * 32 + SAC_THREADS - 1) / SAC_THREADS;
+    if (O <= 32) {  // uniform: record -> registers, layer-1 weights issued behind it, -> LDS
+      float rs[2][NS], ra[NS], rr = 0.f, rd = 0.f;
+#pragma unroll
+      for (int u = 0; u < NS; ++u) {
+        const int i = tid + u * SAC_THREADS;
+        rs[0][u] = i < R * O ? p[i] : 0.f;
+        rs[1][u] = i < R * O ? p[R * O + i] : 0.f;
+        ra[u] = i < R * A ? p[2 * R * O + i] : 0.f;
+      }
+      if (tid < R) {
+        rr = p[2 * R * O + R * A + tid];
+        rd = p[2 * R * O + R * A + R + tid];
+      }
+      ht_issue<T, 1, NCH_H>(h1, w1);
+      h1_issued = true;
+#pragma unroll
+      for (int u = 0; u < NS; ++u) {
+        const int i = tid + u * SAC_THREADS;
+        if (i < R * O) {
+          sB[i] = rs[0][u];
+          s2B[i] = rs[1][u];
+        }
+        if (i < R * A) aB[i] = ra[u];
+      }
+      if (tid < R) {
+        rB[tid] = rr;
+        dB[tid] = rd;
+      }
+    } else {
+      for (int i = tid; i < R * O; i += SAC_THREADS) {
+        sB[i] = p[i];
+        s2B[i] = p[R * O + i];
+      }
+      for (int i = tid; i < R * A; i += SAC_THREADS) aB[i] = p[2 * R * O + i];
+      if (tid < R) {
+        rB[tid] = p[2 * R * O + R * A + tid];
+        dB[tid] = p[2 * R * O + R * A + R + tid];
+      }
     }
     staged = hdr[0] == step && hdr[1] == (uint64_t)rb_size && hdr[2] == (uint64_t)rb_pos &&
              hdr[3] == (uint64_t)(uintptr_t)rb.obs && hdr[4] == (uint64_t)GPC(int64_t, rb.state)[2];
   }
+  if (!h1_issued) ht_issue<T, 1, NCH_H>(h1, w1);
   if (staged && rbi == 0 && role == 0 && h == 0 && tid == 0)
     *(AS_G uint64_t*)(GP(uint32_t, E.sync) + 4) = step;  // SYNC_STAGED (tests)
   if (!staged) {  // uniform
@@ -347,11 +381,18 @@ __device__ __forceinline__ void target_critic_split_body(const EngineDev* __rest
       if (live) {
         float mu, lsr;
         if (tgt) {
-          mu = (gran_get(E, g0 + r * 2 * A + j, ep) + gran_get(E, g1 + r * 2 * A + j, ep)) + b2[j];
-          lsr = (gran_get(E, g0 + r * 2 * A + A + j, ep) + gran_get(E, g1 + r * 2 * A + A + j, ep)) + b2[A + j];
+          const AS_G uint64_t* gg[4] = {g0 + r * 2 * A + j, g1 + r * 2 * A + j, g0 + r * 2 * A + A + j,
+                                        g1 + r * 2 * A + A + j};
+          float v[4];
+          gran_getn<4>(E, gg, ep, v);
+          mu = (v[0] + v[1]) + b2[j];
+          lsr = (v[2] + v[3]) + b2[A + j];
         } else {  // g0 / g1 = this half's own partial (in outB) and the peer's granules, in half order
           const float pown0 = outB[r * ldo + j], pown1 = outB[r * ldo + A + j];
-          const float ppe0 = gran_get(E, g1 + r * 2 * A + j, ep), ppe1 = gran_get(E, g1 + r * 2 * A + A + j, ep);
+          const AS_G uint64_t* gg[2] = {g1 + r * 2 * A + j, g1 + r * 2 * A + A + j};
+          float v[2];
+          gran_getn<2>(E, gg, ep, v);
+          const float ppe0 = v[0], ppe1 = v[1];
           mu = (h == 0 ? pown0 + ppe0 : ppe0 + pown0) + b2[j];
           lsr = (h == 0 ? pown1 + ppe1 : ppe1 + pown1) + b2[A + j];
         }
@@ -526,18 +567,24 @@ __device__ __forceinline__ void target_critic_split_body(const EngineDev* __rest
         const bool v = tid < nvalid;
         const float b2 = GPC(float, L2.bias)[0];
         const float mine = outB[tid * ldo];
-        const float peer = gran_get(E, gs_at(E, qi ? GS_QA2 : GS_QA1, rbi, 1 - h) + tid, ep);
+        // every granule this row needs, polled together: peer half's q partial,
+        // both target critics' two halves, log pi(a'|s')
+        const AS_G uint64_t* gg[6] = {gs_at(E, qi ? GS_QA2 : GS_QA1, rbi, 1 - h) + tid,
+                                      gs_at(E, GS_QT1, rbi, 0) + tid, gs_at(E, GS_QT1, rbi, 1) + tid,
+                                      gs_at(E, GS_QT2, rbi, 0) + tid, gs_at(E, GS_QT2, rbi, 1) + tid,
+                                      gs_at(E, GS_LP, rbi, 0) + tid};
+        float gv[6];
+        gran_getn<6>(E, gg, ep, gv);
+        const float peer = gv[0];
         const float qpre = (h == 0 ? mine + peer : peer + mine) + b2;
         const float q = net.out_act == ACT_ID ? qpre : act_fwd(net.out_act, qpre);
         const AS_C NetDev& t1 = E.net[NET_Q1T];
         const AS_C NetDev& t2 = E.net[NET_Q2T];
-        const float q1tp = gran_get(E, gs_at(E, GS_QT1, rbi, 0) + tid, ep) +
-                           gran_get(E, gs_at(E, GS_QT1, rbi, 1) + tid, ep) + GPC(float, t1.l[2].bias)[0];
-        const float q2tp = gran_get(E, gs_at(E, GS_QT2, rbi, 0) + tid, ep) +
-                           gran_get(E, gs_at(E, GS_QT2, rbi, 1) + tid, ep) + GPC(float, t2.l[2].bias)[0];
+        const float q1tp = gv[1] + gv[2] + GPC(float, t1.l[2].bias)[0];
+        const float q2tp = gv[3] + gv[4] + GPC(float, t2.l[2].bias)[0];
         const float q1t = t1.out_act == ACT_ID ? q1tp : act_fwd(t1.out_act, q1tp);
         const float q2t = t2.out_act == ACT_ID ? q2tp : act_fwd(t2.out_act, q2tp);
-        const float lp2 = gran_get(E, gs_at(E, GS_LP, rbi, 0) + tid, ep);
+        const float lp2 = gv[5];
         const float y = rB[tid] + (E.gamma * (1.f - dB[tid])) * (fmin_nan(q1t, q2t) - alpha32 * lp2);
         if (qi == 0 && h == 0 && b < B) stats[4 + b] = y;
         const float d = q - y;
@@ -740,10 +787,11 @@ __device__ __forceinline__ void actor_split_body(const EngineDev* __restrict__ E
       const bool v = tid < nvalid;
       const AS_C NetDev& q1n = E.net[NET_Q1];
       const AS_C NetDev& q2n = E.net[NET_Q2];
-      const float q1p = gran_get(E, c10 + R * A + tid, ep) + gran_get(E, c11 + R * A + tid, ep) +
-                        GPC(float, q1n.l[2].bias)[0];
-      const float q2p = gran_get(E, c20 + R * A + tid, ep) + gran_get(E, c21 + R * A + tid, ep) +
-                        GPC(float, q2n.l[2].bias)[0];
+      const AS_G uint64_t* gg[4] = {c10 + R * A + tid, c11 + R * A + tid, c20 + R * A + tid, c21 + R * A + tid};
+      float gv[4];
+      gran_getn<4>(E, gg, ep, gv);
+      const float q1p = gv[0] + gv[1] + GPC(float, q1n.l[2].bias)[0];
+      const float q2p = gv[2] + gv[3] + GPC(float, q2n.l[2].bias)[0];
       const float q1 = q1n.out_act == ACT_ID ? q1p : act_fwd(q1n.out_act, q1p);
       const float q2 = q2n.out_act == ACT_ID ? q2p : act_fwd(q2n.out_act, q2p);
       const float m = fmin_nan(q1, q2);
@@ -762,8 +810,11 @@ __device__ __forceinline__ void actor_split_body(const EngineDev* __restrict__ E
   __syncthreads();
   for (int i = tid; i < R * A; i += SAC_THREADS) {
     const int r = i / A;
-    const float da1 = gran_get(E, c10 + i, ep) + gran_get(E, c11 + i, ep);
-    const float da2 = gran_get(E, c20 + i, ep) + gran_get(E, c21 + i, ep);
+    const AS_G uint64_t* gg[4] = {c10 + i, c11 + i, c20 + i, c21 + i};
+    float gv[4];
+    gran_getn<4>(E, gg, ep, gv);  // all four are in by now (the q granules above came after them)
+    const float da1 = gv[0] + gv[1];
+    const float da2 = gv[2] + gv[3];
     gaB[i] = g1B[r] * da1 + g2B[r] * da2;
   }
   __syncthreads();
