@@ -374,8 +374,11 @@ __device__ __forceinline__ void target_critic_split_body(const EngineDev* __rest
     const AS_G float* b2 = GPC(float, pn.l[2].bias);
     const int AP = A <= 1 ? 1 : 1 << (32 - __builtin_clz(A - 1));
     const int rpp = SAC_THREADS / AP;
+    const int jj = tid % AP;
+    // this lane's head biases, loaded before the polls (not one more round trip after them)
+    const float b2mu = jj < A ? b2[jj] : 0.f, b2ls = jj < A ? b2[A + jj] : 0.f;
     for (int base = 0; base < R; base += rpp) {
-      const int r = base + tid / AP, j = tid % AP;
+      const int r = base + tid / AP, j = jj;
       const bool live = r < R && j < A;
       float lp = 0.f, corr = 0.f;
       if (live) {
@@ -385,16 +388,16 @@ __device__ __forceinline__ void target_critic_split_body(const EngineDev* __rest
                                         g1 + r * 2 * A + A + j};
           float v[4];
           gran_getn<4>(E, gg, ep, v);
-          mu = (v[0] + v[1]) + b2[j];
-          lsr = (v[2] + v[3]) + b2[A + j];
+          mu = (v[0] + v[1]) + b2mu;
+          lsr = (v[2] + v[3]) + b2ls;
         } else {  // g0 / g1 = this half's own partial (in outB) and the peer's granules, in half order
           const float pown0 = outB[r * ldo + j], pown1 = outB[r * ldo + A + j];
           const AS_G uint64_t* gg[2] = {g1 + r * 2 * A + j, g1 + r * 2 * A + A + j};
           float v[2];
           gran_getn<2>(E, gg, ep, v);
           const float ppe0 = v[0], ppe1 = v[1];
-          mu = (h == 0 ? pown0 + ppe0 : ppe0 + pown0) + b2[j];
-          lsr = (h == 0 ? pown1 + ppe1 : ppe1 + pown1) + b2[A + j];
+          mu = (h == 0 ? pown0 + ppe0 : ppe0 + pown0) + b2mu;
+          lsr = (h == 0 ? pown1 + ppe1 : ppe1 + pown1) + b2ls;
         }
         const float e = epsB[r * A + j];
         const float lo = E.ls_min, hi = E.ls_max;
@@ -566,6 +569,9 @@ __device__ __forceinline__ void target_critic_split_body(const EngineDev* __rest
         const int b = r0 + tid;
         const bool v = tid < nvalid;
         const float b2 = GPC(float, L2.bias)[0];
+        const AS_C NetDev& t1 = E.net[NET_Q1T];
+        const AS_C NetDev& t2 = E.net[NET_Q2T];
+        const float bt1 = GPC(float, t1.l[2].bias)[0], bt2 = GPC(float, t2.l[2].bias)[0];  // before the poll
         const float mine = outB[tid * ldo];
         // every granule this row needs, polled together: peer half's q partial,
         // both target critics' two halves, log pi(a'|s')
@@ -578,10 +584,8 @@ __device__ __forceinline__ void target_critic_split_body(const EngineDev* __rest
         const float peer = gv[0];
         const float qpre = (h == 0 ? mine + peer : peer + mine) + b2;
         const float q = net.out_act == ACT_ID ? qpre : act_fwd(net.out_act, qpre);
-        const AS_C NetDev& t1 = E.net[NET_Q1T];
-        const AS_C NetDev& t2 = E.net[NET_Q2T];
-        const float q1tp = gv[1] + gv[2] + GPC(float, t1.l[2].bias)[0];
-        const float q2tp = gv[3] + gv[4] + GPC(float, t2.l[2].bias)[0];
+        const float q1tp = gv[1] + gv[2] + bt1;
+        const float q2tp = gv[3] + gv[4] + bt2;
         const float q1t = t1.out_act == ACT_ID ? q1tp : act_fwd(t1.out_act, q1tp);
         const float q2t = t2.out_act == ACT_ID ? q2tp : act_fwd(t2.out_act, q2tp);
         const float lp2 = gv[5];
@@ -676,6 +680,14 @@ __device__ __forceinline__ void actor_split_body(const EngineDev* __restrict__ E
     HTiles<T, 1, NCH_H> h1;
     ht_issue<T, 2, HC0>(h0, w0);
     ht_issue<T, 1, NCH_H>(h1, w1);
+    // layer-1 dX operand of this half, held from the start as well (its fetch
+    // would otherwise sit between the forward pass and the backward GEMM)
+    const GemmW wt1 = gw_sub<T>(L1.WTc, L1.Np, 0, L1.Kp, h * HH, HH, nullptr, 0);
+    HTiles<T, 2, NCH_HH> ht1;
+    ht_issue<T, 2, NCH_HH>(ht1, wt1);
+    // the W2 (fp32 master) element of this thread's column n = tid % HH of the unit-seed backward
+    static_assert(SAC_THREADS % HH == 0, "one W2 column per thread in the unit-seed loop");
+    const float w2n = GPC(float, net.P + L2.w_off)[h * HH + tid % HH];
     for (int i = tid; i < R * O; i += SAC_THREADS) sB[i] = GPC(float, E.s_st)[(size_t)r0 * O + i];
     for (int i = tid; i < R * A; i += SAC_THREADS) aB[i] = GPC(float, E.a_st)[(size_t)r0 * A + i];
     __syncthreads();
@@ -712,10 +724,6 @@ __device__ __forceinline__ void actor_split_body(const EngineDev* __restrict__ E
     });
     if (act != ACT_RELU && act != ACT_ID) act_pass_fwd<R>(H1, ldh1, HH >> 4, act);
     __syncthreads();
-    // layer-1 dX operand of this half, issued now (h1's registers are free)
-    const GemmW wt1 = gw_sub<T>(L1.WTc, L1.Np, 0, L1.Kp, h * HH, HH, nullptr, 0);
-    HTiles<T, 2, NCH_HH> ht1;
-    ht_issue<T, 2, NCH_HH>(ht1, wt1);
     {
       GemmW w2 = gw_sub<T>(L2.Wc, L2.Kp, 0, L2.Np, h * HH, HH, nullptr, 0);
       w2.NT = (L2.N + 15) >> 4;
@@ -724,10 +732,9 @@ __device__ __forceinline__ void actor_split_body(const EngineDev* __restrict__ E
     STAMP(36 + qi);
     // unit-seed backward down to a~ (the pi role applies the min-Q weights and act'(q))
     {
-      const AS_G float* w2row = GPC(float, net.P + L2.w_off) + h * HH;
       for (int i = tid; i < R * HH; i += SAC_THREADS) {
-        const int r = i / HH, n = i % HH;
-        U1[r * ldu1 + n] = act_bwd(act, P1[r * ldp1 + n], w2row[n]);
+        const int r = i / HH, n = i % HH;  // n == tid % HH
+        U1[r * ldu1 + n] = act_bwd(act, P1[r * ldp1 + n], w2n);
       }
       __syncthreads();
       gemm_hs<T, 2, NCH_HH>(U1, ldu1, wt1, &ht1, [&](int j, int col, const f32x4& acc) {
@@ -774,6 +781,15 @@ __device__ __forceinline__ void actor_split_body(const EngineDev* __restrict__ E
     for (int i = tid; i < R * HH; i += SAC_THREADS) P1[(i / HH) * ldp1 + i % HH] = p1[(i / HH) * L1.Np + i % HH];
     if (tid < R) lpB[tid] = GPC(float, E.lp_st)[par * E.Br + r0 + tid];
   }
+  // the head stash of this thread's (row, dim) and the critics' output biases,
+  // loaded now: after the critics' hand-off they would be one more round trip
+  float hsv[4] = {0.f, 0.f, 0.f, 0.f};
+  if (tid < R * A && r0 + tid / A < E.Br) {
+    const AS_G float* hs = GPC(float, E.head_st) + (size_t)(r0 + tid / A) * 4 * A;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) hsv[q] = hs[q * A + tid % A];
+  }
+  const float bq1 = GPC(float, E.net[NET_Q1].l[2].bias)[0], bq2 = GPC(float, E.net[NET_Q2].l[2].bias)[0];
   __syncthreads();
   STAMP(34);
   // combine the critics' unit-seed partials with the min-Q weights (L_pi = mean(alpha logpi - min Q))
@@ -790,8 +806,8 @@ __device__ __forceinline__ void actor_split_body(const EngineDev* __restrict__ E
       const AS_G uint64_t* gg[4] = {c10 + R * A + tid, c11 + R * A + tid, c20 + R * A + tid, c21 + R * A + tid};
       float gv[4];
       gran_getn<4>(E, gg, ep, gv);
-      const float q1p = gv[0] + gv[1] + GPC(float, q1n.l[2].bias)[0];
-      const float q2p = gv[2] + gv[3] + GPC(float, q2n.l[2].bias)[0];
+      const float q1p = gv[0] + gv[1] + bq1;
+      const float q2p = gv[2] + gv[3] + bq2;
       const float q1 = q1n.out_act == ACT_ID ? q1p : act_fwd(q1n.out_act, q1p);
       const float q2 = q2n.out_act == ACT_ID ? q2p : act_fwd(q2n.out_act, q2p);
       const float m = fmin_nan(q1, q2);
@@ -820,13 +836,14 @@ __device__ __forceinline__ void actor_split_body(const EngineDev* __restrict__ E
   __syncthreads();
   STAMP(39);
   // squashed-Gaussian head backward (models.py:79-87), one lane per (row, action dim)
-  for (int i = tid; i < R * A; i += SAC_THREADS) {
-    const int r = i / A, j = i % A, b = r0 + r;
+  static_assert(SAC_ROWS * 32 <= SAC_THREADS, "one (row, action dim) per thread");
+  if (tid < R * A) {
+    const int i = tid;
+    const int r = i / A, j = i % A;
     const bool v = r < nvalid;
     const float gl = v ? alpha32 * (1.0f / (float)B) : 0.f;
-    const AS_G float* hs = GPC(float, E.head_st) + (size_t)b * 4 * A;
     const float lo = E.ls_min, hi = E.ls_max, scale = E.scale;
-    const float mu = hs[j], lsr = hs[A + j], z = hs[2 * A + j], e = hs[3 * A + j];
+    const float mu = hsv[0], lsr = hsv[1], z = hsv[2], e = hsv[3];
     const float ls = lsr < lo ? lo : (lsr > hi ? hi : lsr);
     const float sd = expf(ls);
     const float t = tanhf(z);
