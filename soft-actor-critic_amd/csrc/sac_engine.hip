@@ -337,10 +337,16 @@ static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
   // both nets, identity pi output, 2 act <= 32, and 12 * nrt co-resident blocks
   int split = c->q_layers == 3 && c->pi_layers == 3 && c->q_dims[1] == SPLIT_H && c->q_dims[2] == SPLIT_H &&
               c->pi_dims[1] == SPLIT_H && c->pi_dims[2] == SPLIT_H && c->pi_out_act == SAC_ACT_IDENTITY &&
-              2 * A <= 32 && 12 * nrt0 <= 256 && SAC_ROWS * (A + 1) <= SAC_HAND_STRIDE;
+              2 * A <= 32 && 12 * nrt0 <= 256 && (3 * split_wc(esz) + 1) * nrt0 <= 256 &&
+              SAC_ROWS * (A + 1) <= SAC_HAND_STRIDE;
   if (const char* v = getenv("SAC_SPLIT")) split = split && atoi(v) != 0;
   if (const char* v = getenv("SAC_ROLES")) split = split && atoi(v) != 0;
-  const int bp0 = split ? 2 * Bp : Bp;  // batch columns of layer 0's GT / XT
+  // batch columns of layer 0's operands under the split: X^T 2 Bp (phase A's two
+  // halves store it), dY^T 2 Bp for the critics (phase A halves), split_wc Bp for
+  // pi (phase C parts)
+  const int wc = split_wc(esz);
+  const int bp0 = split ? 2 * Bp : Bp;
+  const int bp0_pi = split ? wc * Bp : Bp;
   for (int ni = 0; ni < 5; ++ni) {
     const bool is_pi = ni == NET_PI;
     const bool trainable = ni <= NET_Q2;
@@ -378,9 +384,10 @@ static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
           ly.XT = P(o);
           ly.xt_par = is_pi ? (long)ly.Kp * bpl : 0;
         }
-        ly.GT = P(lay.take((size_t)ly.Np * bpl * esz));
-        // bias-gradient partials: one row per row tile (split layer 0: per half and row tile)
-        ly.dbp = (float*)P(lay.take((size_t)(l == 0 && split ? 2 * Bp / SAC_ROWS : nrt) * ly.N * 4));
+        const int bpg = (l == 0 && is_pi) ? bp0_pi : bpl;
+        ly.GT = P(lay.take((size_t)ly.Np * bpg * esz));
+        // bias-gradient partials: one row per row tile (split layer 0: per part and row tile)
+        ly.dbp = (float*)P(lay.take((size_t)(l == 0 && split ? bpg / SAC_ROWS : nrt) * ly.N * 4));
       }
       if (is_pi) ly.pstash = (float*)P(lay.take((size_t)Br * ly.Np * 4));
     }
@@ -400,14 +407,15 @@ static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
   h.stg = (float*)P(lay.take((size_t)nrt * h.stg_stride * 4));
   h.split = split;
   h.gs2 = SAC_ROWS * std::max(2 * A, A + 1);
-  h.gran2 = (uint64_t*)P(lay.take((size_t)GS_COUNT * nrt * 2 * h.gs2 * 8));
+  h.gran2 = (uint64_t*)P(lay.take((size_t)GS_COUNT * nrt * SPLIT_GP * h.gs2 * 8));
   int nB = 0, nD = 0, nhalf = 0;
   for (int ni = NET_PI; ni <= NET_Q2; ++ni)
     for (int l = 0; l < h.net[ni].L; ++l) {
       const int t = (h.net[ni].l[l].Np / 32) * (h.net[ni].l[l].Kp / 32);
-      const int halves = (l == 0 && split) ? 2 : 1;  // split layer 0: one block per batch half
-      (ni == NET_PI ? nD : nB) += t * halves;
-      if (halves == 2) nhalf += t;
+      // split layer 0: one block per batch part (critics 2: phase A halves; pi wc: phase C parts)
+      const int parts = (l == 0 && split) ? (ni == NET_PI ? wc : 2) : 1;
+      (ni == NET_PI ? nD : nB) += t * parts;
+      nhalf += t * (parts - 1);  // producer parts: one 1024-granule slot each
     }
   const size_t o_tB = lay.take((size_t)nB * sizeof(TileDesc));
   const size_t o_tD = lay.take((size_t)nD * sizeof(TileDesc));
@@ -548,8 +556,9 @@ static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
           for (int kt = 0; kt < ly.Kp / 32; ++kt) {
             TileDesc t;
             memset(&t, 0, sizeof(t));
-            const int bpl = (l == 0 && split) ? 2 * Bp : Bp;
-            t.GT = (const char*)ly.GT + (size_t)nt * 32 * bpl * esz2;
+            const int bpl = (l == 0 && split) ? 2 * Bp : Bp;                     // X^T row stride
+            const int bpg = (l == 0 && split) ? (ni == NET_PI ? wc : 2) * Bp : Bp;  // dY^T row stride
+            t.GT = (const char*)ly.GT + (size_t)nt * 32 * bpg * esz2;
             t.XT = (const char*)ly.XT + (size_t)kt * 32 * bpl * esz2;
             t.W = nd.P + ly.w_off;
             t.Wm = nd.M + ly.w_off;
@@ -574,19 +583,28 @@ static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
             t.n0 = nt * 32;
             t.k0 = kt * 32;
             t.opt = ni;
-            t.nrt = (l == 0 && split) ? 2 * Bp / SAC_ROWS : nrt;
+            t.nrt = (l == 0 && split) ? bpg / SAC_ROWS : nrt;
             t.ld = t.bp;
-            t.khalf = 0;
-            if (l == 0 && split) {  // consumer half (columns [0, Bp)) + producer half ([Bp, 2 Bp))
+            t.ldx = t.bp;
+            t.kpart = 0;
+            t.nparts = 1;
+            if (l == 0 && split) {
+              // consumer part 1 (dY^T columns [0, Bp)) + producer parts 2..P ([(p-1) Bp, p Bp));
+              // every part reads X^T columns [0, Bp) (X is the same in every part's columns)
+              const int parts = ni == NET_PI ? wc : 2;
+              t.ld = parts * Bp;
+              t.ldx = 2 * Bp;
               t.bp = Bp;
-              t.khalf = 1;
+              t.kpart = 1;
+              t.nparts = parts;
               t.part = (uint64_t*)(base + o_part) + (size_t)ihalf * 1024;
-              ++ihalf;
-              TileDesc pt = t;
-              pt.khalf = 2;
-              pt.GT = (const char*)t.GT + (size_t)Bp * esz2;
-              pt.XT = (const char*)t.XT + (size_t)Bp * esz2;
-              (ni == NET_PI ? halvesD : halvesB).push_back(pt);
+              ihalf += parts - 1;
+              for (int pp = 2; pp <= parts; ++pp) {
+                TileDesc pt = t;
+                pt.kpart = pp;
+                pt.GT = (const char*)t.GT + (size_t)(pp - 1) * Bp * esz2;
+                (ni == NET_PI ? halvesD : halvesB).push_back(pt);
+              }
             }
             (ni == NET_PI ? e->hostD : e->hostB).push_back(t);
           }
@@ -703,7 +721,7 @@ static void launch_kind(sac_engine* e, int kind, const sac_replay* rb, const int
       break;
     case L_C:
       if (e->h.split)
-        sac_actor_split<T><<<e->nrt * 6 + stg, SAC_THREADS, lf, s>>>(e->d, *rb);
+        sac_actor_split<T><<<e->nrt * 3 * split_wc((int)sizeof(T)) + stg, SAC_THREADS, lf, s>>>(e->d, *rb);
       else if (e->h.roles)
         sac_actor<T, true, false><<<e->nrt * 3 + stg, SAC_THREADS, lf, s>>>(e->d, *rb);
       else

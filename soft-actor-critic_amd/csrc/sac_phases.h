@@ -146,14 +146,15 @@ struct TileDesc {
   long xt_par;     // element offset of the odd-step X^T copy (pi tiles), else 0
   int K, N, Kp, Np, n0, k0, opt, nrt;
   int bp;          // batch columns this tile reduces over
-  int ld;          // row stride of the GT / XT operands in elements (Bp; 2 Bp for a hidden-split
-                   // layer 0: the two halves' partial dY side by side, X duplicated)
-  // A hidden-split layer-0 tile is two blocks, one per batch half (bp = Bp each,
-  // so no block streams more operand bytes than a plain tile): khalf 2 publishes
-  // its partial dW as 1024 data-tagged granules (part: {value, launch epoch},
-  // one 8-B sc1 store each, no drain or flag); khalf 1 polls them, adds them to
-  // its own half (own + peer: fixed order) and runs Adam.  0: a whole tile.
-  int khalf;
+  int ld, ldx;     // row strides of the GT / XT operands in elements (Bp; for a hidden-split
+                   // layer 0 the parts' partial dY side by side, X duplicated)
+  // A hidden-split layer-0 tile is one block per batch part (bp = Bp each, so
+  // no block streams more operand bytes than a plain tile): producer parts
+  // 2..nparts publish their partial dW as 1024 data-tagged granules each (part
+  // + (kpart - 2) * 1024: {value, launch epoch}, one 8-B sc1 store each, no
+  // drain or flag); part 1 polls them, adds them to its own (parts in order)
+  // and runs Adam.  kpart 0: a whole tile.
+  int kpart, nparts;
   uint64_t* part;
 };
 
@@ -882,7 +883,7 @@ __device__ __forceinline__ void dw_adam_tile(const AS_C EngineDev& E, const Tile
     v[e] = Wv[idx[e]];
     tp[e] = polyak ? tW[idx[e]] : 0.f;
   }
-  const bool do_bias = td.k0 == 0 && td.khalf != 2;
+  const bool do_bias = td.k0 == 0 && td.kpart <= 1;
   float pb = 0.f, mb = 0.f, vb = 0.f, tbv = 0.f;
   if (do_bias && tid < 32 && td.n0 + tid < td.N) {
     pb = GPC(float, td.b)[td.n0 + tid];
@@ -940,7 +941,7 @@ __device__ __forceinline__ void dw_adam_tile(const AS_C EngineDev& E, const Tile
           const int i = tid + pi * UT;
           const int row = i / per_row, pc = i % per_row;
           const AS_G T* src = row < 32 ? GPC(T, td.GT) + (size_t)row * td.ld
-                                       : GPC(T, td.XT) + par * td.xt_par + (size_t)(row - 32) * td.ld;
+                                       : GPC(T, td.XT) + par * td.xt_par + (size_t)(row - 32) * td.ldx;
           if (i < 64 * per_row) rg[sl][pi] = *(const AS_G u32x4*)(src + b0 + pc * EPR);
         }
       }
@@ -1014,21 +1015,31 @@ __device__ __forceinline__ void dw_adam_tile(const AS_C EngineDev& E, const Tile
     if (do_bias && t < 512) red[(t >> 4) * 17 + (t & 15)] = bsum[j];
   }
   __syncthreads();
-  if (td.khalf) {  // hidden-split layer 0: the two batch halves of this tile meet here
+  if (td.kpart) {  // hidden-split layer 0: the batch parts of this tile meet here
     const uint32_t ep = *GPC(uint32_t, E.sync) + 1u;  // per launch (B and D have their own granules)
-    if (td.khalf == 2) {
+    if (td.kpart >= 2) {
+      AS_G uint64_t* mine = GP(uint64_t, td.part) + (size_t)(td.kpart - 2) * 1024;
       for (int el = tid; el < 1024; el += UT) {
         const uint64_t x = (uint64_t)__float_as_uint(accs[(el >> 5) * 33 + (el & 31)]) | ((uint64_t)ep << 32);
-        __hip_atomic_store(td.part + el, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store((uint64_t*)(mine + el), x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
-      return;  // uniform: the peer block runs Adam on the sum
+      return;  // uniform: part 1 runs Adam on the sum
     }
     for (int el = tid; el < 1024; el += UT) {
-      uint64_t x = 0;
+      float v[3] = {0.f, 0.f, 0.f};
+      const int np = td.nparts - 1;  // producer parts (1..3)
       for (int it = 0;; ++it) {
-        x = __hip_atomic_load(td.part + el, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if ((uint32_t)(x >> 32) == ep) break;
-        if (it > E.spin_limit) {  // the producer half never ran: flag the error, do not hang
+        bool all = true;
+#pragma unroll
+        for (int q = 0; q < 3; ++q)
+          if (q < np) {
+            const uint64_t x = __hip_atomic_load(td.part + (size_t)q * 1024 + el, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT);
+            all = all && (uint32_t)(x >> 32) == ep;
+            v[q] = __uint_as_float((uint32_t)x);
+          }
+        if (all) break;
+        if (it > E.spin_limit) {  // a producer part never ran: flag the error, do not hang
           __hip_atomic_store((uint32_t*)GP(uint32_t, E.sync) + 1 /* SYNC_TIMEOUT */, 1u, __ATOMIC_RELAXED,
                              __HIP_MEMORY_SCOPE_AGENT);
           break;
@@ -1036,7 +1047,11 @@ __device__ __forceinline__ void dw_adam_tile(const AS_C EngineDev& E, const Tile
         __builtin_amdgcn_s_sleep(1);
       }
       const int o = (el >> 5) * 33 + (el & 31);
-      accs[o] = accs[o] + __uint_as_float((uint32_t)x);
+      float sum = accs[o];
+#pragma unroll
+      for (int q = 0; q < 3; ++q)
+        if (q < np) sum += v[q];
+      accs[o] = sum;
     }
     __syncthreads();
   }

@@ -30,8 +30,16 @@
 
 #define SPLIT_H 256
 #define SPLIT_HH 128
+// Phase C splits layer 1 into split_wc parts: four in fp32 (3 roles x 4 parts x
+// nrt = 192 workgroups at C2: its critical path is three layer-1 GEMMs -- critic
+// forward, critic dX, pi dX -- each then a quarter of the MFMA-bound fp32 work
+// per workgroup), two in bf16 (its layer-1 steps are short; the extra batch
+// parts of phase D's layer-0 tiles cost more than the quarters save).
+// Phase A keeps halves (6 roles x 2 x nrt = 192).
+__host__ __device__ constexpr int split_wc(int elem_bytes) { return elem_bytes == 4 ? 4 : 2; }
+#define SPLIT_GP 4  // granule part slots per (kind, row tile): max over precisions of split_wc
 
-// Split granule kinds: [GS_COUNT][nrt][2 halves][E.gs2] 8-B granules
+// Split granule kinds: [GS_COUNT][nrt][SPLIT_GP parts][E.gs2] 8-B granules
 enum SplitGran {
   GS_PI = 0,   // pi(s') layer-2 partial [R][2A]              -> target critics
   GS_PS = 1,   // pi(s) layer-2 partial [R][2A]               -> the peer pi(s) half
@@ -45,7 +53,7 @@ enum SplitGran {
   GS_COUNT = 9
 };
 __device__ __forceinline__ AS_G uint64_t* gs_at(const AS_C EngineDev& E, int kind, int rbi, int h) {
-  return GP(uint64_t, E.gran2) + ((size_t)(kind * E.nrt + rbi) * 2 + h) * E.gs2;
+  return GP(uint64_t, E.gran2) + ((size_t)(kind * E.nrt + rbi) * SPLIT_GP + h) * E.gs2;
 }
 
 // ---------------------------------------------------------------------------- held GEMM
@@ -67,12 +75,16 @@ __device__ __forceinline__ void ht_issue(HTiles<T, NTW, HC>& ht, const GemmW& w)
   static_for<NTW>([&](auto jc) {
     constexpr int j = decltype(jc)::value;
     int t = wave + j * SAC_NW;
-    t = t < w.NT ? t : w.NT - 1;  // clamped: loads valid memory, the tile is skipped
+    const bool has = t < w.NT;  // wave-uniform: a wave without this tile loads nothing
+    t = has ? t : w.NT - 1;
     const uint32_t o = (uint32_t)(((size_t)t * 16 * w.tcols + lane * MM<T>::KL) * sizeof(T));
     static_for<HC>([&](auto uc) {
       constexpr int u = decltype(uc)::value;
       const uint32_t cu = u < nch ? u : nch - 1;
-      ht.f[j][u] = coh_frag<T, COH>(rs, o + cu * FSB);
+      if (has)
+        ht.f[j][u] = coh_frag<T, COH>(rs, o + cu * FSB);
+      else
+        ht.f[j][u] = typename MM<T>::Frag{};
     });
     if (w.bias) {
       const int n = t * 16 + (lane & 15);
@@ -112,7 +124,8 @@ __device__ __forceinline__ void gemm_hs(const lf* __restrict__ A, int lda, const
       if (u < nch)
         static_for<NTW>([&](auto jc) {
           constexpr int j = decltype(jc)::value;
-          MM<T>::mma(acc[j][u & 1], a[u], ht->f[j][u]);
+          if (wave + j * SAC_NW < w.NT)  // wave-uniform: no MFMA issue for a wave without this tile
+            MM<T>::mma(acc[j][u & 1], a[u], ht->f[j][u]);
         });
     });
     ch0 = HC;
@@ -146,7 +159,7 @@ __device__ __forceinline__ void gemm_hs(const lf* __restrict__ A, int lda, const
         if (u < rem)
           static_for<NTW>([&](auto jc) {
             constexpr int j = decltype(jc)::value;
-            MM<T>::mma(acc[j][u & 1], a[u], f[j][u]);
+            if (wave + j * SAC_NW < w.NT) MM<T>::mma(acc[j][u & 1], a[u], f[j][u]);
           });
       });
     }
@@ -631,16 +644,16 @@ __device__ __forceinline__ void actor_split_body(const EngineDev* __restrict__ E
   const AS_C EngineDev& E = *(const AS_C EngineDev*)Ep;
   extern __shared__ float lds_raw[];
   lf* lds = (lf*)lds_raw;
-  constexpr int R = SAC_ROWS, HH = SPLIT_HH;
+  constexpr int R = SAC_ROWS, W = split_wc(sizeof(T)), HH = SPLIT_H / W;  // HH: layer-1 outputs of a part
   constexpr int KC = MM<T>::KC;
   constexpr int HC0 = 64 / KC;
   constexpr int NCH_H = SPLIT_H / KC;
   constexpr int NCH_HH = HH / KC;
   constexpr int NCH_32 = 32 / KC;
   const int tid = threadIdx.x;
-  const int n2 = 2 * E.nrt;
+  const int n2 = W * E.nrt;
   const int grp = bid / n2, idx = bid % n2;
-  const int h = idx & 1, rbi = idx >> 1;
+  const int h = idx % W, rbi = idx / W;  // h: this workgroup's part of layer 1
   // producers first: groups 0 / 1 the critics, group 2 pi
   const bool is_pi = grp == 2;
   const int qi = grp;  // critics
@@ -793,21 +806,36 @@ __device__ __forceinline__ void actor_split_body(const EngineDev* __restrict__ E
   __syncthreads();
   STAMP(34);
   // combine the critics' unit-seed partials with the min-Q weights (L_pi = mean(alpha logpi - min Q))
-  const AS_G uint64_t* c10 = gs_at(E, GS_C1, rbi, 0);
-  const AS_G uint64_t* c11 = gs_at(E, GS_C1, rbi, 1);
-  const AS_G uint64_t* c20 = gs_at(E, GS_C2, rbi, 0);
-  const AS_G uint64_t* c21 = gs_at(E, GS_C2, rbi, 1);
+  // the critics' parts, summed in part order by every consumer
+  const AS_G uint64_t* c1p[W];
+  const AS_G uint64_t* c2p[W];
+#pragma unroll
+  for (int p = 0; p < W; ++p) {
+    c1p[p] = gs_at(E, GS_C1, rbi, p);
+    c2p[p] = gs_at(E, GS_C2, rbi, p);
+  }
   if (tid < 64) {
     float term = 0.f;
     if (tid < R) {
       const bool v = tid < nvalid;
       const AS_C NetDev& q1n = E.net[NET_Q1];
       const AS_C NetDev& q2n = E.net[NET_Q2];
-      const AS_G uint64_t* gg[4] = {c10 + R * A + tid, c11 + R * A + tid, c20 + R * A + tid, c21 + R * A + tid};
-      float gv[4];
-      gran_getn<4>(E, gg, ep, gv);
-      const float q1p = gv[0] + gv[1] + bq1;
-      const float q2p = gv[2] + gv[3] + bq2;
+      const AS_G uint64_t* gg[2 * W];
+#pragma unroll
+      for (int p = 0; p < W; ++p) {
+        gg[p] = c1p[p] + R * A + tid;
+        gg[W + p] = c2p[p] + R * A + tid;
+      }
+      float gv[2 * W];
+      gran_getn<2 * W>(E, gg, ep, gv);
+      float q1p = gv[0], q2p = gv[W];
+#pragma unroll
+      for (int p = 1; p < W; ++p) {
+        q1p += gv[p];
+        q2p += gv[W + p];
+      }
+      q1p += bq1;
+      q2p += bq2;
       const float q1 = q1n.out_act == ACT_ID ? q1p : act_fwd(q1n.out_act, q1p);
       const float q2 = q2n.out_act == ACT_ID ? q2p : act_fwd(q2n.out_act, q2p);
       const float m = fmin_nan(q1, q2);
@@ -826,11 +854,20 @@ __device__ __forceinline__ void actor_split_body(const EngineDev* __restrict__ E
   __syncthreads();
   for (int i = tid; i < R * A; i += SAC_THREADS) {
     const int r = i / A;
-    const AS_G uint64_t* gg[4] = {c10 + i, c11 + i, c20 + i, c21 + i};
-    float gv[4];
-    gran_getn<4>(E, gg, ep, gv);  // all four are in by now (the q granules above came after them)
-    const float da1 = gv[0] + gv[1];
-    const float da2 = gv[2] + gv[3];
+    const AS_G uint64_t* gg[2 * W];
+#pragma unroll
+    for (int p = 0; p < W; ++p) {
+      gg[p] = c1p[p] + i;
+      gg[W + p] = c2p[p] + i;
+    }
+    float gv[2 * W];
+    gran_getn<2 * W>(E, gg, ep, gv);  // all in by now (the q granules above came after them)
+    float da1 = gv[0], da2 = gv[W];
+#pragma unroll
+    for (int p = 1; p < W; ++p) {
+      da1 += gv[p];
+      da2 += gv[W + p];
+    }
     gaB[i] = g1B[r] * da1 + g2B[r] * da2;
   }
   __syncthreads();
@@ -898,7 +935,7 @@ __device__ __forceinline__ void actor_split_body(const EngineDev* __restrict__ E
   });
   if (act != ACT_RELU && act != ACT_ID) act_pass_bwd<R>(Xb, ld, P0, ldp0, L1.Kp >> 4, L1.K, act);
   __syncthreads();
-  store_T<T, R>(Xb, ld, L0.Np, L0.N, L0.GT, 2 * Bp, h * Bp + r0, nvalid, L0.dbp);
+  store_T<T, R>(Xb, ld, L0.Np, L0.N, L0.GT, W * Bp, h * Bp + r0, nvalid, L0.dbp);
   STAMP(35);
 }
 
@@ -908,7 +945,7 @@ __global__ void __launch_bounds__(SAC_THREADS) sac_actor_split(const EngineDev* 
   const AS_C EngineDev& E = *(const AS_C EngineDev*)Ep;
   extern __shared__ float lds_raw[];
   const int bid = (int)blockIdx.x;
-  const int nrole = 6 * E.nrt;  // 3 roles x 2 halves x nrt
+  const int nrole = 3 * split_wc(sizeof(T)) * E.nrt;  // 3 roles x parts x nrt
   if (bid >= nrole)
     stage_next_batch(E, rb, bid - nrole, (lf*)lds_raw);
   else

@@ -39,7 +39,8 @@ n_d = _tiles([O_] + H_ + [2 * A_])
 OFF = {"A": n_d + 1, "C": n_b} if eng.fused else {"A": 0, "C": 0}
 lib.sac_engine_uses_split.argtypes = [ctypes.c_void_p]
 SPLIT = bool(lib.sac_engine_uses_split(eng.handle))
-GROUP = 2 * nrt if SPLIT else nrt  # blocks per role group (hidden split: two halves per row tile)
+GROUP = 2 * nrt if SPLIT else nrt  # blocks per role group (hidden split: two halves per row tile in A)
+GROUP_C = (4 if prec == "fp32" else 2) * nrt if SPLIT else nrt  # phase C: split_wc parts per row tile
 buf = torch.zeros(nblk * 64, dtype=torch.int64, device=dev)
 E.check(lib.sac_engine_debug_stamps(eng.handle, E.ptr(buf), eng._stream()))
 eng.train(rb, 20)
@@ -96,7 +97,8 @@ for ph, ids in PH.items():
     groups = {"all": np.ones(len(blk), bool)}
     if ph in ROLES and eng.roles:
         rb_ = blk - OFF[ph]
-        groups = {nm: (rb_ >= 0) & ((rb_ // GROUP) == k) for k, nm in enumerate(ROLES[ph])}
+        G = GROUP_C if ph == "C" else GROUP
+        groups = {nm: (rb_ >= 0) & ((rb_ // G) == k) for k, nm in enumerate(ROLES[ph])}
         if OFF[ph]:
             groups["upd"] = rb_ < 0
     print(f"=== phase {ph}")
@@ -157,7 +159,8 @@ for ph, ids in PH.items():
                 if ph in ROLES and eng.roles:
                     rb2 = blk_r - OFF[ph]
                     k = list(groups).index(g) if g in ROLES.get(ph, []) else -1
-                    gm = (rb2 >= 0) & ((rb2 // GROUP) == k) if k >= 0 else (rb2 < 0)
+                    G = GROUP_C if ph == "C" else GROUP
+                    gm = (rb2 >= 0) & ((rb2 // G) == k) if k >= 0 else (rb2 < 0)
                 v = sel_r[gm, i]
                 v = v[v > 0]
                 if v.size:
