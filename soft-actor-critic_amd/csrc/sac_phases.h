@@ -878,10 +878,14 @@ __device__ __forceinline__ void dw_adam_tile(const AS_C EngineDev& E, const Tile
     const int n = td.n0 + en, k = td.k0 + ek;
     ok[e] = n < td.N && k < td.K;
     idx[e] = ok[e] ? (size_t)n * td.K + k : 0;
-    p[e] = W[idx[e]];
-    m[e] = Wm[idx[e]];
-    v[e] = Wv[idx[e]];
-    tp[e] = polyak ? tW[idx[e]] : 0.f;
+    if (td.kpart < 2) {  // uniform: a producer part only computes its partial dW
+      p[e] = W[idx[e]];
+      m[e] = Wm[idx[e]];
+      v[e] = Wv[idx[e]];
+      tp[e] = polyak ? tW[idx[e]] : 0.f;
+    } else {
+      p[e] = m[e] = v[e] = tp[e] = 0.f;
+    }
   }
   const bool do_bias = td.k0 == 0 && td.kpart <= 1;
   float pb = 0.f, mb = 0.f, vb = 0.f, tbv = 0.f;
