@@ -408,12 +408,19 @@ static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
   h.split = split;
   h.gs2 = SAC_ROWS * std::max(2 * A, A + 1);
   h.gran2 = (uint64_t*)P(lay.take((size_t)GS_COUNT * nrt * SPLIT_GP * h.gs2 * 8));
+  // Batch parts of an update tile (TileDesc.kpart): the hidden split's layer 0
+  // reduces over its parts' columns (critics 2: phase A halves; pi wc: phase C
+  // parts); a large batch is split into parts of at most 1024 columns (C3:
+  // 4 x 1024), so no block streams more than 1024 batch columns of operands.
+  auto tile_parts = [&](int ni, int l) {
+    if (l == 0 && split) return ni == NET_PI ? wc : 2;
+    return Bp > 1024 ? std::min(4, (Bp + 1023) / 1024) : 1;
+  };
   int nB = 0, nD = 0, nhalf = 0;
   for (int ni = NET_PI; ni <= NET_Q2; ++ni)
     for (int l = 0; l < h.net[ni].L; ++l) {
       const int t = (h.net[ni].l[l].Np / 32) * (h.net[ni].l[l].Kp / 32);
-      // split layer 0: one block per batch part (critics 2: phase A halves; pi wc: phase C parts)
-      const int parts = (l == 0 && split) ? (ni == NET_PI ? wc : 2) : 1;
+      const int parts = tile_parts(ni, l);
       (ni == NET_PI ? nD : nB) += t * parts;
       nhalf += t * (parts - 1);  // producer parts: one 1024-granule slot each
     }
@@ -588,21 +595,26 @@ static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
             t.ldx = t.bp;
             t.kpart = 0;
             t.nparts = 1;
-            if (l == 0 && split) {
-              // consumer part 1 (dY^T columns [0, Bp)) + producer parts 2..P ([(p-1) Bp, p Bp));
-              // every part reads X^T columns [0, Bp) (X is the same in every part's columns)
-              const int parts = ni == NET_PI ? wc : 2;
-              t.ld = parts * Bp;
-              t.ldx = 2 * Bp;
-              t.bp = Bp;
+            const int parts = tile_parts(ni, l);
+            if (parts > 1) {
+              // consumer part 1 (batch columns [0, bpp)) + producer parts 2..P ([(p-1) bpp, p bpp))
+              const bool xsame = l == 0 && split;  // split layer 0: X^T columns [0, Bp) serve every part
+              const int total = xsame ? parts * Bp : Bp;
+              const int bpp = xsame ? Bp : rup((Bp + parts - 1) / parts, 32);
+              t.ld = xsame ? parts * Bp : Bp;
+              t.ldx = xsame ? 2 * Bp : Bp;
+              t.bp = bpp;
               t.kpart = 1;
               t.nparts = parts;
               t.part = (uint64_t*)(base + o_part) + (size_t)ihalf * 1024;
               ihalf += parts - 1;
               for (int pp = 2; pp <= parts; ++pp) {
                 TileDesc pt = t;
+                const int off = (pp - 1) * bpp;
                 pt.kpart = pp;
-                pt.GT = (const char*)t.GT + (size_t)(pp - 1) * Bp * esz2;
+                pt.bp = std::min(bpp, total - off);
+                pt.GT = (const char*)t.GT + (size_t)off * esz2;
+                if (!xsame) pt.XT = (const char*)t.XT + (size_t)off * esz2;
                 (ni == NET_PI ? halvesD : halvesB).push_back(pt);
               }
             }
@@ -622,7 +634,7 @@ static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
       // on C2: four launches stay the default; SAC_FUSE=1|2 opts in.
       int fuse = 0;
       if (const char* v = getenv("SAC_FUSE")) fuse = std::max(0, std::min(2, atoi(v)));
-      if (!e->h.roles || e->h.split || nD + 1 + 6 * nrt > 256) fuse = 0;
+      if (!e->h.roles || e->h.split || nhalf || nD + 1 + 6 * nrt > 256) fuse = 0;
       if (fuse == 2 && nB + 3 * nrt > 256) fuse = 1;
       e->fused = fuse;
     }
