@@ -343,26 +343,79 @@ class SAC:
         return {"q1_loss": l[0], "q2_loss": l[1], "policy_loss": l[2], "alpha_loss": l[3],
                 "alpha": float(self.alpha.item())}
 
-    # Reference sub-steps.  The engine fuses them; calling one alone is not a
-    # supported mode of the fused step (see DESIGN.md "API surface").
-    def compute_target_q_values(self, *a, **k):
-        self._fused_only("compute_target_q_values")
+    # Reference sub-steps (agent.py:195-300), unfused.  training_step() runs
+    # them fused on the HIP engine; called one by one they keep the reference's
+    # semantics on the engine's own state: the modules' parameters, the Adam
+    # moments and log alpha ARE the engine's buffers, so these run as PyTorch
+    # eager ops on the GPU (the reference's own code, not the hot path), with
+    # the optimizer step counts taken from and returned to the engine and the
+    # packed MFMA copies re-derived after each update (sync_params).
+    # tests/test_gpu_substeps.py: the five composed == one fused step.
+    def _opt_step(self, opt, idx: int) -> None:
+        eng = self._engine()
+        t = float(eng.opt_steps[idx].item())
+        for st in opt.state.values():
+            st["step"] = torch.tensor(t)
+        opt.step()
+        eng.opt_steps[idx] = t + 1.0
 
-    def _fused_only(self, name):
-        raise NotImplementedError(
-            f"SAC.{name} is fused into SAC.training_step on the MI355X engine; call training_step()")
+    def compute_target_q_values(self, rewards: Any, dones: Any, next_states: Any) -> Any:
+        """y = r + gamma (1 - d)(min Q_t(s', a') - alpha log pi(a'|s')) (agent.py:195-211)."""
+        self._engine()
+        with torch.no_grad():
+            alpha = self.alpha.detach()
+            next_actions, next_log_pi = self.policy_net.sample_action(next_states)
+            q1 = self.q_net1_target(next_states, next_actions)
+            q2 = self.q_net2_target(next_states, next_actions)
+            return rewards + self.config["sac"]["gamma"] * (1 - dones) * (torch.min(q1, q2) - alpha * next_log_pi)
 
-    def update_q_networks(self, *a, **k):
-        self._fused_only("update_q_networks")
+    def update_q_networks(self, states: Any, actions: Any, target_q_values: Any) -> None:
+        """MSE critic losses, one Adam step per critic (agent.py:213-236)."""
+        eng = self._engine()
+        for net, opt, idx in ((self.q_net1, self.q1_optimizer, 1), (self.q_net2, self.q2_optimizer, 2)):
+            loss = torch.nn.functional.mse_loss(net(states, actions), target_q_values)
+            opt.zero_grad()
+            loss.backward()
+            self._opt_step(opt, idx)
+        eng.sync_params()
 
-    def update_policy_network(self, *a, **k):
-        self._fused_only("update_policy_network")
+    def update_policy_network(self, states: Any):
+        """L_pi = mean(alpha log pi - min Q) through the current critics; returns log pi (agent.py:238-260)."""
+        eng = self._engine()
+        actions, log_pi = self.policy_net.sample_action(states)
+        min_q = torch.min(self.q_net1(states, actions), self.q_net2(states, actions))
+        policy_loss = (self.alpha.detach() * log_pi - min_q).mean()
+        self.policy_optimizer.zero_grad()
+        policy_loss.backward()
+        self._opt_step(self.policy_optimizer, 0)
+        for net in (self.q_net1, self.q_net2):  # the reference leaves critic grads behind; drop them
+            net.zero_grad(set_to_none=True)
+        eng.sync_params()
+        return log_pi
 
-    def update_entropy_temperature(self, *a, **k):
-        self._fused_only("update_entropy_temperature")
+    def update_entropy_temperature(self, log_pi: Any) -> Dict[str, float]:
+        """Adam step on float64 log alpha (agent.py:263-280); {} when alpha is fixed."""
+        eng = self._engine()
+        if not self._auto:
+            return {}
+        term = (log_pi + self.target_entropy).detach()
+        alpha_loss = -(self.log_alpha.to(term.dtype) * term).mean()
+        if eng.alpha_updates:  # off after a reference-style load_agent (agent.py:550-554)
+            self.log_alpha.grad = (-term.mean()).to(self.log_alpha.dtype).reshape(self.log_alpha.shape)
+            self._opt_step(self.alpha_optimizer, 3)
+            self.log_alpha.grad = None
+            eng.alpha_state[1] = eng.alpha_state[0].exp()
+        return {"alpha_loss": alpha_loss.item(), "alpha": self.alpha.item()}
 
-    def soft_update_target_networks(self):
-        self._fused_only("soft_update_target_networks")
+    def soft_update_target_networks(self) -> None:
+        """Polyak t <- tau p + (1 - tau) t (agent.py:282-300)."""
+        eng = self._engine()
+        tau = self.config["sac"]["tau"]
+        with torch.no_grad():
+            for tgt, src in ((self.q_net1_target, self.q_net1), (self.q_net2_target, self.q_net2)):
+                for tp, sp in zip(tgt.parameters(), src.parameters()):
+                    tp.data.copy_(tau * sp.data + (1.0 - tau) * tp.data)
+        eng.sync_params()
 
     # ------------------------------------------------------------------ loops
     def run_training_loop(self, num_episodes: int, logger=None, tqdm_disable: bool = False,

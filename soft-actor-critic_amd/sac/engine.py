@@ -160,9 +160,12 @@ class SacEngine:
         except Exception:
             pass
 
+    alpha_updates = True
+
     def set_alpha_update(self, enabled: bool) -> None:
         """Temperature (log alpha) Adam updates on/off (see sac_engine.h)."""
         E.check(self.lib.sac_engine_set_alpha_update(self.handle, int(bool(enabled)), self._stream()))
+        self.alpha_updates = bool(enabled)
 
     def sync_params(self) -> None:
         """Re-pack the MFMA compute copies after host-side parameter changes."""

@@ -55,15 +55,24 @@ def test_hot_path_fails_loudly_without_gpu():
         agent.store_transition(np.zeros(meta["obs"]), np.zeros(meta["act"]), 0.0, np.zeros(meta["obs"]), False)
 
 
-def test_fused_substeps_are_not_separately_callable():
+def test_substeps_need_the_engine():
+    """The reference sub-steps run on the engine's device state: without a GPU
+    they fail loudly like the fused step (no CPU fallback)."""
+    import torch
+
+    from sac import _engine as E
     from sac.agent import SAC
 
     cfg, meta = _cfg()
     agent = SAC(FakeEnv(meta["obs"], meta["act"]), cfg)
-    for name in ("compute_target_q_values", "update_q_networks", "update_policy_network",
-                 "update_entropy_temperature", "soft_update_target_networks"):
-        with pytest.raises(NotImplementedError):
-            getattr(agent, name)()
+    s = torch.zeros(4, meta["obs"])
+    a = torch.zeros(4, meta["act"])
+    r = torch.zeros(4)
+    calls = {"compute_target_q_values": (r, r, s), "update_q_networks": (s, a, r), "update_policy_network": (s,),
+             "update_entropy_temperature": (r,), "soft_update_target_networks": ()}
+    for name, args in calls.items():
+        with pytest.raises(E.EngineUnavailable):
+            getattr(agent, name)(*args)
 
 
 def test_replay_buffer_cpu_contract():
