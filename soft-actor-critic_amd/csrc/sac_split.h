@@ -285,8 +285,14 @@ __device__ __forceinline__ void target_critic_split_body(const EngineDev* __rest
 
   const uint64_t step = *GPC(uint64_t, E.rng_step);
   const int par = (int)(step & 1);
-  if (role == 0 && rbi == 0 && h == 0 && tid < 4 && (tid < 3 || (E.auto_entropy && E.alpha_update))) {
-    // optimizer step counters and this step's Adam bias corrections (torch adam.py)
+#ifndef SAC_ADAM_LAST
+#define SAC_ADAM_LAST 1
+#endif
+  const bool adam_blk = SAC_ADAM_LAST ? (role == 5 && rbi == E.nrt - 1 && h == 1) : (role == 0 && rbi == 0 && h == 0);
+  if (adam_blk && tid < 4 && (tid < 3 || (E.auto_entropy && E.alpha_update))) {
+    // optimizer step counters and this step's Adam bias corrections (torch adam.py), read
+    // by phases B and D only: done by the last pi(s) workgroup, off the y chain (a load
+    // round trip + double pow() here delayed pi(s') of row tile 0, hence the whole launch)
     const double t = GP(double, E.opt_steps)[tid] + 1.0;
     GP(double, E.opt_steps)[tid] = t;
     if (tid < 3) {
