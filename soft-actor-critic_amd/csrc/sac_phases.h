@@ -950,10 +950,13 @@ __device__ __forceinline__ void dw_adam_tile(const AS_C EngineDev& E, const Tile
         }
       }
     }
+    // slot by slot: its pieces -> LDS (waits only for this slot's loads: they
+    // complete in issue order), barrier, its MFMAs -- while the later slots'
+    // loads are still landing
 #pragma unroll
     for (int sl = 0; sl < MAXS; ++sl) {
       const int b0 = r0 + sl * SAC_UPD_BCH;
-      if (sl < nslot && b0 < Bp) {
+      if (sl < nslot && b0 < Bp) {  // uniform
         const int bch = Bp - b0 < SAC_UPD_BCH ? Bp - b0 : SAC_UPD_BCH;
         const int per_row = bch / EPR;
 #pragma unroll
@@ -962,32 +965,25 @@ __device__ __forceinline__ void dw_adam_tile(const AS_C EngineDev& E, const Tile
           const int row = i / per_row, pc = i % per_row;
           if (i < 64 * per_row) *(AS_L u32x4*)(stage + sl * slot_el + row * lds_row + pc * EPR) = rg[sl][pi];
         }
-      }
-    }
-    __syncthreads();
-    if (r0 == 0) STAMP(polyak ? 51 : 55);
-    {
-      for (int sl = 0; sl < nslot; ++sl) {
-        const int b0 = r0 + sl * SAC_UPD_BCH;
-        if (b0 >= Bp) break;
-        const int bch = Bp - b0 < SAC_UPD_BCH ? Bp - b0 : SAC_UPD_BCH;
+        __syncthreads();
+        if (r0 == 0 && sl == 0) STAMP(polyak ? 51 : 55);
 #pragma unroll
         for (int j = 0; j < PPW; ++j) {
-        const int pr = wave + j * NWV, kq = pr >> 2;
-        const int ns = ((pr & 3) >> 1) * 16, ks = (pr & 1) * 16;
-        const AS_L T* arow = stage + sl * slot_el + (ns + c) * lds_row + g * KL;
-        const AS_L T* brow = stage + sl * slot_el + (32 + ks + c) * lds_row + g * KL;
-        for (int ch = kq; ch < bch / KC; ch += KQ) {
-          typename MM<T>::Frag a, b;
-          if constexpr (sizeof(T) == 2) {
-            a = *(const AS_L bf16x8*)(arow + ch * KC);
-            b = *(const AS_L bf16x8*)(brow + ch * KC);
-          } else {
-            a = *(const AS_L f32x4*)(arow + ch * KC);
-            b = *(const AS_L f32x4*)(brow + ch * KC);
+          const int pr = wave + j * NWV, kq = pr >> 2;
+          const int ns = ((pr & 3) >> 1) * 16, ks = (pr & 1) * 16;
+          const AS_L T* arow = stage + sl * slot_el + (ns + c) * lds_row + g * KL;
+          const AS_L T* brow = stage + sl * slot_el + (32 + ks + c) * lds_row + g * KL;
+          for (int ch = kq; ch < bch / KC; ch += KQ) {
+            typename MM<T>::Frag a, b;
+            if constexpr (sizeof(T) == 2) {
+              a = *(const AS_L bf16x8*)(arow + ch * KC);
+              b = *(const AS_L bf16x8*)(brow + ch * KC);
+            } else {
+              a = *(const AS_L f32x4*)(arow + ch * KC);
+              b = *(const AS_L f32x4*)(brow + ch * KC);
+            }
+            MM<T>::mma(acc[j], a, b);
           }
-          MM<T>::mma(acc[j], a, b);
-        }
         }
       }
     }
