@@ -339,7 +339,7 @@ static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
   // both nets, identity pi output, 2 act <= 32, and 12 * nrt co-resident blocks
   int split = c->q_layers == 3 && c->pi_layers == 3 && c->q_dims[1] == SPLIT_H && c->q_dims[2] == SPLIT_H &&
               c->pi_dims[1] == SPLIT_H && c->pi_dims[2] == SPLIT_H && c->pi_out_act == SAC_ACT_IDENTITY &&
-              2 * A <= 32 && 12 * nrt0 <= 256 && (3 * split_wc(esz) + 1) * nrt0 <= 256 &&
+              2 * A <= 32 && (10 + split_wpi(esz)) * nrt0 <= 256 && (3 * split_wc(esz) + 1) * nrt0 <= 256 &&
               SAC_ROWS * (A + 1) <= SAC_HAND_STRIDE;
   if (const char* v = getenv("SAC_SPLIT")) split = split && atoi(v) != 0;
   if (const char* v = getenv("SAC_ROLES")) split = split && atoi(v) != 0;
@@ -724,7 +724,8 @@ static void launch_kind(sac_engine* e, int kind, const sac_replay* rb, const int
   switch (kind) {
     case L_A:
       if (e->h.split)
-        sac_target_critic_split<T><<<e->nrt * 12, SAC_THREADS, lf, s>>>(e->d, *rb, idx, eps);
+        sac_target_critic_split<T><<<e->nrt * (10 + split_wpi((int)sizeof(T))), SAC_THREADS, lf, s>>>(e->d, *rb, idx,
+                                                                                                  eps);
       else if (e->h.roles)
         sac_target_critic<T, true, false><<<e->nrt * 6, SAC_THREADS, lf, s>>>(e->d, *rb, idx, eps);
       else
@@ -983,15 +984,16 @@ int sac_replay_push(const sac_replay* rb, const float* rows, int64_t n, int64_t 
   return SAC_OK;
 }
 
-// rows per wave of the records gather: 16 below 256K rows (4x the waves in flight: 65,536 rows
-// 1.51 -> 2.41 TB/s), 64 above; SAC_GATHER_RPW overrides (16 / 32 / 64)
+// rows per wave of the records gather: 16 (4x the waves in flight of 64 rows per wave:
+// 65,536 rows 1.51 -> 2.42 TB/s, 1,048,576 rows 3.00 -> 3.17 TB/s); SAC_GATHER_RPW overrides
 static int gather_rpw(int batch) {
   static const int env = [] {
     const char* v = getenv("SAC_GATHER_RPW");
     const int x = v ? atoi(v) : 0;
     return (x == 16 || x == 32 || x == 64) ? x : 0;
   }();
-  return env ? env : (batch >= (1 << 18) ? 64 : 16);
+  (void)batch;
+  return env ? env : 16;
 }
 
 int sac_replay_gather(const sac_replay* rb, const int32_t* logical_idx, int32_t batch, float* s, float* a, float* r,

@@ -37,6 +37,10 @@
 // parts of phase D's layer-0 tiles cost more than the quarters save).
 // Phase A keeps halves (6 roles x 2 x nrt = 192).
 __host__ __device__ constexpr int split_wc(int elem_bytes) { return elem_bytes == 4 ? 4 : 2; }
+// Phase A's pi(s') role -- the head of the y chain -- gets the same parts as
+// phase C (fp32: 4; the other five roles keep halves: (4 + 10) x nrt = 224
+// workgroups at C2).
+__host__ __device__ constexpr int split_wpi(int elem_bytes) { return split_wc(elem_bytes); }
 #define SPLIT_GP 4  // granule part slots per (kind, row tile): max over precisions of split_wc
 
 // Split granule kinds: [GS_COUNT][nrt][SPLIT_GP parts][E.gs2] 8-B granules
@@ -235,9 +239,14 @@ __device__ __forceinline__ void target_critic_split_body(const EngineDev* __rest
   constexpr int NCH_H = SPLIT_H / KC;  // layer 1 reduction
   constexpr int NCH_HH = HH / KC;      // layer 1 dX reduction of a half
   const int tid = threadIdx.x;
-  const int n2 = 2 * E.nrt;
-  const int grp = (int)blockIdx.x / n2, idx = (int)blockIdx.x % n2;
-  const int h = idx & 1, rbi = idx >> 1;
+  // blocks: pi(s') as WP parts x nrt, then roles 1..5 as 2 halves x nrt each
+  constexpr int WP = split_wpi(sizeof(T));
+  const int n2 = 2 * E.nrt, n0 = WP * E.nrt;
+  const int bidA = (int)blockIdx.x;
+  const int grp = bidA < n0 ? 0 : 1 + (bidA - n0) / n2;
+  const int idx = bidA < n0 ? bidA : (bidA - n0) % n2;
+  const int h = bidA < n0 ? idx % WP : idx & 1, rbi = bidA < n0 ? idx / WP : idx >> 1;
+  const int HHr = grp == 0 ? SPLIT_H / WP : SPLIT_HH;  // layer-1 outputs of this workgroup's part
   // roles in producer-first order: 0 pi(s'), 1/2 target critics, 3/4 critics, 5 pi(s)
   const int role = grp;
   const bool is_pi = role == 0 || role == 5;
@@ -251,7 +260,7 @@ __device__ __forceinline__ void target_critic_split_body(const EngineDev* __rest
   // (the bulk of the bytes) after the batch record's loads, so the waits for
   // the record do not include it (loads complete in issue order)
   const GemmW w0 = gw_fwd(L0);
-  const GemmW w1 = gw_sub<T>(L1.Wc, L1.Kp, h * HH, HH, 0, L1.Kp, L1.bias + h * HH, HH);
+  const GemmW w1 = gw_sub<T>(L1.Wc, L1.Kp, h * HHr, HHr, 0, L1.Kp, L1.bias + h * HHr, HHr);
   HTiles<T, 2, HC0> h0;
   HTiles<T, 1, NCH_H> h1;
   ht_issue<T, 2, HC0>(h0, w0);
@@ -388,6 +397,9 @@ __device__ __forceinline__ void target_critic_split_body(const EngineDev* __rest
 
   // pi's squashed-Gaussian head (models.py:79-87) from two layer-2 partials:
   // o = p0 + p1 + b2 (same order in every consumer), one lane per (row, dim)
+  // tgt: the WP parts of pi(s')'s layer-2 partial (g0 = part 0's granules; parts
+  // are gs2 granules apart), summed in part order; else this half's own partial
+  // (outB) and the peer half's granules g1, in half order
   auto head = [&](const AS_G uint64_t* g0, const AS_G uint64_t* g1, bool tgt, lf* actB, lf* lpOut, bool stash) {
     const AS_C NetDev& pn = E.net[NET_PI];
     const AS_G float* b2 = GPC(float, pn.l[2].bias);
@@ -403,12 +415,22 @@ __device__ __forceinline__ void target_critic_split_body(const EngineDev* __rest
       if (live) {
         float mu, lsr;
         if (tgt) {
-          const AS_G uint64_t* gg[4] = {g0 + r * 2 * A + j, g1 + r * 2 * A + j, g0 + r * 2 * A + A + j,
-                                        g1 + r * 2 * A + A + j};
-          float v[4];
-          gran_getn<4>(E, gg, ep, v);
-          mu = (v[0] + v[1]) + b2mu;
-          lsr = (v[2] + v[3]) + b2ls;
+          const AS_G uint64_t* gg[2 * WP];
+#pragma unroll
+          for (int p = 0; p < WP; ++p) {
+            gg[p] = g0 + (size_t)p * E.gs2 + r * 2 * A + j;
+            gg[WP + p] = g0 + (size_t)p * E.gs2 + r * 2 * A + A + j;
+          }
+          float v[2 * WP];
+          gran_getn<2 * WP>(E, gg, ep, v);
+          float smu = v[0], sls = v[WP];
+#pragma unroll
+          for (int p = 1; p < WP; ++p) {
+            smu += v[p];
+            sls += v[WP + p];
+          }
+          mu = smu + b2mu;
+          lsr = sls + b2ls;
         } else {  // g0 / g1 = this half's own partial (in outB) and the peer's granules, in half order
           const float pown0 = outB[r * ldo + j], pown1 = outB[r * ldo + A + j];
           const AS_G uint64_t* gg[2] = {g1 + r * 2 * A + j, g1 + r * 2 * A + A + j};
@@ -483,7 +505,7 @@ __device__ __forceinline__ void target_critic_split_body(const EngineDev* __rest
         H1[r * ldh1 + col] = act == ACT_RELU ? (p > 0.f ? p : 0.f) : p;
       }
     });
-    if (act != ACT_RELU && act != ACT_ID) act_pass_fwd<R>(H1, ldh1, HH >> 4, act);
+    if (act != ACT_RELU && act != ACT_ID) act_pass_fwd<R>(H1, ldh1, HHr >> 4, act);
     __syncthreads();
     if (pi_actor) {  // this half's layer-1 pre-activations
       AS_G float* ps = GP(float, L1.pstash) + (size_t)r0 * L1.Np + h * HH;
@@ -494,7 +516,7 @@ __device__ __forceinline__ void target_critic_split_body(const EngineDev* __rest
                     nvalid, nullptr);
     STAMP(3);
     // layer 2, this half's partial sum: outB [R][Np2]
-    const GemmW w2 = gw_sub<T>(L2.Wc, L2.Kp, 0, L2.Np, h * HH, HH, nullptr, 0);
+    const GemmW w2 = gw_sub<T>(L2.Wc, L2.Kp, 0, L2.Np, h * HHr, HHr, nullptr, 0);
     GemmW w2n = w2;
     w2n.NT = (L2.N + 15) >> 4;  // output tiles that hold data
     gemm_ksplit<T>(H1, ldh1, w2n, red, outB, ldo);
@@ -539,7 +561,7 @@ __device__ __forceinline__ void target_critic_split_body(const EngineDev* __rest
   } else if (role == 1 || role == 2) {
     // ---- target critic t (agent.py:195-211): a~', log pi' from pi(s')'s two partials
     const int t = role - 1;
-    head(gs_at(E, GS_PI, rbi, 0), gs_at(E, GS_PI, rbi, 1), true, a2B, lpB, false);
+    head(gs_at(E, GS_PI, rbi, 0), nullptr, true, a2B, lpB, false);
     if (t == 0 && h == 0 && tid < R) gran_put(gs_at(E, GS_LP, rbi, 0) + tid, lpB[tid], ep);
     STAMP(7);
     build_x(s2B, a2B, A);

@@ -78,6 +78,17 @@ if SPLIT:  # sac_split.h stamps
     names.update({2: "L0", 3: "L1 half", 4: "L2 partial", 6: "partials published", 7: "pi head (s')",
                   9: "Qt partial published", 33: "inputs", 34: "pi inputs", 36: "Q1 fwd", 37: "Q2 fwd",
                   38: "Q1 da partial", 39: "pi: critics combined", 35: "pi bwd + GT"})
+WPI = (4 if prec == "fp32" else 2) if SPLIT else 1  # phase A: pi(s') parts (split_wpi)
+
+
+def role_of(ph, b, G):
+    """Role index of phase-relative block ids b (phase A: pi(s') has WPI parts per row tile)."""
+    if ph == "A" and SPLIT:
+        n0 = WPI * nrt
+        return np.where(b < n0, 0, 1 + (b - n0) // G)
+    return b // G
+
+
 PH = {"A": list(range(0, 17)) + [20, 21, 22, 23, 56, 57, 59, 60],  # 20-23: free for DSTAMP probes
       "C": list(range(32, 40)) + [61], "B": [48, 51, 49, 50, 62], "D": [52, 55, 53, 54, 63]}
 ROLES = {"A": ["pi(s')", "Qt1", "Qt2", "Q1", "Q2", "pi(s)"], "C": ["Q1", "Q2", "pi"]}  # block-group order
@@ -98,7 +109,8 @@ for ph, ids in PH.items():
     if ph in ROLES and eng.roles:
         rb_ = blk - OFF[ph]
         G = GROUP_C if ph == "C" else GROUP
-        groups = {nm: (rb_ >= 0) & ((rb_ // G) == k) for k, nm in enumerate(ROLES[ph])}
+        ridx = role_of(ph, rb_, G)
+        groups = {nm: (rb_ >= 0) & (ridx == k) for k, nm in enumerate(ROLES[ph])}
         if OFF[ph]:
             groups["upd"] = rb_ < 0
     print(f"=== phase {ph}")
@@ -160,7 +172,7 @@ for ph, ids in PH.items():
                     rb2 = blk_r - OFF[ph]
                     k = list(groups).index(g) if g in ROLES.get(ph, []) else -1
                     G = GROUP_C if ph == "C" else GROUP
-                    gm = (rb2 >= 0) & ((rb2 // G) == k) if k >= 0 else (rb2 < 0)
+                    gm = (rb2 >= 0) & (role_of(ph, rb2, G) == k) if k >= 0 else (rb2 < 0)
                 v = sel_r[gm, i]
                 v = v[v > 0]
                 if v.size:
