@@ -471,7 +471,8 @@ __device__ __forceinline__ void target_critic_split_body(const EngineDev* __rest
   };
 
   // ---- layer 0 (full) and layer 1 (this half) forward: H0, H1 in LDS; P0 / P1 kept
-  auto forward01 = [&](bool keepP, bool stXT, bool pi_actor) {
+  auto no_hook = [] {};
+  auto forward01 = [&](bool keepP, bool stXT, bool pi_actor, auto&& after_l1) {
     // layer 0: X [R][Kp0] -> P0 / H0 [R][H]
     const int act = net.hid_act;
     gemm_hs<T, 2, HC0>(Xb, ld, w0, &h0, [&](int j, int col, const f32x4& acc) {
@@ -505,6 +506,7 @@ __device__ __forceinline__ void target_critic_split_body(const EngineDev* __rest
         H1[r * ldh1 + col] = act == ACT_RELU ? (p > 0.f ? p : 0.f) : p;
       }
     });
+    after_l1();  // layer 1's held weights are dead from here
     if (act != ACT_RELU && act != ACT_ID) act_pass_fwd<R>(H1, ldh1, HHr >> 4, act);
     __syncthreads();
     if (pi_actor) {  // this half's layer-1 pre-activations
@@ -537,7 +539,7 @@ __device__ __forceinline__ void target_critic_split_body(const EngineDev* __rest
   if (role == 0) {
     // ---- pi(s'): the critical path's head
     build_x(s2B, aB, 0);
-    forward01(false, false, false);
+    forward01(false, false, false, no_hook);
     AS_G uint64_t* g = gs_at(E, GS_PI, rbi, h);
     for (int i = tid; i < R * 2 * A; i += SAC_THREADS) gran_put(g + i, outB[(i / (2 * A)) * ldo + i % (2 * A)], ep);
     STAMP(6);
@@ -548,7 +550,7 @@ __device__ __forceinline__ void target_critic_split_body(const EngineDev* __rest
     build_x(sB, aB, 0);
     // layer-0 input X^T: both halves store it (columns h Bp + r0: the partial dW layout)
     store_T<T, R>(Xb, ld, L0.Kp, L0.K, (T*)L0.XT + par * L0.xt_par, 2 * Bp, h * Bp + r0, nvalid, nullptr);
-    forward01(true, true, true);
+    forward01(true, true, true, no_hook);
     AS_G uint64_t* g = gs_at(E, GS_PS, rbi, h);
     for (int i = tid; i < R * 2 * A; i += SAC_THREADS) gran_put(g + i, outB[(i / (2 * A)) * ldo + i % (2 * A)], ep);
     head(nullptr, gs_at(E, GS_PS, rbi, 1 - h), false, a2B, lpB, h == 0);
@@ -565,7 +567,7 @@ __device__ __forceinline__ void target_critic_split_body(const EngineDev* __rest
     if (t == 0 && h == 0 && tid < R) gran_put(gs_at(E, GS_LP, rbi, 0) + tid, lpB[tid], ep);
     STAMP(7);
     build_x(s2B, a2B, A);
-    forward01(false, false, false);
+    forward01(false, false, false, no_hook);
     if (tid < R) gran_put(gs_at(E, t ? GS_QT2 : GS_QT1, rbi, h) + tid, outB[tid * ldo], ep);
     STAMP(9);
   } else {
@@ -574,19 +576,25 @@ __device__ __forceinline__ void target_critic_split_body(const EngineDev* __rest
     // layer 1's dX operand for this half (rows k all, reduction over this half's n), held
     const GemmW wt1 = gw_sub<T>(L1.WTc, L1.Np, 0, L1.Kp, h * HH, HH, nullptr, 0);
     HTiles<T, 2, NCH_HH> ht1;
+    // bf16: held from the start too; fp32 (no register room: 51 VGPRs would
+    // spill) issued as soon as layer 1's forward GEMM has freed h1's registers.
+    // W2's element for this thread's column n = tid % HH
+    if constexpr (sizeof(T) == 2) ht_issue<T, 2, NCH_HH>(ht1, wt1);
+    static_assert(SAC_THREADS % SPLIT_HH == 0, "one W2 column per thread in the unit-seed loop");
+    const float w2n = GPC(float, net.P + L2.w_off)[h * HH + tid % HH];  // W2 [1][H] fp32 master
     build_x(sB, aB, A);
     // layer-0 input X^T is shared by Q1 and Q2: Q1's halves store it (columns h Bp + r0)
     if (qi == 0) store_T<T, R>(Xb, ld, L0.Kp, L0.K, L0.XT, 2 * Bp, h * Bp + r0, nvalid, nullptr);
-    forward01(true, true, false);
-    ht_issue<T, 2, NCH_HH>(ht1, wt1);  // h1's registers are free now
+    forward01(true, true, false, [&] {
+      if constexpr (sizeof(T) == 4) ht_issue<T, 2, NCH_HH>(ht1, wt1);
+    });
     if (tid < R) gran_put(gs_at(E, qi ? GS_QA2 : GS_QA1, rbi, h) + tid, outB[tid * ldo], ep);
     // unit-seed backward (every layer's dY is linear in the row's seed 2(q - y)/B):
     // U1[r][n] = act'(P1[r][n]) * W2[0][h HH + n];  U0p = act'(P0) * (U1 W1[half])
     {
-      const AS_G float* w2row = GPC(float, net.P + L2.w_off) + h * HH;  // W2 [1][H] fp32 master
       for (int i = tid; i < R * HH; i += SAC_THREADS) {
-        const int r = i / HH, n = i % HH;
-        U1[r * ldu1 + n] = act_bwd(net.hid_act, P1[r * ldp1 + n], w2row[n]);
+        const int r = i / HH, n = i % HH;  // n == tid % HH
+        U1[r * ldu1 + n] = act_bwd(net.hid_act, P1[r * ldp1 + n], w2n);
       }
       __syncthreads();
       gemm_hs<T, 2, NCH_HH>(U1, ldu1, wt1, &ht1, [&](int j, int col, const f32x4& acc) {
