@@ -109,8 +109,11 @@ def gather_sweep(rb, device, sizes=(256, 4096, 65536, 1_048_576), reps=20):
                      which also runs B = 1,048,576 > the 1e6-row buffer.
     Returns {form: {B: GB/s}} with GB/s = B_gather / kernel time, B_gather =
     4 B (2 obs + act + 2) bytes read (the gather writes as many
-    again), plus the per-launch ms of each point (hipEvents on the launch
-    stream, the current torch stream)."""
+    again), plus the per-launch ms of each point: `reps` back-to-back launches
+    timed with hipEvents on the launch stream, and (as "ms_graph") the same
+    launches captured in one hipGraph and timed around its replay (measured:
+    within ~10% of the eager figure; the graph form is the slower one at
+    B = 65,536)."""
     from sac import _engine as E
     import ctypes
 
@@ -118,7 +121,7 @@ def gather_sweep(rb, device, sizes=(256, 4096, 65536, 1_048_576), reps=20):
     W = 2 * rb.obs_dim + rb.act_dim + 2
     st = E.stream_handle(device)
     desc = rb.desc
-    out = {"sample_gather": {}, "gather": {}, "ms": {}}
+    out = {"sample_gather": {}, "gather": {}, "ms": {}, "ms_graph": {}}
     f = dict(dtype=torch.float32, device=device)
     for B in sizes:
         s, a, r, s2, d = (torch.empty(B, rb.obs_dim, **f), torch.empty(B, rb.act_dim, **f), torch.empty(B, **f),
@@ -126,23 +129,36 @@ def gather_sweep(rb, device, sizes=(256, 4096, 65536, 1_048_576), reps=20):
         ptrs = [E.ptr(t) for t in (s, a, r, s2, d)]
         ridx = torch.randint(0, len(rb), (B,), dtype=torch.int32, device=device,
                              generator=torch.Generator(device=device).manual_seed(B))
-        forms = {"gather": lambda k: E.check(lib.sac_replay_gather(ctypes.byref(desc), E.ptr(ridx), B, *ptrs, st))}
+        forms = {"gather": lambda k, st: E.check(lib.sac_replay_gather(ctypes.byref(desc), E.ptr(ridx), B, *ptrs, st))}
         if B <= len(rb):
-            forms["sample_gather"] = lambda k: E.check(lib.sac_replay_sample_gather(
+            forms["sample_gather"] = lambda k, st: E.check(lib.sac_replay_sample_gather(
                 ctypes.byref(desc), B, 7, k, None, *ptrs, st))
         for form, once in forms.items():
             for k in range(3):
-                once(k)
+                once(k, st)
             torch.cuda.synchronize()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
             for k in range(reps):
-                once(k)
+                once(k, st)
             e1.record()
             torch.cuda.synchronize()
             ms = e0.elapsed_time(e1) / reps
             out[form][str(B)] = round(B * W * 4 / (ms * 1e-3) / 1e9, 3)
             out["ms"][f"{form}/{B}"] = round(ms, 5)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                cst = E.stream_handle(device)  # the capture stream
+                for k in range(reps):
+                    once(k, cst)
+            g.replay()
+            torch.cuda.synchronize()
+            e0.record()
+            g.replay()
+            e1.record()
+            torch.cuda.synchronize()
+            del g
+            out["ms_graph"][f"{form}/{B}"] = round(e0.elapsed_time(e1) / reps, 5)
     return out
 
 
@@ -374,6 +390,7 @@ def main():
             line["replay_gather_GBps_sweep"] = sweep["gather"]
             line["replay_layout"] = f"transition records, row stride {rb.row_stride} floats"
             line["replay_gather_GBps_sweep_soa_layout"] = sweep_soa["gather"]
+            line["replay_gather_ms_per_launch"] = {"eager": sweep["ms"], "graph": sweep["ms_graph"]}
             bmax = max(int(b) for b in sweep["gather"])
             ms = sweep["ms"][f"gather/{bmax}"]
             gk = ("replay_gather_records_kernel" if rb.layout == "records" and rb.row_stride in (16, 32, 64, 128, 256)

@@ -864,7 +864,30 @@ __device__ __forceinline__ void dw_adam_tile(const AS_C EngineDev& E, const Tile
   // this step's Adam scalars (written by phase A)
   const float neg_step = GPC(float, E.adam_sc)[par * 6 + td.opt * 2];
   const float bc2s = GPC(float, E.adam_sc)[par * 6 + td.opt * 2 + 1];
-  // ---- 1. loads: element state + bias state + staged operands
+  // ---- 1. loads: the first round of staged operands, then element state + bias
+  // state + bias partials, all before the first wait (one round trip; the bias
+  // sums below wait for everything issued before them, in issue order)
+  constexpr int MAXS = 4, PPT = 64 * (SAC_UPD_BCH / EPR) / UT;  // slots, pieces per thread per full chunk
+  const int rstep = nslot * SAC_UPD_BCH;                          // batch columns per round
+  u32x4 rg[MAXS][PPT];
+  // round r0's slot sl -> rg[sl] (16-B pieces of the 32 dY^T rows, then the 32 X^T rows)
+  auto issue = [&](int r0, auto slc) {
+    constexpr int sl = decltype(slc)::value;
+    const int b0 = r0 + sl * SAC_UPD_BCH;
+    if (sl < nslot && b0 < Bp) {  // uniform
+      const int bch = Bp - b0 < SAC_UPD_BCH ? Bp - b0 : SAC_UPD_BCH;
+      const int per_row = bch / EPR;  // 16-B pieces per operand row of this chunk
+#pragma unroll
+      for (int pi = 0; pi < PPT; ++pi) {
+        const int i = threadIdx.x + pi * UT;
+        const int row = i / per_row, pc = i % per_row;
+        const AS_G T* src = row < 32 ? GPC(T, td.GT) + (size_t)row * td.ld
+                                     : GPC(T, td.XT) + par * td.xt_par + (size_t)(row - 32) * td.ldx;
+        if (i < 64 * per_row) rg[sl][pi] = *(const AS_G u32x4*)(src + b0 + pc * EPR);
+      }
+    }
+  };
+  static_for<MAXS>([&](auto sl) { issue(0, sl); });
   AS_G float* W = GP(float, td.W);
   AS_G float* Wm = GP(float, td.Wm);
   AS_G float* Wv = GP(float, td.Wv);
@@ -897,9 +920,9 @@ __device__ __forceinline__ void dw_adam_tile(const AS_C EngineDev& E, const Tile
   }
   // bias gradient: the row tiles' partial sums, 16 partial lanes per column
   // (512 lanes, BPT per thread: the same sums for 4-, 8- and 16-wave blocks);
-  // each lane's loads are issued 8 at a time (one round trip per 8 row tiles,
+  // each lane's loads are issued 16 at a time (one round trip per 16 row tiles,
   // not one per row tile: 256 row tiles at B = 4096) and added in row-tile order
-  constexpr int BPT = (512 + UT - 1) / UT;
+  constexpr int BPT = (512 + UT - 1) / UT, BU = 16;
   float bsum[BPT];
 #pragma unroll
   for (int j = 0; j < BPT; ++j) {
@@ -907,23 +930,23 @@ __device__ __forceinline__ void dw_adam_tile(const AS_C EngineDev& E, const Tile
     bsum[j] = 0.f;
     if (do_bias && t < 512 && td.n0 + bn < td.N) {
       const AS_G float* dbp = GPC(float, td.dbp) + td.n0 + bn;
-      for (int rt0 = bs; rt0 < td.nrt; rt0 += 16 * 8) {
-        float pv[8];
+      for (int rt0 = bs; rt0 < td.nrt; rt0 += 16 * BU) {
+        float pv[BU];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
+        for (int u = 0; u < BU; ++u) {
           const int rt = rt0 + 16 * u;
           pv[u] = rt < td.nrt ? dbp[(size_t)rt * td.N] : 0.f;
         }
 #pragma unroll
-        for (int u = 0; u < 8; ++u)
+        for (int u = 0; u < BU; ++u)
           if (rt0 + 16 * u < td.nrt) bsum[j] += pv[u];
       }
     }
   }
   // ---- 2. dW = dY^T X over the batch, staged through LDS in 512-B row chunks,
-  // nslot chunks per round (every load of a round in flight before its first
-  // LDS store: one round trip per nslot chunks); waves 0-3 run one 16x16
-  // sub-tile each, chunks in batch order
+  // nslot chunks per round; waves run (16x16 sub-tile, K-quarter) pairs, chunks
+  // in batch order.  A slot's registers are re-issued for the next round as
+  // soon as they are in LDS, so round r + 1's loads land under round r's MFMAs.
   const int lane = tid & 63, wave = wave_id();
   const int c = lane & 15, g = lane >> 4;
   constexpr int KQ = 4, NWV = UT / 64, PPW = 16 / NWV;  // K-quarters, waves, pairs per wave
@@ -931,30 +954,12 @@ __device__ __forceinline__ void dw_adam_tile(const AS_C EngineDev& E, const Tile
   f32x4 acc[PPW];
 #pragma unroll
   for (int j = 0; j < PPW; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  constexpr int MAXS = 4, PPT = 64 * (SAC_UPD_BCH / EPR) / UT;  // slots, pieces per thread per full chunk
-  for (int r0 = 0; r0 < Bp; r0 += nslot * SAC_UPD_BCH) {
-    u32x4 rg[MAXS][PPT];
-#pragma unroll
-    for (int sl = 0; sl < MAXS; ++sl) {
-      const int b0 = r0 + sl * SAC_UPD_BCH;
-      if (sl < nslot && b0 < Bp) {  // uniform
-        const int bch = Bp - b0 < SAC_UPD_BCH ? Bp - b0 : SAC_UPD_BCH;
-        const int per_row = bch / EPR;  // 16-B pieces per operand row of this chunk
-#pragma unroll
-        for (int pi = 0; pi < PPT; ++pi) {
-          const int i = tid + pi * UT;
-          const int row = i / per_row, pc = i % per_row;
-          const AS_G T* src = row < 32 ? GPC(T, td.GT) + (size_t)row * td.ld
-                                       : GPC(T, td.XT) + par * td.xt_par + (size_t)(row - 32) * td.ldx;
-          if (i < 64 * per_row) rg[sl][pi] = *(const AS_G u32x4*)(src + b0 + pc * EPR);
-        }
-      }
-    }
+  for (int r0 = 0; r0 < Bp; r0 += rstep) {
     // slot by slot: its pieces -> LDS (waits only for this slot's loads: they
-    // complete in issue order), barrier, its MFMAs -- while the later slots'
-    // loads are still landing
-#pragma unroll
-    for (int sl = 0; sl < MAXS; ++sl) {
+    // complete in issue order), the next round's loads into its registers,
+    // barrier, its MFMAs -- while the later slots' loads are still landing
+    static_for<MAXS>([&](auto slc) {
+      constexpr int sl = decltype(slc)::value;
       const int b0 = r0 + sl * SAC_UPD_BCH;
       if (sl < nslot && b0 < Bp) {  // uniform
         const int bch = Bp - b0 < SAC_UPD_BCH ? Bp - b0 : SAC_UPD_BCH;
@@ -965,6 +970,7 @@ __device__ __forceinline__ void dw_adam_tile(const AS_C EngineDev& E, const Tile
           const int row = i / per_row, pc = i % per_row;
           if (i < 64 * per_row) *(AS_L u32x4*)(stage + sl * slot_el + row * lds_row + pc * EPR) = rg[sl][pi];
         }
+        issue(r0 + rstep, slc);
         __syncthreads();
         if (r0 == 0 && sl == 0) STAMP(polyak ? 51 : 55);
 #pragma unroll
@@ -986,7 +992,7 @@ __device__ __forceinline__ void dw_adam_tile(const AS_C EngineDev& E, const Tile
           }
         }
       }
-    }
+    });
     __syncthreads();  // the stage is refilled by the next round
   }
   STAMP(polyak ? 49 : 53);
