@@ -844,7 +844,7 @@ __device__ __forceinline__ void count_done(uint32_t* counter) {
 #define SAC_UPD_LDS_FOR(slots) ((slots) * SAC_UPD_SLOT_BYTES + 2 * 32 * 33 * 4 + 32 * 17 * 4)
 template <typename T, int UT, bool COH>
 __device__ __forceinline__ void dw_adam_tile(const AS_C EngineDev& E, const TileDesc* tdp_, bool polyak, int par,
-                                             lf* lds) {
+                                             int par_x, lf* lds) {
   constexpr int KC = MM<T>::KC, KL = MM<T>::KL;
   constexpr int EPR = 16 / sizeof(T);  // elements per 16-B piece (= KL)
   constexpr int EPT = 1024 / UT;       // elements per thread
@@ -867,10 +867,17 @@ __device__ __forceinline__ void dw_adam_tile(const AS_C EngineDev& E, const Tile
   // ---- 1. loads: the first round of staged operands, then element state + bias
   // state + bias partials, all before the first wait (one round trip; the bias
   // sums below wait for everything issued before them, in issue order)
-  constexpr int MAXS = 4, PPT = 64 * (SAC_UPD_BCH / EPR) / UT;  // slots, pieces per thread per full chunk
-  const int rstep = nslot * SAC_UPD_BCH;                          // batch columns per round
-  u32x4 rg[MAXS][PPT];
-  // round r0's slot sl -> rg[sl] (16-B pieces of the 32 dY^T rows, then the 32 X^T rows)
+  // slots, pieces per thread per operand (32 rows) per full chunk
+  constexpr int MAXS = 4, PPO = 32 * (SAC_UPD_BCH / EPR) / UT;
+  static_assert(PPO >= 1 && (32 * (SAC_UPD_BCH / EPR)) % UT == 0, "whole pieces per thread");
+  const int rstep = nslot * SAC_UPD_BCH;  // batch columns per round
+  u32x4 rg[MAXS][2][PPO];
+  // the two operands' bases as separate values: a per-lane choice between two
+  // descriptor fields was compiled into a per-lane LOAD of the chosen field and a
+  // wait before every piece (the pieces' loads ran one round trip after another)
+  const AS_G T* const src_op[2] = {GPC(T, td.GT), GPC(T, td.XT) + par_x * td.xt_par};
+  const int ld_op[2] = {td.ld, td.ldx};
+  // round r0's slot sl -> rg[sl] (16-B pieces of the 32 dY^T rows, then of the 32 X^T rows)
   auto issue = [&](int r0, auto slc) {
     constexpr int sl = decltype(slc)::value;
     const int b0 = r0 + sl * SAC_UPD_BCH;
@@ -878,13 +885,14 @@ __device__ __forceinline__ void dw_adam_tile(const AS_C EngineDev& E, const Tile
       const int bch = Bp - b0 < SAC_UPD_BCH ? Bp - b0 : SAC_UPD_BCH;
       const int per_row = bch / EPR;  // 16-B pieces per operand row of this chunk
 #pragma unroll
-      for (int pi = 0; pi < PPT; ++pi) {
-        const int i = threadIdx.x + pi * UT;
-        const int row = i / per_row, pc = i % per_row;
-        const AS_G T* src = row < 32 ? GPC(T, td.GT) + (size_t)row * td.ld
-                                     : GPC(T, td.XT) + par * td.xt_par + (size_t)(row - 32) * td.ldx;
-        if (i < 64 * per_row) rg[sl][pi] = *(const AS_G u32x4*)(src + b0 + pc * EPR);
-      }
+      for (int op = 0; op < 2; ++op)
+#pragma unroll
+        for (int pi = 0; pi < PPO; ++pi) {
+          const int i = threadIdx.x + pi * UT;
+          const int row = i / per_row, pc = i % per_row;
+          if (i < 32 * per_row)
+            rg[sl][op][pi] = *(const AS_G u32x4*)(src_op[op] + (size_t)row * ld_op[op] + b0 + pc * EPR);
+        }
     }
   };
   static_for<MAXS>([&](auto sl) { issue(0, sl); });
@@ -965,11 +973,13 @@ __device__ __forceinline__ void dw_adam_tile(const AS_C EngineDev& E, const Tile
         const int bch = Bp - b0 < SAC_UPD_BCH ? Bp - b0 : SAC_UPD_BCH;
         const int per_row = bch / EPR;
 #pragma unroll
-        for (int pi = 0; pi < PPT; ++pi) {
-          const int i = tid + pi * UT;
-          const int row = i / per_row, pc = i % per_row;
-          if (i < 64 * per_row) *(AS_L u32x4*)(stage + sl * slot_el + row * lds_row + pc * EPR) = rg[sl][pi];
-        }
+        for (int op = 0; op < 2; ++op)
+#pragma unroll
+          for (int pi = 0; pi < PPO; ++pi) {
+            const int i = tid + pi * UT;
+            const int row = i / per_row + 32 * op, pc = i % per_row;
+            if (i < 32 * per_row) *(AS_L u32x4*)(stage + sl * slot_el + row * lds_row + pc * EPR) = rg[sl][op][pi];
+          }
         issue(r0 + rstep, slc);
         __syncthreads();
         if (r0 == 0 && sl == 0) STAMP(polyak ? 51 : 55);
@@ -1438,7 +1448,7 @@ __device__ __forceinline__ void target_critic_body(const EngineDev* __restrict__
     if (bid <= E.nD) {
       const int parD = (int)((*GPC(uint64_t, E.rng_step) - 1) & 1);  // the step phase C just closed
       if (bid < E.nD)
-        dw_adam_tile<T, SAC_THREADS, true>(E, E.tilesD + bid, false, parD, lds);
+        dw_adam_tile<T, SAC_THREADS, true>(E, E.tilesD + bid, false, parD, parD, lds);
       else
         alpha_and_losses(E, parD, lds);
       count_done((uint32_t*)E.sync + SYNC_DDONE);
@@ -2113,7 +2123,7 @@ __global__ void __launch_bounds__(SAC_THREADS) sac_actor(const EngineDev* __rest
   const int nrole = ROLES ? 3 * E.nrt : E.nrt * E.xs;
   if (WITH_B && (int)blockIdx.x < E.nB) {
     const AS_C TileDesc& td = *((const AS_C TileDesc*)E.tilesB + blockIdx.x);
-    dw_adam_tile<T, SAC_THREADS, true>(E, E.tilesB + blockIdx.x, true, (int)(*GPC(uint64_t, E.rng_step) & 1),
+    dw_adam_tile<T, SAC_THREADS, true>(E, E.tilesB + blockIdx.x, true, (int)(*GPC(uint64_t, E.rng_step) & 1), 0,
                                        (lf*)lds_raw);
     count_done((uint32_t*)E.sync + SYNC_BDONE + 16 * (td.opt - 1));
   } else if (bid >= nrole) {
@@ -2131,7 +2141,8 @@ __global__ void __launch_bounds__(SAC_UPD_THREADS) sac_critic_update(const Engin
                                                          const TileDesc* __restrict__ tiles) {
   const AS_C EngineDev& E = *(const AS_C EngineDev*)Ep;
   extern __shared__ float upd_lds[];
-  dw_adam_tile<T, SAC_UPD_THREADS, false>(E, tiles + blockIdx.x, true, (int)(*GPC(uint64_t, E.rng_step) & 1),
+  // critic tiles: one X^T copy (xt_par = 0), so their operand loads need not wait for the step's parity
+  dw_adam_tile<T, SAC_UPD_THREADS, false>(E, tiles + blockIdx.x, true, (int)(*GPC(uint64_t, E.rng_step) & 1), 0,
                                           (lf*)upd_lds);
   END_STAMP(62);  // standalone: the launch boundary publishes (no counter)
 }
@@ -2143,7 +2154,7 @@ __global__ void __launch_bounds__(SAC_UPD_THREADS) sac_actor_update(const Engine
   const int par = (int)((*GPC(uint64_t, E.rng_step) - 1) & 1);  // phase C already advanced the step
   extern __shared__ float upd_lds[];
   if ((int)blockIdx.x < ntiles)
-    dw_adam_tile<T, SAC_UPD_THREADS, false>(E, tiles + blockIdx.x, false, par, (lf*)upd_lds);
+    dw_adam_tile<T, SAC_UPD_THREADS, false>(E, tiles + blockIdx.x, false, par, par, (lf*)upd_lds);
   else
     alpha_and_losses(E, par, (lf*)upd_lds);
   END_STAMP(63);  // standalone: the launch boundary publishes (no counter)
