@@ -415,8 +415,12 @@ static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
   // reduces over its parts' columns (critics 2: phase A halves; pi wc: phase C
   // parts); a large batch is split into parts of at most 1024 columns (C3:
   // 4 x 1024), so no block streams more than 1024 batch columns of operands.
+  // fp32 hidden-split layer 0: the parts' partial dY summed while staging in one
+  // block (TileDesc.gsum; SAC_GSUM=0: batch parts with a granule hand-off)
+  int gsum_on = esz == 4;
+  if (const char* v = getenv("SAC_GSUM")) gsum_on = gsum_on && atoi(v) != 0;
   auto tile_parts = [&](int ni, int l) {
-    if (l == 0 && split) return ni == NET_PI ? wc : 2;
+    if (l == 0 && split) return gsum_on ? 1 : ni == NET_PI ? wc : 2;
     return Bp > 1024 ? std::min(4, (Bp + 1023) / 1024) : 1;
   };
   int nB = 0, nD = 0, nhalf = 0;
@@ -598,6 +602,15 @@ static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
             t.ldx = t.bp;
             t.kpart = 0;
             t.nparts = 1;
+            t.gsum = 1;
+            t.goff = 0;
+            if (l == 0 && split && gsum_on) {  // one block: dY parts [p Bp, (p+1) Bp) summed, X^T [0, Bp)
+              t.gsum = ni == NET_PI ? wc : 2;
+              t.goff = Bp;
+              t.bp = Bp;
+              t.ld = bpg;
+              t.ldx = 2 * Bp;
+            }
             const int parts = tile_parts(ni, l);
             if (parts > 1) {
               // consumer part 1 (batch columns [0, bpp)) + producer parts 2..P ([(p-1) bpp, p bpp))

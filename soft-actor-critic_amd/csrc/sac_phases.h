@@ -156,6 +156,11 @@ struct TileDesc {
   // and runs Adam.  kpart 0: a whole tile.
   int kpart, nparts;
   uint64_t* part;
+  // fp32 hidden-split layer 0, one block (kpart 0): the gsum parts' partial dY
+  // column blocks (goff elements apart) are added elementwise while staging, in
+  // part order, and reduced once against X -- no batch parts, no hand-off
+  long goff;
+  int gsum, pad_;
 };
 
 
@@ -216,7 +221,11 @@ __device__ __forceinline__ void prefetch_engine(const void* p) {
   const uint64_t base = (uint64_t)(uintptr_t)p;  // kernel-argument pointer: already uniform (SGPRs)
   asm volatile("s_load_dword s95, %0, 0\n\t" "s_load_dword s95, %0, 64\n\t" "s_load_dword s95, %0, 128\n\t" "s_load_dword s95, %0, 192\n\t" "s_load_dword s95, %0, 256\n\t" "s_load_dword s95, %0, 320\n\t" "s_load_dword s95, %0, 384\n\t" "s_load_dword s95, %0, 448\n\t" "s_load_dword s95, %0, 512\n\t" "s_load_dword s95, %0, 576\n\t" "s_load_dword s95, %0, 640\n\t" "s_load_dword s95, %0, 704\n\t" "s_load_dword s95, %0, 768\n\t" "s_load_dword s95, %0, 832\n\t" "s_load_dword s95, %0, 896\n\t" "s_load_dword s95, %0, 960\n\t" "s_load_dword s95, %0, 1024\n\t" "s_load_dword s95, %0, 1088\n\t" "s_load_dword s95, %0, 1152\n\t" "s_load_dword s95, %0, 1216\n\t" "s_load_dword s95, %0, 1280\n\t" "s_load_dword s95, %0, 1344\n\t" "s_load_dword s95, %0, 1408\n\t" "s_load_dword s95, %0, 1472\n\t" "s_load_dword s95, %0, 1536\n\t" "s_load_dword s95, %0, 1600\n\t" "s_load_dword s95, %0, 1664\n\t" "s_load_dword s95, %0, 1728\n\t" "s_load_dword s95, %0, 1792\n\t" "s_load_dword s95, %0, 1856\n\t" "s_load_dword s95, %0, 1920\n\t" "s_load_dword s95, %0, 1984\n\t" "s_load_dword s95, %0, 2048\n\t" "s_load_dword s95, %0, 2112\n\t" "s_load_dword s95, %0, 2176\n\t" "s_load_dword s95, %0, 2240\n\t" "s_load_dword s95, %0, 2304\n\t" "s_load_dword s95, %0, 2368\n\t" "s_load_dword s95, %0, 2432\n\t" "s_load_dword s95, %0, 2496\n\t" "s_load_dword s95, %0, 2560\n\t" "s_load_dword s95, %0, 2624\n\t" "s_load_dword s95, %0, 2688\n\t" "s_load_dword s95, %0, 2752\n\t" "s_load_dword s95, %0, 2816\n\t" "s_load_dword s95, %0, 2880\n\t" "s_load_dword s95, %0, 2944\n\t" "s_load_dword s95, %0, 3008\n\t" "s_load_dword s95, %0, 3072\n\t" "s_load_dword s95, %0, 3136\n\t" "s_load_dword s95, %0, 3200\n\t" "s_load_dword s95, %0, 3264\n\t" "s_load_dword s95, %0, 3328\n\t" "s_load_dword s95, %0, 3392\n\t" "s_load_dword s95, %0, 3456\n\t" "s_load_dword s95, %0, 3520\n\t" "s_load_dword s95, %0, 3584\n\t" "s_load_dword s95, %0, 3648\n\t" "s_load_dword s95, %0, 3712\n\t" "s_load_dword s95, %0, 3776\n\t" "s_load_dword s95, %0, 3840\n\t" "s_load_dword s95, %0, 3904\n\t" "s_load_dword s95, %0, 3968\n\t" "s_load_dword s95, %0, 4032\n\t" "s_waitcnt lgkmcnt(0)" :: "s"(base) : "s95", "memory");
 }
+#ifdef SAC_NO_PREFETCH
+#define PREFETCH_ARG(ptr) ((void)0)
+#else
 #define PREFETCH_ARG(ptr) prefetch_engine(ptr)
+#endif
 
 // ============================================================================ MFMA layer steps
 // A GEMM step streams a fragment-packed B matrix (weights W for a forward step,
@@ -842,9 +851,10 @@ __device__ __forceinline__ void count_done(uint32_t* counter) {
 // (>= the alpha block's 5 x 1024 floats)
 #define SAC_UPD_SLOT_BYTES (64 * 528)
 #define SAC_UPD_LDS_FOR(slots) ((slots) * SAC_UPD_SLOT_BYTES + 2 * 32 * 33 * 4 + 32 * 17 * 4)
-template <typename T, int UT, bool COH>
+template <typename T, int UT, bool COH, int GS = 1>
 __device__ __forceinline__ void dw_adam_tile(const AS_C EngineDev& E, const TileDesc* tdp_, bool polyak, int par,
                                              int par_x, lf* lds) {
+  static_assert(GS == 1 || sizeof(T) == 4, "dY parts are summed in fp32 only");
   constexpr int KC = MM<T>::KC, KL = MM<T>::KL;
   constexpr int EPR = 16 / sizeof(T);  // elements per 16-B piece (= KL)
   constexpr int EPT = 1024 / UT;       // elements per thread
@@ -867,31 +877,35 @@ __device__ __forceinline__ void dw_adam_tile(const AS_C EngineDev& E, const Tile
   // ---- 1. loads: the first round of staged operands, then element state + bias
   // state + bias partials, all before the first wait (one round trip; the bias
   // sums below wait for everything issued before them, in issue order)
-  // slots, pieces per thread per operand (32 rows) per full chunk
-  constexpr int MAXS = 4, PPO = 32 * (SAC_UPD_BCH / EPR) / UT;
+  // slots (2 with summed dY parts: register room), pieces per thread per operand
+  // (32 rows) per full chunk
+  constexpr int MAXS = GS > 1 ? 2 : 4, PPO = 32 * (SAC_UPD_BCH / EPR) / UT;
   static_assert(PPO >= 1 && (32 * (SAC_UPD_BCH / EPR)) % UT == 0, "whole pieces per thread");
-  const int rstep = nslot * SAC_UPD_BCH;  // batch columns per round
-  u32x4 rg[MAXS][2][PPO];
-  // the two operands' bases as separate values: a per-lane choice between two
+  const int ns = nslot < MAXS ? nslot : MAXS;  // slots per round
+  const int rstep = ns * SAC_UPD_BCH;          // batch columns per round
+  u32x4 rg[MAXS][GS + 1][PPO];                 // [slot][dY part 0..GS-1, then X][piece]
+  // the operands' bases as separate values: a per-lane choice between two
   // descriptor fields was compiled into a per-lane LOAD of the chosen field and a
   // wait before every piece (the pieces' loads ran one round trip after another)
-  const AS_G T* const src_op[2] = {GPC(T, td.GT), GPC(T, td.XT) + par_x * td.xt_par};
-  const int ld_op[2] = {td.ld, td.ldx};
-  // round r0's slot sl -> rg[sl] (16-B pieces of the 32 dY^T rows, then of the 32 X^T rows)
+  const AS_G T* const gsrc = GPC(T, td.GT);
+  const AS_G T* const xsrc = GPC(T, td.XT) + par_x * td.xt_par;
+  const long goff = GS > 1 ? td.goff : 0;
+  const int ldg = td.ld, ldx = td.ldx;
+  // round r0's slot sl -> rg[sl] (16-B pieces of the 32 dY^T rows of every part, then of the 32 X^T rows)
   auto issue = [&](int r0, auto slc) {
     constexpr int sl = decltype(slc)::value;
     const int b0 = r0 + sl * SAC_UPD_BCH;
-    if (sl < nslot && b0 < Bp) {  // uniform
+    if (sl < ns && b0 < Bp) {  // uniform
       const int bch = Bp - b0 < SAC_UPD_BCH ? Bp - b0 : SAC_UPD_BCH;
       const int per_row = bch / EPR;  // 16-B pieces per operand row of this chunk
 #pragma unroll
-      for (int op = 0; op < 2; ++op)
+      for (int op = 0; op <= GS; ++op)
 #pragma unroll
         for (int pi = 0; pi < PPO; ++pi) {
           const int i = threadIdx.x + pi * UT;
           const int row = i / per_row, pc = i % per_row;
-          if (i < 32 * per_row)
-            rg[sl][op][pi] = *(const AS_G u32x4*)(src_op[op] + (size_t)row * ld_op[op] + b0 + pc * EPR);
+          const AS_G T* src = op < GS ? gsrc + op * goff + (size_t)row * ldg : xsrc + (size_t)row * ldx;
+          if (i < 32 * per_row) rg[sl][op][pi] = *(const AS_G u32x4*)(src + b0 + pc * EPR);
         }
     }
   };
@@ -969,7 +983,7 @@ __device__ __forceinline__ void dw_adam_tile(const AS_C EngineDev& E, const Tile
     static_for<MAXS>([&](auto slc) {
       constexpr int sl = decltype(slc)::value;
       const int b0 = r0 + sl * SAC_UPD_BCH;
-      if (sl < nslot && b0 < Bp) {  // uniform
+      if (sl < ns && b0 < Bp) {  // uniform
         const int bch = Bp - b0 < SAC_UPD_BCH ? Bp - b0 : SAC_UPD_BCH;
         const int per_row = bch / EPR;
 #pragma unroll
@@ -978,7 +992,15 @@ __device__ __forceinline__ void dw_adam_tile(const AS_C EngineDev& E, const Tile
           for (int pi = 0; pi < PPO; ++pi) {
             const int i = tid + pi * UT;
             const int row = i / per_row + 32 * op, pc = i % per_row;
-            if (i < 32 * per_row) *(AS_L u32x4*)(stage + sl * slot_el + row * lds_row + pc * EPR) = rg[sl][op][pi];
+            u32x4 v = rg[sl][op ? GS : 0][pi];
+            if constexpr (GS > 1)
+              if (op == 0) {  // dY: the parts' partials added in part order (fp32)
+                f32x4 a = __builtin_bit_cast(f32x4, v);
+#pragma unroll
+                for (int q = 1; q < GS; ++q) a += __builtin_bit_cast(f32x4, rg[sl][q][pi]);
+                v = __builtin_bit_cast(u32x4, a);
+              }
+            if (i < 32 * per_row) *(AS_L u32x4*)(stage + sl * slot_el + row * lds_row + pc * EPR) = v;
           }
         issue(r0 + rstep, slc);
         __syncthreads();
@@ -1133,6 +1155,18 @@ __device__ __forceinline__ void dw_adam_tile(const AS_C EngineDev& E, const Tile
       coh_store16<COH>(base, (uint32_t)(off * sizeof(T)), *(const u32x4*)vv);
     }
   }
+}
+
+// a tile with summed dY parts (fp32 hidden-split layer 0) runs its own instance
+template <typename T, int UT, bool COH>
+__device__ __forceinline__ void dw_adam_tile_any(const AS_C EngineDev& E, const TileDesc* tdp_, bool polyak, int par,
+                                                 int par_x, lf* lds) {
+  if constexpr (sizeof(T) == 4) {
+    const int gs = ((const AS_C TileDesc*)tdp_)->gsum;  // uniform
+    if (gs == 4) return dw_adam_tile<T, UT, COH, 4>(E, tdp_, polyak, par, par_x, lds);
+    if (gs == 2) return dw_adam_tile<T, UT, COH, 2>(E, tdp_, polyak, par, par_x, lds);
+  }
+  dw_adam_tile<T, UT, COH, 1>(E, tdp_, polyak, par, par_x, lds);
 }
 
 // One block: reduces the step's loss partials into stats[0..3] and runs the
@@ -1448,7 +1482,7 @@ __device__ __forceinline__ void target_critic_body(const EngineDev* __restrict__
     if (bid <= E.nD) {
       const int parD = (int)((*GPC(uint64_t, E.rng_step) - 1) & 1);  // the step phase C just closed
       if (bid < E.nD)
-        dw_adam_tile<T, SAC_THREADS, true>(E, E.tilesD + bid, false, parD, parD, lds);
+        dw_adam_tile_any<T, SAC_THREADS, true>(E, E.tilesD + bid, false, parD, parD, lds);
       else
         alpha_and_losses(E, parD, lds);
       count_done((uint32_t*)E.sync + SYNC_DDONE);
@@ -2123,7 +2157,7 @@ __global__ void __launch_bounds__(SAC_THREADS) sac_actor(const EngineDev* __rest
   const int nrole = ROLES ? 3 * E.nrt : E.nrt * E.xs;
   if (WITH_B && (int)blockIdx.x < E.nB) {
     const AS_C TileDesc& td = *((const AS_C TileDesc*)E.tilesB + blockIdx.x);
-    dw_adam_tile<T, SAC_THREADS, true>(E, E.tilesB + blockIdx.x, true, (int)(*GPC(uint64_t, E.rng_step) & 1), 0,
+    dw_adam_tile_any<T, SAC_THREADS, true>(E, E.tilesB + blockIdx.x, true, (int)(*GPC(uint64_t, E.rng_step) & 1), 0,
                                        (lf*)lds_raw);
     count_done((uint32_t*)E.sync + SYNC_BDONE + 16 * (td.opt - 1));
   } else if (bid >= nrole) {
@@ -2142,7 +2176,7 @@ __global__ void __launch_bounds__(SAC_UPD_THREADS) sac_critic_update(const Engin
   const AS_C EngineDev& E = *(const AS_C EngineDev*)Ep;
   extern __shared__ float upd_lds[];
   // critic tiles: one X^T copy (xt_par = 0), so their operand loads need not wait for the step's parity
-  dw_adam_tile<T, SAC_UPD_THREADS, false>(E, tiles + blockIdx.x, true, (int)(*GPC(uint64_t, E.rng_step) & 1), 0,
+  dw_adam_tile_any<T, SAC_UPD_THREADS, false>(E, tiles + blockIdx.x, true, (int)(*GPC(uint64_t, E.rng_step) & 1), 0,
                                           (lf*)upd_lds);
   END_STAMP(62);  // standalone: the launch boundary publishes (no counter)
 }
@@ -2154,7 +2188,7 @@ __global__ void __launch_bounds__(SAC_UPD_THREADS) sac_actor_update(const Engine
   const int par = (int)((*GPC(uint64_t, E.rng_step) - 1) & 1);  // phase C already advanced the step
   extern __shared__ float upd_lds[];
   if ((int)blockIdx.x < ntiles)
-    dw_adam_tile<T, SAC_UPD_THREADS, false>(E, tiles + blockIdx.x, false, par, par, (lf*)upd_lds);
+    dw_adam_tile_any<T, SAC_UPD_THREADS, false>(E, tiles + blockIdx.x, false, par, par, (lf*)upd_lds);
   else
     alpha_and_losses(E, par, (lf*)upd_lds);
   END_STAMP(63);  // standalone: the launch boundary publishes (no counter)
