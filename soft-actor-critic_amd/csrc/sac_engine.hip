@@ -102,13 +102,19 @@ __device__ __forceinline__ void gather_field(const float* __restrict__ src, int 
   V* __restrict__ dv = (V*)dst;
   for (int i0 = 0; i0 < total; i0 += 64 * GATHER_GB) {
     V v[GATHER_GB];
+    int64_t sl[GATHER_GB];
+    int qq[GATHER_GB];
 #pragma unroll
     for (int u = 0; u < GATHER_GB; ++u) {
-      const int i = i0 + u * 64 + lane;
-      const int row = (unsigned)i / (unsigned)Q, q = i - row * Q;
-      const int64_t sl = __shfl(slot, row < 64 ? row : 63, 64);  // every lane joins the shuffle
-      if (i < total) v[u] = sv[sl * SV + q];
+      const int i = min(i0 + u * 64 + lane, total - 1);  // past the end: the last access again
+      const int row = (unsigned)i / (unsigned)Q;
+      qq[u] = i - row * Q;
+      sl[u] = __shfl(slot, row < 64 ? row : 63, 64);  // every lane joins the shuffle
     }
+    // loads unconditional: under a per-lane branch each one waited for the one before
+#pragma unroll
+    for (int u = 0; u < GATHER_GB; ++u)
+      if (i0 + u * 64 < total) v[u] = sv[sl[u] * SV + qq[u]];  // wave-uniform test
 #pragma unroll
     for (int u = 0; u < GATHER_GB; ++u) {
       const int i = i0 + u * 64 + lane;
@@ -164,14 +170,20 @@ __global__ void __launch_bounds__(256) replay_gather_records_kernel(
   const f32x4* __restrict__ rec = (const f32x4*)rb.obs;
   const int64_t SV = rb.row_stride >> 2;
   const int iters = (nrow + RPI - 1) / RPI;
+  const int pcl = piece < live ? piece : live - 1;  // padding pieces re-read the row's last live one
   for (int i0 = 0; i0 < iters; i0 += GATHER_GB) {
     f32x4 v[GATHER_GB];
+    int64_t sl[GATHER_GB];
 #pragma unroll
     for (int u = 0; u < GATHER_GB; ++u) {
       const int row = (i0 + u) * RPI + sub;
-      const int64_t sl = __shfl(slot, row < 64 ? row : 63, 64);
-      if (row < nrow && piece < live) v[u] = rec[sl * SV + piece];
+      sl[u] = __shfl(slot, row < 64 ? row : 63, 64);  // rows past nrow: slot 0
     }
+    // loads unconditional (no per-lane branch: under one each load waited for the
+    // one before, so a wave's rows were fetched one round trip after another)
+#pragma unroll
+    for (int u = 0; u < GATHER_GB; ++u)
+      if (i0 + u < iters) v[u] = rec[sl[u] * SV + pcl];  // wave-uniform test
 #pragma unroll
     for (int u = 0; u < GATHER_GB; ++u) {
       const int row = (i0 + u) * RPI + sub;
