@@ -425,15 +425,35 @@ static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
   h.gran2 = (uint64_t*)P(lay.take((size_t)GS_COUNT * nrt * SPLIT_GP * h.gs2 * 8));
   // Batch parts of an update tile (TileDesc.kpart): the hidden split's layer 0
   // reduces over its parts' columns (critics 2: phase A halves; pi wc: phase C
-  // parts); a large batch is split into parts of at most 1024 columns (C3:
-  // 4 x 1024), so no block streams more than 1024 batch columns of operands.
+  // parts); a large batch (Bp > 1024) is split into P <= 4 parts per phase, P
+  // chosen for the fewest block rounds x the longest block: a block takes about
+  // 2 us + its operand bytes at ~25 GB/s (one workgroup per CU; measured on C3:
+  // 1024 fp32 columns = 256 KB of dY^T / X^T in ~12 us), so at C3 (160 critic
+  // tiles, 80 policy tiles) P = 3: 480 blocks (2 rounds) for B and 240 (one) for D.
   // fp32 hidden-split layer 0: the parts' partial dY summed while staging in one
   // block (TileDesc.gsum; SAC_GSUM=0: batch parts with a granule hand-off)
   int gsum_on = esz == 4;
   if (const char* v = getenv("SAC_GSUM")) gsum_on = gsum_on && atoi(v) != 0;
+  int tilesBD[2] = {0, 0};  // [critics (B), policy (D)]
+  for (int ni = NET_PI; ni <= NET_Q2; ++ni)
+    for (int l = 0; l < h.net[ni].L; ++l)
+      tilesBD[ni == NET_PI] += (h.net[ni].l[l].Np / 32) * (h.net[ni].l[l].Kp / 32);
+  auto batch_parts = [&](int ntiles, int extra) {
+    if (Bp <= 1024) return 1;
+    if (const char* v = getenv("SAC_BPARTS")) return std::max(1, std::min(4, atoi(v)));
+    int best = 4;
+    double bc = 1e30;
+    for (int P = 2; P <= 4; ++P) {
+      const int rounds = (ntiles * P + extra + 255) / 256;
+      const double c = rounds * (2.0 + 64.0 * rup((Bp + P - 1) / P, 32) * esz / 25e3);  // us
+      if (c < bc - 1e-9) bc = c, best = P;
+    }
+    return best;
+  };
+  const int bpartsB = batch_parts(tilesBD[0], 0), bpartsD = batch_parts(tilesBD[1], 1);
   auto tile_parts = [&](int ni, int l) {
     if (l == 0 && split) return gsum_on ? 1 : ni == NET_PI ? wc : 2;
-    return Bp > 1024 ? std::min(4, (Bp + 1023) / 1024) : 1;
+    return ni == NET_PI ? bpartsD : bpartsB;
   };
   int nB = 0, nD = 0, nhalf = 0;
   for (int ni = NET_PI; ni <= NET_Q2; ++ni)
@@ -650,8 +670,8 @@ static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
           }
       }
     }
-    const int bparts = (split || Bp <= 1024) ? 1 : tile_parts(NET_Q1, 1);  // batch parts of every tile
-    auto order = [&](std::vector<TileDesc>& cons, std::vector<TileDesc>& prod) {
+    const int bpartsQ = (split || Bp <= 1024) ? 1 : bpartsB, bpartsP = (split || Bp <= 1024) ? 1 : bpartsD;
+    auto order = [&](std::vector<TileDesc>& cons, std::vector<TileDesc>& prod, int bparts) {
       std::vector<TileDesc> all = cons;
       all.insert(all.end(), prod.begin(), prod.end());
       int xpart = 0;  // measured 2-6% slower on C3 (B 54.5 -> 57.8 us fp32): opt-in
@@ -664,8 +684,8 @@ static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
       // producer parts first: in-order dispatch starts every producer before its consumer
       cons.insert(cons.begin(), prod.begin(), prod.end());
     };
-    order(e->hostB, halvesB);
-    order(e->hostD, halvesD);
+    order(e->hostB, halvesB, bpartsQ);
+    order(e->hostD, halvesD, bpartsP);
     e->h.nBq[0] = e->h.nBq[1] = 0;
     for (const TileDesc& t : e->hostB) ++e->h.nBq[t.opt - 1];
     {
