@@ -412,6 +412,7 @@ static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
   h.lp_st = (float*)P(lay.take((size_t)2 * Br * 4));
   h.head_st = (float*)P(lay.take((size_t)Br * 4 * A * 4));
   h.lossp = (float*)P(lay.take((size_t)2 * nrt * 4 * 4));
+  h.seedq = (float*)P(lay.take((size_t)2 * Bp * 4));
   h.adam_sc = (float*)P(lay.take(2 * 6 * 4));
   h.alpha_sc = (double*)P(lay.take(2 * 2 * 8));
   h.sync = (uint32_t*)P(lay.take((size_t)(SYNC_FLAGS + HK_COUNT * nrt * 16) * 4));
@@ -636,6 +637,8 @@ static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
             t.nparts = 1;
             t.gsum = 1;
             t.goff = 0;
+            t.seed = nullptr;
+            if (split && esz == 4 && ni != NET_PI && l < 2) t.seed = h.seedq + (size_t)(ni - NET_Q1) * Bp;
             if (l == 0 && split && gsum_on) {  // one block: dY parts [p Bp, (p+1) Bp) summed, X^T [0, Bp)
               t.gsum = ni == NET_PI ? wc : 2;
               t.goff = Bp;
@@ -663,6 +666,7 @@ static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
                 pt.bp = std::min(bpp, total - off);
                 pt.GT = (const char*)t.GT + (size_t)off * esz2;
                 if (!xsame) pt.XT = (const char*)t.XT + (size_t)off * esz2;
+                if (t.seed && !xsame) pt.seed = t.seed + off;
                 (ni == NET_PI ? halvesD : halvesB).push_back(pt);
               }
             }

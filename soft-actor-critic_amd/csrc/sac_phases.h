@@ -106,6 +106,7 @@ struct EngineDev {
   uint32_t* sync;
   float* hand;     // hand-off payloads [HK_COUNT][nrt][SAC_HAND_STRIDE]
   float* stats;
+  float* seedq;    // [2][Bp] fp32 split: each critic row's dL/dq seed, applied by phase B to the unit-seed dY^T
   long long* stamps;  // optional in-kernel timestamps (SAC_STAMPS builds)
   // Next-step batch staging: phase C's stager blocks sample and gather step
   // t+1's rows per row tile into stg (header: step, replay size, replay write
@@ -161,6 +162,10 @@ struct TileDesc {
   // part order, and reduced once against X -- no batch parts, no hand-off
   long goff;
   int gsum, pad_;
+  // fp32 split critics' layers 0 / 1: dY^T holds the unit-seed backward (phase A
+  // stores it before y is known); every batch column b is scaled by seed[b]
+  // while staging, and the bias gradient is summed from the scaled rows here
+  const float* seed;
 };
 
 
@@ -884,6 +889,8 @@ __device__ __forceinline__ void dw_adam_tile(const AS_C EngineDev& E, const Tile
   const int ns = nslot < MAXS ? nslot : MAXS;  // slots per round
   const int rstep = ns * SAC_UPD_BCH;          // batch columns per round
   u32x4 rg[MAXS][GS + 1][PPO];                 // [slot][dY part 0..GS-1, then X][piece]
+  const AS_G float* const seedp = sizeof(T) == 4 ? GPC(float, td.seed) : nullptr;  // uniform
+  f32x4 sdr[sizeof(T) == 4 ? MAXS : 1][PPO];   // the seeds of this thread's dY pieces
   // the operands' bases as separate values: a per-lane choice between two
   // descriptor fields was compiled into a per-lane LOAD of the chosen field and a
   // wait before every piece (the pieces' loads ran one round trip after another)
@@ -906,6 +913,8 @@ __device__ __forceinline__ void dw_adam_tile(const AS_C EngineDev& E, const Tile
           const int row = i / per_row, pc = i % per_row;
           const AS_G T* src = op < GS ? gsrc + op * goff + (size_t)row * ldg : xsrc + (size_t)row * ldx;
           if (i < 32 * per_row) rg[sl][op][pi] = *(const AS_G u32x4*)(src + b0 + pc * EPR);
+          if constexpr (sizeof(T) == 4)
+            if (op == 0 && seedp && i < 32 * per_row) sdr[sl][pi] = *(const AS_G f32x4*)(seedp + b0 + pc * EPR);
         }
     }
   };
@@ -950,7 +959,7 @@ __device__ __forceinline__ void dw_adam_tile(const AS_C EngineDev& E, const Tile
   for (int j = 0; j < BPT; ++j) {
     const int t = tid + j * UT, bn = t >> 4, bs = t & 15;
     bsum[j] = 0.f;
-    if (do_bias && t < 512 && td.n0 + bn < td.N) {
+    if (do_bias && !seedp && t < 512 && td.n0 + bn < td.N) {
       const AS_G float* dbp = GPC(float, td.dbp) + td.n0 + bn;
       for (int rt0 = bs; rt0 < td.nrt; rt0 += 16 * BU) {
         float pv[BU];
@@ -1000,11 +1009,21 @@ __device__ __forceinline__ void dw_adam_tile(const AS_C EngineDev& E, const Tile
                 for (int q = 1; q < GS; ++q) a += __builtin_bit_cast(f32x4, rg[sl][q][pi]);
                 v = __builtin_bit_cast(u32x4, a);
               }
+            if constexpr (sizeof(T) == 4)
+              if (op == 0 && seedp) v = __builtin_bit_cast(u32x4, __builtin_bit_cast(f32x4, v) * sdr[sl][pi]);
             if (i < 32 * per_row) *(AS_L u32x4*)(stage + sl * slot_el + row * lds_row + pc * EPR) = v;
           }
         issue(r0 + rstep, slc);
         __syncthreads();
         if (r0 == 0 && sl == 0) STAMP(polyak ? 51 : 55);
+        if (seedp && do_bias) {  // bias gradient: this lane's columns of the slot's scaled dY rows
+#pragma unroll
+          for (int j = 0; j < BPT; ++j) {
+            const int t = tid + j * UT, bn = t >> 4, bs = t & 15;
+            if (t < 512)
+              for (int c = bs; c < bch; c += 16) bsum[j] += (float)stage[sl * slot_el + bn * lds_row + c];
+          }
+        }
 #pragma unroll
         for (int j = 0; j < PPW; ++j) {
           const int pr = wave + j * NWV, kq = pr >> 2;

@@ -612,6 +612,13 @@ __device__ __forceinline__ void target_critic_split_body(const EngineDev* __rest
       __syncthreads();
     }
     STAMP(16);
+    if constexpr (sizeof(T) == 4) {
+      // fp32: layers 1 and 0's unit-seed dY^T stored now, while y is still on its
+      // way; phase B scales each batch column by its row's seed (E.seedq) as it
+      // stages them, and sums their bias gradients itself
+      store_T<T, R>(U1, ldu1, HH, HH, (T*)L1.GT + (size_t)h * HH * Bp, Bp, r0, nvalid, nullptr);
+      store_T<T, R>(Xb, ld, L0.Np, L0.N, L0.GT, 2 * Bp, h * Bp + r0, nvalid, nullptr);
+    }
     if (tid < 64) {  // wave 0: q, y, loss partial, seed dL/dq = 2(q - y)/B  (mse_loss backward)
       float sq = 0.f;
       if (tid < R) {
@@ -645,6 +652,7 @@ __device__ __forceinline__ void target_critic_split_body(const EngineDev* __rest
         float seed = v ? (2.0f / (float)B) * d : 0.f;
         if (net.out_act != ACT_ID) seed = act_bwd(net.out_act, qpre, seed);
         qtB[tid] = seed;
+        if (sizeof(T) == 4 && h == 0) GP(float, E.seedq)[qi * Bp + b] = seed;
       }
       sq = wave_sum(sq);
       if (tid == 0 && h == 0) GP(float, E.lossp)[(par * E.nrt + rbi) * 4 + qi] = sq;
@@ -658,8 +666,10 @@ __device__ __forceinline__ void target_critic_split_body(const EngineDev* __rest
       __syncthreads();
       store_T<T, R>(g2, ldo, L2.Np, L2.N, L2.GT, Bp, r0, nvalid, L2.dbp, qtB);
     }
-    store_T<T, R>(U1, ldu1, HH, HH, (T*)L1.GT + (size_t)h * HH * Bp, Bp, r0, nvalid, L1.dbp + h * HH, qtB, L1.N);
-    store_T<T, R>(Xb, ld, L0.Np, L0.N, L0.GT, 2 * Bp, h * Bp + r0, nvalid, L0.dbp, qtB);
+    if constexpr (sizeof(T) == 2) {
+      store_T<T, R>(U1, ldu1, HH, HH, (T*)L1.GT + (size_t)h * HH * Bp, Bp, r0, nvalid, L1.dbp + h * HH, qtB, L1.N);
+      store_T<T, R>(Xb, ld, L0.Np, L0.N, L0.GT, 2 * Bp, h * Bp + r0, nvalid, L0.dbp, qtB);
+    }
     STAMP(11 + 2 * qi);
   }
 }
