@@ -432,9 +432,10 @@ static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
   // 1024 fp32 columns = 256 KB of dY^T / X^T in ~12 us), so at C3 (160 critic
   // tiles, 80 policy tiles) P = 3: 480 blocks (2 rounds) for B and 240 (one) for D.
   // fp32 hidden-split layer 0: the parts' partial dY summed while staging in one
-  // block (TileDesc.gsum; SAC_GSUM=0: batch parts with a granule hand-off)
-  int gsum_on = esz == 4;
-  if (const char* v = getenv("SAC_GSUM")) gsum_on = gsum_on && atoi(v) != 0;
+  // block (TileDesc.gsum), which also sees every batch column of the tile -- the
+  // seeded bias sums of TileDesc.seed rely on that; bf16: a block per dY part
+  // with a granule hand-off to part 1
+  const bool gsum_on = esz == 4;
   int tilesBD[2] = {0, 0};  // [critics (B), policy (D)]
   for (int ni = NET_PI; ni <= NET_Q2; ++ni)
     for (int l = 0; l < h.net[ni].L; ++l)

@@ -77,6 +77,15 @@ def test_engine_matches_oracle(name, precision):
             assert abs(la - st.log_alpha) <= (1e-7 if precision == "fp32" else 1e-5), (la, st.log_alpha)
 
 
+@pytest.mark.parametrize("precision,parts", [("fp32", "4"), ("bf16", "2")])
+def test_c3_batch_part_counts_match_oracle(precision, parts, monkeypatch):
+    """C3's update tiles with a batch-part count other than the cost model's
+    choice (3; SAC_BPARTS overrides it): 4 parts (the round-2 layout before the
+    model) and 2, against the oracle like test_baseline_config_matches_oracle."""
+    monkeypatch.setenv("SAC_BPARTS", parts)
+    test_baseline_config_matches_oracle("c3", 12_288, 2, precision)
+
+
 @pytest.mark.parametrize("name", ["c1_auto", "c2"])
 def test_engine_matches_reference_golden_directly(name):
     """Step 1 against the reference's own captured outputs (no oracle in between)."""
