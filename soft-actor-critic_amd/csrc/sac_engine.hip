@@ -1084,7 +1084,7 @@ static int gather_rpw(int batch) {
   static const int env = [] {
     const char* v = getenv("SAC_GATHER_RPW");
     const int x = v ? atoi(v) : 0;
-    return (x == 16 || x == 32 || x == 64) ? x : 0;
+    return (x == 4 || x == 8 || x == 16 || x == 32 || x == 64) ? x : 0;
   }();
   (void)batch;
   return env ? env : 16;
