@@ -1388,6 +1388,28 @@ __device__ __forceinline__ void gran_issue(const AS_G uint64_t* const (&g)[N], u
 #pragma unroll
   for (int i = 0; i < N; ++i) x[i] = __hip_atomic_load((uint64_t*)g[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+// one poll in flight (register-lean: N granules need 2N VGPRs, not 4N)
+template <int N>
+__device__ __forceinline__ void gran_getn1(const AS_C EngineDev& E, const AS_G uint64_t* const (&g)[N], uint32_t ep,
+                                           float (&out)[N]) {
+  uint64_t x[N];
+  for (int it = 0;; ++it) {
+#pragma unroll
+    for (int i = 0; i < N; ++i) x[i] = __hip_atomic_load((uint64_t*)g[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    bool all = true;
+#pragma unroll
+    for (int i = 0; i < N; ++i) all = all && (uint32_t)(x[i] >> 32) == ep;
+    if (all) break;
+    if (it > E.spin_limit) {
+      __hip_atomic_store((uint32_t*)GP(uint32_t, E.sync) + SYNC_TIMEOUT, 1u, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+      break;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+#pragma unroll
+  for (int i = 0; i < N; ++i) out[i] = __uint_as_float((uint32_t)x[i]);
+}
 template <int N>
 __device__ __forceinline__ void gran_getn(const AS_C EngineDev& E, const AS_G uint64_t* const (&g)[N], uint32_t ep,
                                           float (&out)[N]) {
@@ -1422,23 +1444,7 @@ __device__ __forceinline__ void gran_getn(const AS_C EngineDev& E, const AS_G ui
     gran_issue<N>(g, y);
   }
 #else
-  uint64_t x[N];
-  for (int it = 0;; ++it) {
-#pragma unroll
-    for (int i = 0; i < N; ++i) x[i] = __hip_atomic_load((uint64_t*)g[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    bool all = true;
-#pragma unroll
-    for (int i = 0; i < N; ++i) all = all && (uint32_t)(x[i] >> 32) == ep;
-    if (all) break;
-    if (it > E.spin_limit) {
-      __hip_atomic_store((uint32_t*)GP(uint32_t, E.sync) + SYNC_TIMEOUT, 1u, __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);
-      break;
-    }
-    __builtin_amdgcn_s_sleep(1);
-  }
-#pragma unroll
-  for (int i = 0; i < N; ++i) out[i] = __uint_as_float((uint32_t)x[i]);
+  gran_getn1<N>(E, g, ep, out);
 #endif
 }
 

@@ -179,24 +179,71 @@ __device__ __forceinline__ void gemm_hs(const lf* __restrict__ A, int lda, const
 // Small-N steps (NT <= 2 output tiles, long reduction): the reduction is
 // split over the waves (SAC_NW / NT waves per tile, consecutive chunk slices),
 // partial tiles summed through LDS in slice order.  out[r][col] for col < 16 NT.
+// A wave's slice of a k-split step held in registers: a step that follows a
+// hand-off (the target critics' and pi(s')'s layer 2) issues its fragment
+// before the poll instead of one more memory round trip after it.  Held when
+// the slice is one chunk (bf16: a 128-deep reduction over 8 waves); longer
+// slices stream as before.  Same-box A/B at C2: bf16 +2.7% steps/s; holding
+// fp32's 4-chunk slices measured 1-2% slower (phase A), so fp32 streams.
+#ifndef SAC_KS_HELD
+#define SAC_KS_HELD 1
+#endif
+template <typename T>
+struct KsHeld {
+  static constexpr int MAXC = 1;
+  typename MM<T>::Frag f[MAXC];
+  bool ok;
+};
+template <typename T>
+__device__ __forceinline__ void ks_slice(const GemmW& w, int& t, int& c0, int& c1, int& wpt) {
+  const int wave = wave_id();
+  const int NT = w.NT;  // 1 or 2
+  wpt = SAC_NW / NT;
+  t = wave % NT;
+  const int sl = wave / NT;
+  const int nch = w.cols / MM<T>::KC;
+  const int per = (nch + wpt - 1) / wpt;
+  c0 = sl * per;
+  c1 = c0 + per < nch ? c0 + per : nch;
+}
+template <typename T, bool COH = false>
+__device__ __forceinline__ void ks_issue(KsHeld<T>& kh, const GemmW& w) {
+  constexpr uint32_t FSB = 64 * MM<T>::KL * sizeof(T);
+  int t, c0, c1, wpt;
+  ks_slice<T>(w, t, c0, c1, wpt);
+  const int nch = w.cols / MM<T>::KC, per = (nch + wpt - 1) / wpt;
+  kh.ok = SAC_KS_HELD && per <= KsHeld<T>::MAXC;  // uniform
+  if (!kh.ok) return;
+  const __amdgpu_buffer_rsrc_t rs = coh_rsrc(w.p, 0xFFFFFFF0u);
+  const uint32_t o = (uint32_t)(((size_t)t * 16 * w.tcols + (threadIdx.x & 63) * MM<T>::KL) * sizeof(T));
+  static_for<KsHeld<T>::MAXC>([&](auto uc) {
+    constexpr int u = decltype(uc)::value;
+    if (c0 + u < c1) kh.f[u] = coh_frag<T, COH>(rs, o + (c0 + u) * FSB);
+  });
+}
+
 template <typename T, bool COH = false>
 __device__ __forceinline__ void gemm_ksplit(const lf* __restrict__ A, int lda, const GemmW& w, lf* red, lf* out,
-                                            int ldo) {
+                                            int ldo, const KsHeld<T>* kh = nullptr) {
   typedef typename MM<T>::Frag F;
   constexpr int KC = MM<T>::KC, KL = MM<T>::KL;
   constexpr uint32_t FSB = 64 * KL * sizeof(T);
   const int lane = threadIdx.x & 63, wave = wave_id();
   const int c = lane & 15, g = lane >> 4;
   const int NT = w.NT;  // 1 or 2
-  const int wpt = SAC_NW / NT;
-  const int t = wave % NT, sl = wave / NT;
-  const int nch = w.cols / KC;
-  const int per = (nch + wpt - 1) / wpt;
-  const int c0 = sl * per, c1 = c0 + per < nch ? c0 + per : nch;
+  int t, c0, c1, wpt;
+  ks_slice<T>(w, t, c0, c1, wpt);
   const __amdgpu_buffer_rsrc_t rs = coh_rsrc(w.p, 0xFFFFFFF0u);
   const uint32_t o = (uint32_t)(((size_t)t * 16 * w.tcols + lane * KL) * sizeof(T));
   const lf* arow = A + c * lda + g * KL;
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  if (kh && kh->ok) {  // uniform: the slice's fragments are already in registers
+    static_for<KsHeld<T>::MAXC>([&](auto uc) {
+      constexpr int u = decltype(uc)::value;
+      if (c0 + u < c1) MM<T>::mma(acc, MM<T>::from_lds(arow + (c0 + u) * KC), kh->f[u]);
+    });
+    c1 = c0;  // nothing left to stream
+  }
   for (int cb = c0; cb < c1; cb += 4) {
     const int rem = c1 - cb < 4 ? c1 - cb : 4;
     F f[4], a[4];
@@ -365,6 +412,12 @@ __device__ __forceinline__ void target_critic_split_body(const EngineDev* __rest
              hdr[3] == (uint64_t)(uintptr_t)rb.obs && hdr[4] == (uint64_t)GPC(int64_t, rb.state)[2];
   }
   if (!h1_issued) ht_issue<T, 1, NCH_H>(h1, w1);
+  // layer 2's k-split slice (layer 2 runs after the hand-off for the target
+  // critics, and at the end of pi(s')'s chain): held from here
+  GemmW w2n = gw_sub<T>(L2.Wc, L2.Kp, 0, L2.Np, h * HHr, HHr, nullptr, 0);
+  w2n.NT = (L2.N + 15) >> 4;  // output tiles that hold data
+  KsHeld<T> kh2;
+  ks_issue<T>(kh2, w2n);
   if (staged && rbi == 0 && role == 0 && h == 0 && tid == 0)
     *(AS_G uint64_t*)(GP(uint32_t, E.sync) + 4) = step;  // SYNC_STAGED (tests)
   if (!staged) {  // uniform
@@ -518,10 +571,7 @@ __device__ __forceinline__ void target_critic_split_body(const EngineDev* __rest
                     nvalid, nullptr);
     STAMP(3);
     // layer 2, this half's partial sum: outB [R][Np2]
-    const GemmW w2 = gw_sub<T>(L2.Wc, L2.Kp, 0, L2.Np, h * HHr, HHr, nullptr, 0);
-    GemmW w2n = w2;
-    w2n.NT = (L2.N + 15) >> 4;  // output tiles that hold data
-    gemm_ksplit<T>(H1, ldh1, w2n, red, outB, ldo);
+    gemm_ksplit<T>(H1, ldh1, w2n, red, outB, ldo, &kh2);
     STAMP(4);
   };
 
@@ -860,6 +910,63 @@ __device__ __forceinline__ void actor_split_body(const EngineDev* __restrict__ E
     c1p[p] = gs_at(E, GS_C1, rbi, p);
     c2p[p] = gs_at(E, GS_C2, rbi, p);
   }
+  if (R * A <= 64) {  // uniform: wave 0 holds every (row, action dim) lane
+    // ONE poll for everything this block takes from the critics: lane i = (r, j)
+    // polls the da partials of (r, j) and lanes < R also the q partials of row
+    // tid (lanes >= R re-poll row 0's: harmless), so the da values arrive with
+    // the q values instead of one more round trip after them.  Row r's min-Q
+    // weights then come from lane r by a cross-lane read.
+    if (tid < 64) {
+      const bool live = tid < R * A;
+      const int i = live ? tid : 0, r = i / A, rq = tid < R ? tid : 0;
+      const AS_G uint64_t* gg[4 * W];
+#pragma unroll
+      for (int p = 0; p < W; ++p) {
+        gg[p] = c1p[p] + i;
+        gg[W + p] = c2p[p] + i;
+        gg[2 * W + p] = c1p[p] + R * A + rq;
+        gg[3 * W + p] = c2p[p] + R * A + rq;
+      }
+      float gv[4 * W];
+      gran_getn1<4 * W>(E, gg, ep, gv);
+      float term = 0.f, w1 = 0.f, w2 = 0.f;
+      if (tid < R) {
+        const bool v = tid < nvalid;
+        const AS_C NetDev& q1n = E.net[NET_Q1];
+        const AS_C NetDev& q2n = E.net[NET_Q2];
+        float q1p = gv[2 * W], q2p = gv[3 * W];
+#pragma unroll
+        for (int p = 1; p < W; ++p) {
+          q1p += gv[2 * W + p];
+          q2p += gv[3 * W + p];
+        }
+        q1p += bq1;
+        q2p += bq2;
+        const float q1 = q1n.out_act == ACT_ID ? q1p : act_fwd(q1n.out_act, q1p);
+        const float q2 = q2n.out_act == ACT_ID ? q2p : act_fwd(q2n.out_act, q2p);
+        const float m = fmin_nan(q1, q2);
+        term = v ? alpha32 * lpB[tid] - m : 0.f;
+        const float gm = v ? -1.0f / (float)B : 0.f;
+        w1 = (q1 == q2) ? gm * 0.5f : (q1 > q2 ? 0.f : gm);
+        w2 = (q1 == q2) ? gm * 0.5f : (q1 < q2 ? 0.f : gm);
+        if (q1n.out_act != ACT_ID) w1 = act_bwd(q1n.out_act, q1p, w1);
+        if (q2n.out_act != ACT_ID) w2 = act_bwd(q2n.out_act, q2p, w2);
+      }
+      term = wave_sum(term);
+      if (tid == 0 && h == 0) GP(float, E.lossp)[(par * E.nrt + rbi) * 4 + 2] = term;
+      const float w1r = __shfl(w1, r, 64), w2r = __shfl(w2, r, 64);
+      if (live) {
+        float da1 = gv[0], da2 = gv[W];
+#pragma unroll
+        for (int p = 1; p < W; ++p) {
+          da1 += gv[p];
+          da2 += gv[W + p];
+        }
+        gaB[i] = w1r * da1 + w2r * da2;
+      }
+    }
+    __syncthreads();
+  } else {
   if (tid < 64) {
     float term = 0.f;
     if (tid < R) {
@@ -917,6 +1024,7 @@ __device__ __forceinline__ void actor_split_body(const EngineDev* __restrict__ E
     gaB[i] = g1B[r] * da1 + g2B[r] * da2;
   }
   __syncthreads();
+  }
   STAMP(39);
   // squashed-Gaussian head backward (models.py:79-87), one lane per (row, action dim)
   static_assert(SAC_ROWS * 32 <= SAC_THREADS, "one (row, action dim) per thread");
