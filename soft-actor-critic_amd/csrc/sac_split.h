@@ -182,15 +182,24 @@ __device__ __forceinline__ void gemm_hs(const lf* __restrict__ A, int lda, const
 // A wave's slice of a k-split step held in registers: a step that follows a
 // hand-off (the target critics' and pi(s')'s layer 2) issues its fragment
 // before the poll instead of one more memory round trip after it.  Held when
-// the slice is one chunk (bf16: a 128-deep reduction over 8 waves); longer
-// slices stream as before.  Same-box A/B at C2: bf16 +2.7% steps/s; holding
-// fp32's 4-chunk slices measured 1-2% slower (phase A), so fp32 streams.
+// the slice is at most SAC_KS_MAXC32 chunks in fp32 / one chunk in bf16 (a
+// 128-deep reduction over 8 waves).  Same-box A/Bs at C2
+// (profiles/r02_ab_*.txt): bf16 +2.7% steps/s; fp32 phase A with 2- or 4-chunk
+// slices held (issued under layer 1 / before the poll): no change, so fp32
+// streams (MAXC32 = 1); phase C critics' two k-split steps held (SAC_KS_C=1):
+// C 18.4 -> 19.8 us in fp32 wherever they are issued, so off.
 #ifndef SAC_KS_HELD
 #define SAC_KS_HELD 1
 #endif
-template <typename T>
+#ifndef SAC_KS_MAXC32
+#define SAC_KS_MAXC32 1
+#endif
+#ifndef SAC_KS_C
+#define SAC_KS_C 0
+#endif
+template <typename T, int MC = (sizeof(T) == 4 ? SAC_KS_MAXC32 : 1)>
 struct KsHeld {
-  static constexpr int MAXC = 1;
+  static constexpr int MAXC = MC;
   typename MM<T>::Frag f[MAXC];
   bool ok;
 };
@@ -206,25 +215,25 @@ __device__ __forceinline__ void ks_slice(const GemmW& w, int& t, int& c0, int& c
   c0 = sl * per;
   c1 = c0 + per < nch ? c0 + per : nch;
 }
-template <typename T, bool COH = false>
-__device__ __forceinline__ void ks_issue(KsHeld<T>& kh, const GemmW& w) {
+template <typename T, int MC, bool COH = false>
+__device__ __forceinline__ void ks_issue(KsHeld<T, MC>& kh, const GemmW& w) {
   constexpr uint32_t FSB = 64 * MM<T>::KL * sizeof(T);
   int t, c0, c1, wpt;
   ks_slice<T>(w, t, c0, c1, wpt);
   const int nch = w.cols / MM<T>::KC, per = (nch + wpt - 1) / wpt;
-  kh.ok = SAC_KS_HELD && per <= KsHeld<T>::MAXC;  // uniform
+  kh.ok = SAC_KS_HELD && per <= MC;  // uniform
   if (!kh.ok) return;
   const __amdgpu_buffer_rsrc_t rs = coh_rsrc(w.p, 0xFFFFFFF0u);
   const uint32_t o = (uint32_t)(((size_t)t * 16 * w.tcols + (threadIdx.x & 63) * MM<T>::KL) * sizeof(T));
-  static_for<KsHeld<T>::MAXC>([&](auto uc) {
+  static_for<MC>([&](auto uc) {
     constexpr int u = decltype(uc)::value;
     if (c0 + u < c1) kh.f[u] = coh_frag<T, COH>(rs, o + (c0 + u) * FSB);
   });
 }
 
-template <typename T, bool COH = false>
+template <typename T, bool COH = false, int MC = 1>
 __device__ __forceinline__ void gemm_ksplit(const lf* __restrict__ A, int lda, const GemmW& w, lf* red, lf* out,
-                                            int ldo, const KsHeld<T>* kh = nullptr) {
+                                            int ldo, const KsHeld<T, MC>* kh = nullptr) {
   typedef typename MM<T>::Frag F;
   constexpr int KC = MM<T>::KC, KL = MM<T>::KL;
   constexpr uint32_t FSB = 64 * KL * sizeof(T);
@@ -238,7 +247,7 @@ __device__ __forceinline__ void gemm_ksplit(const lf* __restrict__ A, int lda, c
   const lf* arow = A + c * lda + g * KL;
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
   if (kh && kh->ok) {  // uniform: the slice's fragments are already in registers
-    static_for<KsHeld<T>::MAXC>([&](auto uc) {
+    static_for<MC>([&](auto uc) {
       constexpr int u = decltype(uc)::value;
       if (c0 + u < c1) MM<T>::mma(acc, MM<T>::from_lds(arow + (c0 + u) * KC), kh->f[u]);
     });
@@ -417,7 +426,8 @@ __device__ __forceinline__ void target_critic_split_body(const EngineDev* __rest
   GemmW w2n = gw_sub<T>(L2.Wc, L2.Kp, 0, L2.Np, h * HHr, HHr, nullptr, 0);
   w2n.NT = (L2.N + 15) >> 4;  // output tiles that hold data
   KsHeld<T> kh2;
-  ks_issue<T>(kh2, w2n);
+  kh2.ok = false;
+  if (sizeof(T) == 2) ks_issue<T>(kh2, w2n);  // bf16: one fragment, from the start
   if (staged && rbi == 0 && role == 0 && h == 0 && tid == 0)
     *(AS_G uint64_t*)(GP(uint32_t, E.sync) + 4) = step;  // SYNC_STAGED (tests)
   if (!staged) {  // uniform
@@ -548,6 +558,7 @@ __device__ __forceinline__ void target_critic_split_body(const EngineDev* __rest
     if (stXT && h == 0)
       store_T<T, R>(H0, ld, L1.Kp, L1.K, (T*)L1.XT + (pi_actor ? par * L1.xt_par : 0), Bp, r0, nvalid, nullptr);
     STAMP(2);
+    if (sizeof(T) == 4 && !kh2.ok) ks_issue<T>(kh2, w2n);  // fp32: under layer 1 (target critics: before the poll)
     // layer 1, this half: H0 -> P1 / H1 [R][HH]
     gemm_hs<T, 1, NCH_H>(H0, ld, w1, &h1, [&](int j, int col, const f32x4& acc) {
       const float bn = h1.b[j];
@@ -571,7 +582,7 @@ __device__ __forceinline__ void target_critic_split_body(const EngineDev* __rest
                     nvalid, nullptr);
     STAMP(3);
     // layer 2, this half's partial sum: outB [R][Np2]
-    gemm_ksplit<T>(H1, ldh1, w2n, red, outB, ldo, &kh2);
+    gemm_ksplit<T, false, decltype(kh2)::MAXC>(H1, ldh1, w2n, red, outB, ldo, &kh2);
     STAMP(4);
   };
 
@@ -613,6 +624,7 @@ __device__ __forceinline__ void target_critic_split_body(const EngineDev* __rest
   } else if (role == 1 || role == 2) {
     // ---- target critic t (agent.py:195-211): a~', log pi' from pi(s')'s two partials
     const int t = role - 1;
+    if (sizeof(T) == 4) ks_issue<T>(kh2, w2n);
     head(gs_at(E, GS_PI, rbi, 0), nullptr, true, a2B, lpB, false);
     if (t == 0 && h == 0 && tid < R) gran_put(gs_at(E, GS_LP, rbi, 0) + tid, lpB[tid], ep);
     STAMP(7);
@@ -794,11 +806,26 @@ __device__ __forceinline__ void actor_split_body(const EngineDev* __restrict__ E
     const GemmW wt1 = gw_sub<T>(L1.WTc, L1.Np, 0, L1.Kp, h * HH, HH, nullptr, 0);
     HTiles<T, 2, NCH_HH> ht1;
     ht_issue<T, 2, NCH_HH>(ht1, wt1);
+    // the two k-split steps of the critic's chain (layer 2's partial q, then
+    // layer 0's dX for the action columns) read weights phase B has just
+    // written: held (issued behind the inputs), not a cold round trip each
+    // after layer 1 / after dY0 (SAC_KS_C=0: streamed)
+    GemmW w2 = gw_sub<T>(L2.Wc, L2.Kp, 0, L2.Np, h * HH, HH, nullptr, 0);
+    w2.NT = (L2.N + 15) >> 4;
+    const int k0 = (O >> 4) << 4, k1 = (O + A + 15) >> 4 << 4;
+    GemmW wt0 = gw_sub<T>(L0.WTc, L0.Np, k0, k1 - k0, 0, L0.Np, nullptr, 0);
+    KsHeld<T, sizeof(T) == 4 ? 2 : 1> kc2;
+    KsHeld<T, sizeof(T) == 4 ? 8 : 1> kc0;
+    kc2.ok = kc0.ok = false;
     // the W2 (fp32 master) element of this thread's column n = tid % HH of the unit-seed backward
     static_assert(SAC_THREADS % HH == 0, "one W2 column per thread in the unit-seed loop");
     const float w2n = GPC(float, net.P + L2.w_off)[h * HH + tid % HH];
     for (int i = tid; i < R * O; i += SAC_THREADS) sB[i] = GPC(float, E.s_st)[(size_t)r0 * O + i];
     for (int i = tid; i < R * A; i += SAC_THREADS) aB[i] = GPC(float, E.a_st)[(size_t)r0 * A + i];
+    if (SAC_KS_C) {  // behind the inputs: waiting for s / a~ must not wait for these (loads retire in order)
+      ks_issue<T>(kc2, w2);
+      ks_issue<T>(kc0, wt0);
+    }
     __syncthreads();
     const int Kp0 = L0.Kp;
     for (int i = tid; i < R * Kp0; i += SAC_THREADS) {
@@ -833,11 +860,7 @@ __device__ __forceinline__ void actor_split_body(const EngineDev* __restrict__ E
     });
     if (act != ACT_RELU && act != ACT_ID) act_pass_fwd<R>(H1, ldh1, HH >> 4, act);
     __syncthreads();
-    {
-      GemmW w2 = gw_sub<T>(L2.Wc, L2.Kp, 0, L2.Np, h * HH, HH, nullptr, 0);
-      w2.NT = (L2.N + 15) >> 4;
-      gemm_ksplit<T>(H1, ldh1, w2, red, outB, ldo);  // partial q
-    }
+    gemm_ksplit<T, false, decltype(kc2)::MAXC>(H1, ldh1, w2, red, outB, ldo, &kc2);  // partial q
     STAMP(36 + qi);
     // unit-seed backward down to a~ (the pi role applies the min-Q weights and act'(q))
     {
@@ -859,9 +882,7 @@ __device__ __forceinline__ void actor_split_body(const EngineDev* __restrict__ E
       if (act != ACT_RELU && act != ACT_ID) act_pass_bwd<R>(Xb, ld, P0, ldp0, L1.Kp >> 4, L1.K, act);
       __syncthreads();
       // dX of layer 0 for the action columns: the 16-row tiles of W0^T holding [O, O + A)
-      const int k0 = (O >> 4) << 4, k1 = (O + A + 15) >> 4 << 4;
-      GemmW wt0 = gw_sub<T>(L0.WTc, L0.Np, k0, k1 - k0, 0, L0.Np, nullptr, 0);
-      gemm_ksplit<T>(Xb, ld, wt0, red, H0, ld);  // H0 [R][k1 - k0]: partial dX0
+      gemm_ksplit<T, false, decltype(kc0)::MAXC>(Xb, ld, wt0, red, H0, ld, &kc0);  // H0 [R][k1 - k0]: partial dX0
       AS_G uint64_t* g = gs_at(E, GS_C1 + qi, rbi, h);
       for (int i = tid; i < R * A; i += SAC_THREADS) gran_put(g + i, H0[(i / A) * ld + (O - k0) + i % A], ep);
       if (tid < R) gran_put(g + R * A + tid, outB[tid * ldo], ep);
