@@ -186,8 +186,10 @@ __device__ __forceinline__ void gemm_hs(const lf* __restrict__ A, int lda, const
 // 128-deep reduction over 8 waves).  Same-box A/Bs at C2
 // (profiles/r02_ab_*.txt): bf16 +2.7% steps/s; fp32 phase A with 2- or 4-chunk
 // slices held (issued under layer 1 / before the poll): no change, so fp32
-// streams (MAXC32 = 1); phase C critics' two k-split steps held (SAC_KS_C=1):
-// C 18.4 -> 19.8 us in fp32 wherever they are issued, so off.
+// streams (MAXC32 = 1).  Phase C critics' two k-split steps held (SAC_KS_C):
+// with both issued at launch start the fp32 kernel spilled 28 VGPRs (C 18.4 ->
+// 19.8 us); with W0^T's 8 fp32 chunks issued once layer 1's held part is dead,
+// no spill and C 18.6 -> 18.1 us, +0.8% steps/s fp32, +1.3% bf16.
 #ifndef SAC_KS_HELD
 #define SAC_KS_HELD 1
 #endif
@@ -195,7 +197,7 @@ __device__ __forceinline__ void gemm_hs(const lf* __restrict__ A, int lda, const
 #define SAC_KS_MAXC32 1
 #endif
 #ifndef SAC_KS_C
-#define SAC_KS_C 0
+#define SAC_KS_C 1
 #endif
 template <typename T, int MC = (sizeof(T) == 4 ? SAC_KS_MAXC32 : 1)>
 struct KsHeld {
@@ -824,7 +826,7 @@ __device__ __forceinline__ void actor_split_body(const EngineDev* __restrict__ E
     for (int i = tid; i < R * A; i += SAC_THREADS) aB[i] = GPC(float, E.a_st)[(size_t)r0 * A + i];
     if (SAC_KS_C) {  // behind the inputs: waiting for s / a~ must not wait for these (loads retire in order)
       ks_issue<T>(kc2, w2);
-      ks_issue<T>(kc0, wt0);
+      if (sizeof(T) == 2) ks_issue<T>(kc0, wt0);  // fp32: after layer 1 (its held W1 part is dead then; from here it spilled)
     }
     __syncthreads();
     const int Kp0 = L0.Kp;
@@ -858,6 +860,7 @@ __device__ __forceinline__ void actor_split_body(const EngineDev* __restrict__ E
         H1[r * ldh1 + col] = act == ACT_RELU ? (p > 0.f ? p : 0.f) : p;
       }
     });
+    if (SAC_KS_C && sizeof(T) == 4) ks_issue<T>(kc0, wt0);
     if (act != ACT_RELU && act != ACT_ID) act_pass_fwd<R>(H1, ldh1, HH >> 4, act);
     __syncthreads();
     gemm_ksplit<T, false, decltype(kc2)::MAXC>(H1, ldh1, w2, red, outB, ldo, &kc2);  // partial q
