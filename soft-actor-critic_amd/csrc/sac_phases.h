@@ -1371,10 +1371,11 @@ __device__ __forceinline__ float gran_get(const AS_C EngineDev& E, const AS_G ui
 // one lane: N granules polled together (every load of a poll in flight at once:
 // one round trip once the producers have stored, not N in sequence)
 // Pipelined hand-off polls (gran_getn): the s_sleep between a consumer's two
-// polls in flight; 0 = one poll per round trip.  Same-box A/B, C2 fp32: 8 ->
-// +0.6% steps/s (both interleaved reps), 20 -> -1%.
+// polls in flight; 0 = one poll per round trip.  Same-box A/Bs, C2 fp32: 8 ->
+// +0.6% steps/s over 0 (both interleaved reps), 20 -> -1%; then 4 -> +0.5%
+// over 8, 12 mixed (profiles/r02_ab_poll2.txt, r02_ab_poll_spacing.txt).
 #ifndef SAC_POLL2
-#define SAC_POLL2 8
+#define SAC_POLL2 4
 #endif
 template <int N>
 __device__ __forceinline__ bool gran_ok(const uint64_t (&x)[N], uint32_t ep) {
