@@ -5,9 +5,14 @@
 
 A "step" is one full SAC gradient step (device sample + gather, target, both
 critic updates, actor update, alpha update, Polyak) on a full synthetic 1e6-row
-replay buffer resident in HBM, replayed from hipGraphs.  For N > 1 (torchrun),
-each rank is an independent-seed replica on its own GPU (replicas only: the
-step does not shard); value = total steps of all ranks / max wall time.
+replay buffer resident in HBM, replayed from hipGraphs.  For N > 1 each rank is
+an independent-seed replica on its own GPU (replicas only: the step does not
+shard), training through sac.replicas.replica_train, which all-reduces the
+replica metric vector over RCCL every --aggregate-every steps inside the timed
+region; value = total steps of all ranks / max wall time.  The ranks come
+from torchrun (WORLD_SIZE set; it must equal --gpus) or, when --gpus N > 1 is
+given without it, from this script itself (launch_ranks: one child process
+per GPU, started before anything touches the GPU).
 """
 from __future__ import annotations
 
@@ -299,6 +304,67 @@ def cpu_baseline(cfgname, seconds=5.0):
             "host_threads": nthr, "legs": legs}
 
 
+class _StubEngine:
+    """SAC_BENCH_STUB=1 (tests/test_bench_ranks.py, CPU only): the rank and
+    launcher logic of this file without the HIP engine -- a learner whose
+    graph-replayed steps sleep 20 us (+10 us per rank) on the host and whose
+    state tensors are CPU tensors."""
+
+    fused = 0
+
+    def __init__(self, batch, rank):
+        self.batch, self.rank, self.steps_done = batch, rank, 0
+        self.rng_step = torch.zeros(1, dtype=torch.int64)
+        self.stats = torch.tensor([1.0, 2.0, -0.5, 0.1] + [0.0] * (2 * batch), dtype=torch.float32)
+        self.alpha_state = torch.tensor([-2.3, 0.1, 0.0, 0.0], dtype=torch.float64)
+
+    def train_graph(self, rb, n, chunk):
+        time.sleep(n * (20 + 10 * self.rank) * 1e-6)
+        self.rng_step += n
+        self.steps_done += n
+
+    def check(self):
+        pass
+
+    def losses(self):
+        return self.stats[:4].double().tolist()
+
+
+def launch_ranks(n: int, argv) -> int:
+    """``--gpus N`` (N > 1) without torchrun: start one rank process per GPU
+    (RANK = LOCAL_RANK = r, WORLD_SIZE = N, MASTER_ADDR 127.0.0.1, a free
+    MASTER_PORT), each running this file with the same arguments.  This
+    process never touches the GPU (no torch.cuda call before or after), so the
+    ranks start clean; it waits for them and returns the first non-zero exit
+    status (stopping the other ranks then, so none waits at a barrier for a
+    dead peer), else 0.  Rank 0 prints the JSON line."""
+    import socket
+    import subprocess
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code
+                for q in live:  # our own children, by handle
+                    q.terminate()
+        time.sleep(0.05)
+    return rc
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -308,53 +374,139 @@ def main():
     ap.add_argument("--precision", default="fp32", choices=["bf16", "fp32"],
                     help="headline arithmetic; fp32 is the reference's (bf16 is also timed unless --no-bf16)")
     ap.add_argument("--chunk", type=int, default=64)
+    ap.add_argument("--aggregate-every", type=int, default=1024,
+                    help="replicas (N > 1): gradient steps between the RCCL metric all-reduces (SURVEY §8e)")
     ap.add_argument("--prewarm", type=float, default=0.3,
                     help="seconds of replay gathers before the warm-up steps (device clocks; no SAC step)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-sweep", action="store_true")
     ap.add_argument("--no-bf16", action="store_true")
+    ap.add_argument("--no-c3", action="store_true", help="skip the C3 (B = 4096) legs of the c2 line")
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.gpus < 1:
+        raise SystemExit("--gpus must be >= 1")
+    world_env = os.environ.get("WORLD_SIZE")
+    if world_env is None and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    world = int(world_env or 1)
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world} (torchrun --nproc-per-node must "
+                         f"equal --gpus)")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    device = torch.device("cuda", local)
-    torch.cuda.set_device(device)
+    run_rank(args, world, rank, local)
+
+
+def run_rank(args, world, rank, local):
+    stub = os.environ.get("SAC_BENCH_STUB") == "1"
+    if stub:
+        device = torch.device("cpu")
+        sync = lambda: None  # noqa: E731
+        args.no_sweep = args.no_bf16 = args.no_cpu_baseline = args.no_c3 = True
+    else:
+        device = torch.device("cuda", local)
+        torch.cuda.set_device(device)
+        sync = torch.cuda.synchronize
     dist = None
     if world > 1:
         import torch.distributed as dist
 
-        dist.init_process_group("nccl", device_id=device)
+        if stub:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=device)
 
-    from sac.replicas import aggregate_metrics, replica_seed, timed_region
+    from sac.replicas import replica_seed, replica_train, summarise_aggregates, timed_region
 
     seed = replica_seed(0, rank)
     # graph chunk <= the timed steps, so a short driver run is graph-replayed too
     chunk = max(1, min(args.chunk, args.steps))
+    every = args.aggregate_every
 
-    def timed(precision):
-        eng, rb, c = build_engine(args.config, precision, seed, device)
-        # capture (+ upload) the chunk graph first (runs no step): its host-side work
-        # would otherwise leave the device idle between the warm-up and the timed region
-        eng.train_graph(rb, 0, chunk)
-        prewarm(rb, device, args.prewarm)
-        eng.train_graph(rb, args.warmup, chunk)
-        el = timed_region(lambda: eng.train_graph(rb, args.steps, chunk), torch.cuda.synchronize, device)
+    def timed(precision, cfgname, steps=None, warmup=None):
+        steps = args.steps if steps is None else steps
+        warmup = args.warmup if warmup is None else warmup
+        if stub:
+            c = dict(CONFIGS[cfgname])
+            eng, rb = _StubEngine(c["batch"], rank), None
+        else:
+            eng, rb, c = build_engine(cfgname, precision, seed, device)
+            # capture (+ upload) the chunk graph first (runs no step): its host-side work
+            # would otherwise leave the device idle between the warm-up and the timed region
+            eng.train_graph(rb, 0, chunk)
+            prewarm(rb, device, args.prewarm)
+        eng.train_graph(rb, warmup, chunk)
+        aggs = []
+        if dist:  # replicas: the metric all-reduce every `every` steps runs inside the timed region
+            el = timed_region(lambda: aggs.extend(replica_train(eng, rb, steps, chunk, every)), sync, device)
+        else:
+            el = timed_region(lambda: eng.train_graph(rb, steps, chunk), sync, device)
         eng.check()  # in-launch hand-offs all completed (raises HandoffTimeout otherwise)
         ls = eng.losses()
         if not all(np.isfinite(ls[:3])):
             raise SystemExit(f"non-finite losses after benchmark ({precision}): {ls}")
-        return eng, rb, c, el, ls
+        return eng, rb, c, el, ls, aggs
 
-    eng, rb, c, elapsed, losses = timed(args.precision)
+    eng, rb, c, elapsed, losses, aggs = timed(args.precision, args.config)
     total_steps = args.steps * world
+    replica = summarise_aggregates(aggs, world, every) if dist else None
+    sps = total_steps / elapsed
+    line = {
+        "metric": "SAC gradient steps/sec + replay-sample GB/s, BipedalWalker batch=256",
+        "value": round(sps, 2),
+        "unit": "gradient steps/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 5),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": args.precision,
+        "data": "synthetic (numpy default_rng, SURVEY §8d), random-init reference-seeded weights",
+        "config": {"workload": f"{args.config}: {c['name']} obs={c['obs']} act={c['act']} "
+                               f"2x{c['hidden']} MLPs, buffer={c['capacity']}, batch={c['batch']}, "
+                               f"auto-alpha, device sampler, {args.precision} arithmetic",
+                   "global_batch": c["batch"] * world, "parallelism": f"replicas{world}",
+                   "graph_chunk": chunk, "device_prewarm_s": args.prewarm},
+    }
+    if stub:
+        line["stub"] = "SAC_BENCH_STUB=1: rank/launcher logic only, no engine"
+    else:
+        line.update(measure_phases(args, eng, rb, c, elapsed, sps / world))
+        line["losses_last"] = [round(x, 6) for x in losses]
+    if replica is not None:
+        line["replica_metrics"] = replica
+    if rank == 0 and not stub:
+        if not args.no_sweep:
+            line.update(sweep_fields(rb, c, device))
+        if not args.no_bf16 and args.precision == "fp32" and world == 1:  # single-process leg: no barriers
+            eb, rbb, _, elb, lsb, _ = timed("bf16", args.config)
+            line["value_bf16"] = round(total_steps / elb, 2)
+            line["ms_per_step_bf16"] = round(elb / args.steps * 1e3, 5)
+            line["bf16_parity"] = bf16_deviation(args.config, seed, device)
+            del eb, rbb
+        if not args.no_c3 and args.config == "c2" and world == 1:
+            line.update(c3_legs(args, timed))
+        if world == 1 and not args.no_cpu_baseline:
+            line["cpu_baseline"] = cpu_baseline(args.config)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if dist:
+        dist.destroy_process_group()
 
-    # per-phase device time (hipEvents on the launch stream), then roofline of the dominant kernel
-    # Each interval also holds the cost of the event after it; the timed region
-    # above ran the same launches from hipGraphs with no events.  The per-launch
-    # event cost = (sum of the intervals of one step - the event-free step time)
-    # / launches per step; interval - that cost = the kernel's own duration (the
-    # figure rocprofv3 --kernel-trace reports: profiles/<round>_kernel_stats.csv).
+
+def measure_phases(args, eng, rb, c, elapsed, sps_one):
+    """Per-phase device time (hipEvents on the launch stream) and the roofline
+    of the dominant kernel.  Each interval also holds the cost of the event
+    after it; the timed region ran the same launches from hipGraphs with no
+    events.  The per-launch event cost = (sum of the intervals of one step -
+    the event-free step time) / launches per step; interval - that cost = the
+    kernel's own duration (the figure rocprofv3 --kernel-trace reports:
+    profiles/<round>_kernel_stats*.csv)."""
+    from sac import _engine as E
+
     tp = eng.time_phases(rb, 100)
     phase_ms, empty_ms = tp[:4], tp[4]
     step_ms = elapsed / args.steps * 1e3
@@ -367,94 +519,82 @@ def main():
         if eng.fused == 2:
             flops = [flops[0], 0, flops[2] + flops[1], 0]
     dom = int(np.argmax(phase_ms))
-    from sac import _engine as E
-
     kname = E.load_library().sac_phase_kernel_name(dom).decode()
     traffic, traffic_src = pmc_traffic(kname, args.config, args.precision)
     achieved = flops[dom] / (kern_ms[dom] * 1e-3) / 1e12
     peak = PEAK_TFLOPS[args.precision]
-    replica = None
-    if dist:  # the periodic RCCL metric all-reduce of the replicas, here once per run
-        replica = aggregate_metrics([args.steps, elapsed] + list(losses) + [float(eng.alpha_state[1]), 0.0],
-                                    device=device)
+    W = 2 * c["obs"] + c["act"] + 2
+    return {
+        "replay_sample_GBps_in_step": round(sps_one * c["batch"] * W * 4 / 1e9, 4),
+        "phase_ms": [round(x, 5) for x in kern_ms],
+        "phase_event_interval_ms": [round(x, 5) for x in phase_ms],
+        "event_cost_ms": round(ev_cost, 5),
+        "empty_kernel_event_interval_ms": round(empty_ms, 5),
+        "step_gemm_flops_survey": f_total,
+        "roofline": {"bound": "mfma", "kernel": kname, "achieved": round(achieved, 3), "peak": peak,
+                     "unit": "TFLOP/s", "frac": round(achieved / peak, 5), "traffic": traffic,
+                     "traffic_source": traffic_src, "flops_per_launch": flops[dom],
+                     "avg_launch_ms": round(kern_ms[dom], 5),
+                     "timing": "hipEvents after every launch on the launch stream over 100 steps; "
+                               "avg_launch_ms = mean interval of this kernel's launches minus the per-launch "
+                               "event cost (event intervals of a step - event-free graph step time, per launch)"},
+        "step_roofline": {"achieved_TFLOPs": round(f_total * sps_one / 1e12, 3), "peak": peak,
+                          "frac": round(f_total * sps_one / 1e12 / peak, 5),
+                          "note": "SURVEY F_alg per step x steps/s of one learner"},
+    }
 
-    if rank == 0:
-        sweep = {} if args.no_sweep else gather_sweep(rb, device)
-        sweep_soa = {} if args.no_sweep else gather_sweep(soa_copy(rb), device, sizes=(65536, 1_048_576))
-        W = 2 * c["obs"] + c["act"] + 2
-        sps = total_steps / elapsed
-        line = {
-            "metric": "SAC gradient steps/sec + replay-sample GB/s, BipedalWalker batch=256",
-            "value": round(sps, 2),
-            "unit": "gradient steps/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(elapsed / args.steps * 1e3, 5),
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": args.precision,
-            "data": "synthetic (numpy default_rng, SURVEY §8d), random-init reference-seeded weights",
-            "config": {"workload": f"{args.config}: {c['name']} obs={c['obs']} act={c['act']} "
-                                   f"2x{c['hidden']} MLPs, buffer={c['capacity']}, batch={c['batch']}, "
-                                   f"auto-alpha, device sampler, {args.precision} arithmetic",
-                       "global_batch": c["batch"] * world, "parallelism": f"replicas{world}",
-                       "graph_chunk": chunk, "device_prewarm_s": args.prewarm},
-            "replay_sample_GBps_in_step": round(sps / world * c["batch"] * W * 4 / 1e9, 4),
-            "phase_ms": [round(x, 5) for x in kern_ms],
-            "phase_event_interval_ms": [round(x, 5) for x in phase_ms],
-            "event_cost_ms": round(ev_cost, 5),
-            "empty_kernel_event_interval_ms": round(empty_ms, 5),
-            "step_gemm_flops_survey": f_total,
-            "roofline": {"bound": "mfma", "kernel": kname, "achieved": round(achieved, 3), "peak": peak,
-                         "unit": "TFLOP/s", "frac": round(achieved / peak, 5), "traffic": traffic,
-                         "traffic_source": traffic_src, "flops_per_launch": flops[dom],
-                         "avg_launch_ms": round(kern_ms[dom], 5),
-                         "timing": "hipEvents after every launch on the launch stream over 100 steps; "
-                                   "avg_launch_ms = mean interval of this kernel's launches minus the per-launch "
-                                   "event cost (event intervals of a step - event-free graph step time, per launch)"},
-            "step_roofline": {"achieved_TFLOPs": round(f_total * sps / world / 1e12, 3), "peak": peak,
-                              "frac": round(f_total * sps / world / 1e12 / peak, 5),
-                              "note": "SURVEY F_alg per step x steps/s of one learner"},
-            "losses_last": [round(x, 6) for x in losses],
-        }
-        if sweep:
-            line["replay_sample_GBps_sweep"] = sweep["sample_gather"]
-            line["replay_gather_GBps_sweep"] = sweep["gather"]
-            line["replay_layout"] = f"transition records, row stride {rb.row_stride} floats"
-            line["replay_gather_GBps_sweep_soa_layout"] = sweep_soa["gather"]
-            line["replay_gather_ms_per_launch"] = {"eager": sweep["ms"], "graph": sweep["ms_graph"]}
-            bmax = max(int(b) for b in sweep["gather"])
-            ms = sweep["ms"][f"gather/{bmax}"]
-            gk = ("replay_gather_records_kernel" if rb.layout == "records" and rb.row_stride in (16, 32, 64, 128, 256)
-                  and c["obs"] % 4 == 0 and c["act"] % 4 == 0 else "replay_gather_kernel")
-            gtr, gsrc = pmc_traffic(gk, "gather", "fp32")
-            line["roofline_gather"] = {
-                "bound": "hbm", "kernel": gk, "batch": bmax,
-                "achieved": sweep["gather"][str(bmax)], "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                "frac": round(sweep["gather"][str(bmax)] / PEAK_HBM_GBS, 5), "traffic": gtr,
-                "achieved_read_write": round(2 * sweep["gather"][str(bmax)], 3),
-                "frac_read_write": round(2 * sweep["gather"][str(bmax)] / PEAK_HBM_GBS, 5),
-                "traffic_source": gsrc, "bytes_per_launch": bmax * W * 4, "avg_launch_ms": ms,
-                "note": "B_gather = 4 B (2 obs + act + 2) bytes read per launch (SURVEY §8d); the kernel writes "
-                        "as many again (the minibatch it returns), counted in achieved_read_write; traffic = PMC "
-                        "FETCH (x2, gfx950) + WRITE per launch: reads exceed B_gather by the record padding "
-                        "(2O+A+2 floats stored in whole 128-B lines); rows uniform with replacement over the "
-                        "1e6-row buffer"}
-        if not args.no_bf16 and args.precision == "fp32" and world == 1:  # single-process leg: no barriers
-            eb, rbb, _, elb, lsb = timed("bf16")
-            line["value_bf16"] = round(total_steps / elb, 2)
-            line["ms_per_step_bf16"] = round(elb / args.steps * 1e3, 5)
-            line["bf16_parity"] = bf16_deviation(args.config, seed, device)
-            del eb, rbb
-        if replica is not None:
-            line["replica_metrics"] = replica
-        if world == 1 and not args.no_cpu_baseline:
-            line["cpu_baseline"] = cpu_baseline(args.config)
-        print(json.dumps(line), flush=True)
-    if dist:
-        dist.destroy_process_group()
+
+def c3_legs(args, timed):
+    """C3 (BASELINE configs[2]: B = 4096, the MFMA-bound regime) on the same
+    line, so the driver times it: fp32 and bf16 steps/s, graph-replayed like
+    the headline, with the step's fraction of the dtype's dense MFMA peak
+    (SURVEY F_alg per step x steps/s).  C3 steps are ~4-8x longer than C2's,
+    so the timed steps are scaled down (at least 20) to keep the run short."""
+    out = {}
+    steps, warmup = max(20, args.steps // 8), max(5, args.warmup // 8)
+    f_total = gemm_flops(24, 4, [256, 256], 4096)[1]
+    for prec in ("fp32", "bf16"):
+        eng, rb, c, el, ls, _ = timed(prec, "c3", steps, warmup)
+        sps = steps / el
+        key = "value_c3" if prec == "fp32" else "value_c3_bf16"
+        out[key] = round(sps, 2)
+        out[key + "_detail"] = {"steps": steps, "ms_per_step": round(el / steps * 1e3, 5),
+                                "mfma_frac": round(f_total * sps / 1e12 / PEAK_TFLOPS[prec], 5),
+                                "peak_TFLOPs": PEAK_TFLOPS[prec], "losses_last": [round(x, 6) for x in ls]}
+        del eng, rb
+        torch.cuda.empty_cache()
+    return out
+
+
+def sweep_fields(rb, c, device):
+    sweep = gather_sweep(rb, device)
+    sweep_soa = gather_sweep(soa_copy(rb), device, sizes=(65536, 1_048_576))
+    W = 2 * c["obs"] + c["act"] + 2
+    line = {}
+    line["replay_sample_GBps_sweep"] = sweep["sample_gather"]
+    line["replay_gather_GBps_sweep"] = sweep["gather"]
+    line["replay_layout"] = f"transition records, row stride {rb.row_stride} floats"
+    line["replay_gather_GBps_sweep_soa_layout"] = sweep_soa["gather"]
+    line["replay_gather_ms_per_launch"] = {"eager": sweep["ms"], "graph": sweep["ms_graph"]}
+    bmax = max(int(b) for b in sweep["gather"])
+    ms = sweep["ms"][f"gather/{bmax}"]
+    gk = ("replay_gather_records_kernel" if rb.layout == "records" and rb.row_stride in (16, 32, 64, 128, 256)
+          and c["obs"] % 4 == 0 and c["act"] % 4 == 0 else "replay_gather_kernel")
+    gtr, gsrc = pmc_traffic(gk, "gather", "fp32")
+    line["roofline_gather"] = {
+        "bound": "hbm", "kernel": gk, "batch": bmax,
+        "achieved": sweep["gather"][str(bmax)], "peak": PEAK_HBM_GBS, "unit": "GB/s",
+        "frac": round(sweep["gather"][str(bmax)] / PEAK_HBM_GBS, 5), "traffic": gtr,
+        "traffic_kind": "L2 fabric bytes (PMC FETCH_SIZE x2 + WRITE_SIZE): the 256 MB record table nearly fits "
+                        "the 256 MiB Infinity Cache, so part of FETCH is served on-die, not by HBM",
+        "achieved_read_write": round(2 * sweep["gather"][str(bmax)], 3),
+        "frac_read_write": round(2 * sweep["gather"][str(bmax)] / PEAK_HBM_GBS, 5),
+        "traffic_source": gsrc, "bytes_per_launch": bmax * W * 4, "avg_launch_ms": ms,
+        "note": "B_gather = 4 B (2 obs + act + 2) bytes read per launch (SURVEY §8d); the kernel writes "
+                "as many again (the minibatch it returns), counted in achieved_read_write; reads exceed "
+                "B_gather by the record padding (2O+A+2 floats stored in whole 128-B lines); rows uniform "
+                "with replacement over the 1e6-row buffer"}
+    return line
 
 
 if __name__ == "__main__":

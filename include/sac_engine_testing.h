@@ -29,6 +29,15 @@ int sac_engine_uses_split(const sac_engine *e);
  * inside sac_engine_train and sac_replay_sample_indices): out[b] = b-th element
  * of the Philox-keyed Feistel permutation of [0, size) for RNG (seed, step). */
 int sac_debug_sample_indices_host(int64_t size, int32_t batch, uint64_t seed, uint64_t step, int32_t *out);
+/* Host evaluation of the device eps draws of one step (the same inline
+ * philox_normal2 the fused step calls in its default device-RNG mode, compiled
+ * for the host): out[which][b][j], which = 0 the target rsample (agent.py:204),
+ * 1 the actor rsample (agent.py:241), rows b < batch, action dims j < act_dim
+ * (models.py:83: eps of rsample).  Counter (step, b, which << 16 | j / 2), key
+ * seed; Box-Muller gives dims 2p and 2p + 1. */
+int sac_debug_eps_host(uint64_t seed, uint64_t step, int32_t batch, int32_t act_dim, float *out);
+/* The same draws computed on the device (out: device [2][batch][act_dim]). */
+int sac_debug_eps_device(uint64_t seed, uint64_t step, int32_t batch, int32_t act_dim, float *out, void *stream);
 /* Polls a hand-off wait makes before it gives up and sets the timeout flag
  * (default 1 << 22, about 0.3 s); synchronises the stream.  A bound of 0
  * forces the timeout path (tests/test_gpu_engine.py): the API must raise. */

@@ -165,8 +165,12 @@ __host__ __device__ inline void philox4x32_10(uint32_t c[4], uint32_t k0, uint32
   }
 }
 
-// Standard normals for (row, which, pair): counter (step, row, which<<16|pair).
-__device__ __forceinline__ void philox_normal2(uint64_t seed, uint64_t step, uint32_t row,
+// Standard normals for (row, which, pair): counter (step, row, which<<16|pair),
+// key = seed; Box-Muller on the top 24 bits of the first two output words.
+// which = 0: the target rsample draw, 1: the actor rsample draw (models.py:83);
+// pair p gives action dims 2p, 2p+1.  Host-callable so the C ABI can export the
+// same inline code (sac_debug_eps_host); oracle/sampler_oracle.py restates it.
+__host__ __device__ inline void philox_normal2(uint64_t seed, uint64_t step, uint32_t row,
                                                uint32_t which, uint32_t pair, float& n0, float& n1) {
   uint32_t c[4] = {(uint32_t)step, (uint32_t)(step >> 32), row, (which << 16) | pair};
   philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32));

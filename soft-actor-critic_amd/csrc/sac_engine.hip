@@ -258,6 +258,27 @@ __global__ void __launch_bounds__(256) replay_gather_kernel(sac_replay rb, const
   }
 }
 
+// The eps draws of one step exactly as the fused step makes them in its default
+// (device RNG) mode: out[which][b][j] = philox_normal2(seed, step, b, which,
+// j / 2), component j % 2 (sac_phases.h / sac_split.h eps loops).
+__host__ __device__ inline void eps_pair(uint64_t seed, uint64_t step, int b, int which, int p, int B, int A,
+                                         float* out) {
+  float n0, n1;
+  philox_normal2(seed, step, (uint32_t)b, (uint32_t)which, (uint32_t)p, n0, n1);
+  float* o = out + ((size_t)which * B + b) * A;
+  o[2 * p] = n0;
+  if (2 * p + 1 < A) o[2 * p + 1] = n1;
+}
+__global__ void eps_draw_kernel(uint64_t seed, uint64_t step, int B, int A, float* __restrict__ out) {
+  const int NP = (A + 1) / 2;
+  const int64_t n = 2LL * B * NP;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int p = (int)(i % NP);
+    const int64_t rw = i / NP;
+    eps_pair(seed, step, (int)(rw % B), (int)(rw / B), p, B, A, out);
+  }
+}
+
 __global__ void replay_sample_kernel(const int64_t* __restrict__ state, int B, uint64_t seed, uint64_t step,
                                      int32_t* __restrict__ out) {
   const int64_t size = state[0];
@@ -1173,6 +1194,23 @@ int sac_debug_sample_indices_host(int64_t size, int32_t batch, uint64_t seed, ui
   if (!out || batch < 0 || size < batch) return fail(SAC_E_INVALID, "need 0 <= batch <= size and out != NULL");
   const Feistel f = feistel_make(seed, step, size);
   for (int32_t b = 0; b < batch; ++b) out[b] = (int32_t)feistel_sample(f, b, size);
+  return SAC_OK;
+}
+
+int sac_debug_eps_host(uint64_t seed, uint64_t step, int32_t batch, int32_t act_dim, float* out) {
+  if (!out || batch < 1 || act_dim < 1) return fail(SAC_E_INVALID, "need batch >= 1, act_dim >= 1, out != NULL");
+  for (int which = 0; which < 2; ++which)
+    for (int b = 0; b < batch; ++b)
+      for (int p = 0; p < (act_dim + 1) / 2; ++p) eps_pair(seed, step, b, which, p, batch, act_dim, out);
+  return SAC_OK;
+}
+
+int sac_debug_eps_device(uint64_t seed, uint64_t step, int32_t batch, int32_t act_dim, float* out, void* stream) {
+  if (!out || batch < 1 || act_dim < 1) return fail(SAC_E_INVALID, "need batch >= 1, act_dim >= 1, out != NULL");
+  const int64_t n = 2LL * batch * ((act_dim + 1) / 2);
+  const int blocks = (int)std::min<int64_t>(4096, (n + 255) / 256);
+  eps_draw_kernel<<<blocks, 256, 0, (hipStream_t)stream>>>(seed, step, batch, act_dim, out);
+  HIPCHK(hipGetLastError());
   return SAC_OK;
 }
 

@@ -18,9 +18,12 @@ Extra (optional) config keys, all under ``train``:
                the reference's RNG consumption)
     graph_chunk: steps per captured hipGraph for ``train_steps`` (default 32)
 
-Deliberate difference (documented in DESIGN.md): after ``load_agent`` the alpha
-optimizer keeps tuning ``log_alpha``; the reference rebinds ``log_alpha`` but not
-its optimizer (agent.py:550), which freezes alpha after a load.
+After ``load_agent`` with auto-tuning, alpha stays frozen as in the reference
+(it rebinds ``log_alpha`` but not its optimizer, agent.py:550-554); the
+optional ``train.alpha_after_load: tune`` keeps tuning it instead.
+
+Per-env-step ``QValues/*`` logging (``logger.log_q_values``) runs without the
+reference's ``.item()`` syncs (``QValueLog``), in both training loops.
 """
 from __future__ import annotations
 
@@ -131,6 +134,80 @@ class LossLog:
         if self.ev is not None:
             self.ev.synchronize()
             self._emit()
+
+
+class QValueLog:
+    """``QValues/Q1`` and ``QValues/Q2`` per env step (agent.py:370-376,
+    493-500) without the reference's two ``.item()`` host syncs per env step.
+
+    ``record`` evaluates Q1 and Q2 of the env steps' (next state, action)
+    pairs under the critics of that moment -- an eager forward on the
+    engine-owned parameters, queued behind that env step's gradient steps --
+    into a device buffer of [n][2]; the host inputs go up through pinned
+    memory (non-blocking), so nothing waits.  Every ``every`` env steps (and
+    at ``finish``) the filled rows are copied to pinned host memory behind the
+    training launches, and ``logger.log_q_values(q1, q2, step)`` runs for each
+    of them once that copy's event has completed (polled, never waited for,
+    except by ``finish``).  Values are the reference's: the mean over a batch
+    of one row is that row's value, as float32."""
+
+    def __init__(self, agent: "SAC", logger, every: int = 256):
+        self.agent, self.logger, self.every = agent, logger, max(1, int(every))
+        self.cap = 2 * self.every
+        self.dev = torch.empty(self.cap, 2, dtype=torch.float32, device=agent.device)
+        self.fill = 0
+        self.steps = []
+        self.pending = []
+
+    def record(self, states: Any, actions: Any, first_step: int) -> None:
+        """Q of rows (states[i], actions[i]) logged at step first_step + i."""
+        a = self.agent
+        host = np.concatenate([np.asarray(states, np.float32).reshape(-1, a.obs_size),
+                               np.asarray(actions, np.float32).reshape(-1, a.action_size)], axis=1)
+        n = host.shape[0]
+        if self.fill + n > self.cap:
+            self._flush()
+        x = torch.from_numpy(np.ascontiguousarray(host))
+        if a.device.type == "cuda":
+            x = x.pin_memory().to(a.device, non_blocking=True)
+        s, act = x[:, :a.obs_size], x[:, a.obs_size:]
+        with torch.no_grad():
+            self.dev[self.fill:self.fill + n, 0] = a.q_net1(s, act).reshape(-1)
+            self.dev[self.fill:self.fill + n, 1] = a.q_net2(s, act).reshape(-1)
+        self.steps.extend(range(first_step, first_step + n))
+        self.fill += n
+        if self.fill >= self.every:
+            self._flush()
+        self._drain(block=False)
+
+    def _flush(self) -> None:
+        if not self.fill:
+            return
+        cuda = self.dev.is_cuda
+        host = torch.empty(self.fill, 2, dtype=torch.float32, pin_memory=cuda)
+        host.copy_(self.dev[:self.fill], non_blocking=cuda)
+        ev = None
+        if cuda:
+            ev = torch.cuda.Event()
+            ev.record()
+        # later record() writes to self.dev queue behind this copy on the stream
+        self.pending.append((ev, host, self.steps))
+        self.steps, self.fill = [], 0
+
+    def _drain(self, block: bool) -> None:
+        while self.pending:
+            ev, host, steps = self.pending[0]
+            if ev is not None:
+                if not block and not ev.query():
+                    return
+                ev.synchronize()
+            for (q1, q2), st in zip(host.tolist(), steps):
+                self.logger.log_q_values(q1, q2, st)
+            self.pending.pop(0)
+
+    def finish(self) -> None:
+        self._flush()
+        self._drain(block=True)
 
 
 class SAC:
@@ -337,6 +414,13 @@ class SAC:
             return None
         return LossLog(self.engine, active_logger, every)
 
+    def _q_log(self, active_logger) -> Optional[QValueLog]:
+        """logger.log_q_values: per-env-step Q values, flushed every
+        logger.q_values_flush_every env steps (default 256) without host syncs."""
+        if active_logger is None or not self.config["logger"]["log_q_values"]:
+            return None
+        return QValueLog(self, active_logger, int(self.config["logger"].get("q_values_flush_every", 256)))
+
     def last_losses(self) -> Dict[str, float]:
         """Losses of the last step (reads device memory: synchronises)."""
         l = self._engine().losses()
@@ -429,6 +513,7 @@ class SAC:
         update_every = tr.get("update_frequency", 1)
         n_grad = tr.get("gradient_steps_per_update", 1)
         loss_log = self._loss_log(active_logger)
+        q_log = self._q_log(active_logger)
         for episode in _tqdm(range(num_episodes), disable=tqdm_disable):
             state, _ = self.env.reset()
             done = False
@@ -448,11 +533,8 @@ class SAC:
                     self._run_updates(n_grad)
                     if loss_log is not None:
                         loss_log.after_updates(total_steps)
-                if active_logger is not None and self.config["logger"]["log_q_values"]:
-                    self._log_q_values(
-                        states=torch.FloatTensor(np.asarray(state)).unsqueeze(0).to(self.device),
-                        actions=torch.FloatTensor(np.asarray(action)).unsqueeze(0).to(self.device),
-                        logger=active_logger, step=total_steps)
+                if q_log is not None:  # Q(s', a) of this env step (agent.py:370-376), no host sync
+                    q_log.record(state, action, total_steps)
             returns_window.append(episode_return)
             avg_return = float(np.mean(returns_window))
             best_avg_return = max(best_avg_return, avg_return)
@@ -465,6 +547,8 @@ class SAC:
             self.engine.check()
         if loss_log is not None:
             loss_log.finish()
+        if q_log is not None:
+            q_log.finish()
         metrics = {"total_episodes": total_episodes, "best_avg_return": best_avg_return,
                    "final_avg_return": avg_return}
         if active_logger is not None:
@@ -520,6 +604,7 @@ class SAC:
         total_steps = total_episodes = grad_steps = 0
         log_episodes = active_logger is not None and self.config["logger"]["log_episode_stats"]
         loss_log = self._loss_log(active_logger)
+        q_log = self._q_log(active_logger)
         pbar = _tqdm(range((int(total_env_steps) + N - 1) // N), disable=tqdm_disable)
         for _ in pbar:
             actions = self.select_actions(obs)
@@ -536,6 +621,8 @@ class SAC:
                 grad_steps += due
                 if loss_log is not None:
                     loss_log.after_updates(total_steps)
+            if q_log is not None:  # env step old + 1 + i logs Q(s'_i, a_i) under the critics after this vector step
+                q_log.record(info["final_obs"], actions, old + 1)
             ep_ret += rewards
             ep_len += 1
             for i in np.nonzero(dones)[0]:
@@ -556,6 +643,8 @@ class SAC:
             self.engine.check()  # a timed-out hand-off invalidates the run: raise, do not report it
         if loss_log is not None:
             loss_log.finish()
+        if q_log is not None:
+            q_log.finish()
         metrics = {"total_episodes": total_episodes, "best_avg_return": best_avg_return,
                    "final_avg_return": avg_return, "total_env_steps": total_steps, "gradient_steps": grad_steps}
         if active_logger is not None:

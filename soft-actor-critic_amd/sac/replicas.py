@@ -3,20 +3,36 @@ does not shard — each step depends on the previous step's parameters, so
 multi-GPU = N independent learners).  The only collective is the periodic
 metric aggregation over RCCL (``torch.distributed`` backend "nccl" on ROCm),
 a few float64 scalars per reduction.
+
+``replica_train`` is the replica training entry point: it trains this rank's
+learner in blocks of ``every`` gradient steps (graph-replayed) and after each
+block all-reduces the replica metric vector ("every R steps (e.g.
+1,000)").  The vector is built and reduced on the device, on the training
+stream's order, with no host synchronisation: training never waits for the
+host, only (on the device) for the tens-of-bytes all-reduce.
 """
 from __future__ import annotations
 
-from typing import Optional, Sequence
+import time
+from typing import List, Optional, Sequence, Tuple
 
 import torch
 
-# order of the aggregated metric vector
+# order of the aggregated metric vector of aggregate_metrics
 METRICS = ("steps", "wall_s", "q1_loss", "q2_loss", "policy_loss", "alpha_loss", "alpha", "mean_return")
+# order of the per-block device vector of replica_train (no host values: no sync)
+REPLICA_METRICS = ("steps", "q1_loss", "q2_loss", "policy_loss", "alpha_loss", "alpha")
 
 
 def replica_seed(base_seed: int, rank: int) -> int:
     """Seed of replica ``rank``: base + rank (network init, device RNG, env)."""
     return int(base_seed) + int(rank)
+
+
+def _initialised() -> bool:
+    import torch.distributed as dist
+
+    return dist.is_available() and dist.is_initialized()
 
 
 def aggregate_metrics(values: Sequence[float], group=None, device: Optional[torch.device] = None):
@@ -35,14 +51,60 @@ def aggregate_metrics(values: Sequence[float], group=None, device: Optional[torc
     return {"sum": s.tolist(), "mean": (s / world).tolist(), "max": m.tolist(), "world": world}
 
 
+def metric_vector(engine) -> torch.Tensor:
+    """REPLICA_METRICS of the engine's last step as a float64 device tensor,
+    built by device ops from the engine's own buffers (no host read)."""
+    return torch.cat([engine.rng_step.double(), engine.stats[:4].double(), engine.alpha_state[1:2].double()])
+
+
+def aggregate_device(v: torch.Tensor, group=None) -> Tuple[torch.Tensor, torch.Tensor]:
+    """(sum, max) over replicas of a device vector, without a host sync: with
+    RCCL the collectives run on the process group's stream after the current
+    stream's work, and the current stream waits for them on the device."""
+    import torch.distributed as dist
+
+    s, m = v.clone(), v.clone()
+    dist.all_reduce(s, op=dist.ReduceOp.SUM, group=group)
+    dist.all_reduce(m, op=dist.ReduceOp.MAX, group=group)
+    return s, m
+
+
+def replica_train(engine, replay, n_steps: int, chunk: int, every: int = 1024, group=None) -> List[Tuple]:
+    """``n_steps`` gradient steps of this rank's learner (hipGraph chunks of
+    ``chunk``), the replica metric vector all-reduced after every block of
+    ``every`` steps (and after the last, partial block) when torch.distributed
+    is initialised.  Returns the [(sum, max)] device tensors of every
+    aggregation; ``summarise_aggregates`` reads them (a sync) once training is
+    over."""
+    on = _initialised()
+    out = []
+    done = 0
+    every = max(1, int(every))
+    while done < n_steps:
+        k = min(every, n_steps - done)
+        engine.train_graph(replay, k, chunk)
+        done += k
+        if on:
+            out.append(aggregate_device(metric_vector(engine), group))
+    return out
+
+
+def summarise_aggregates(aggs, world: int, every: int) -> dict:
+    """Host view of replica_train's aggregates (reads device memory)."""
+    if not aggs:
+        return {"every": every, "aggregations": 0}
+    s, m = aggs[-1]
+    s, m = s.tolist(), m.tolist()
+    return {"every": every, "aggregations": len(aggs), "world": world, "fields": list(REPLICA_METRICS),
+            "last_sum": s, "last_mean": [x / world for x in s], "last_max": m}
+
+
 def timed_region(run, sync, device: Optional[torch.device] = None, group=None) -> float:
     """Wall time of ``run()`` bracketed by (barrier + ``sync()``) on both sides,
     MAX over ranks (the bench contract; single process when not initialised)."""
-    import time
-
     import torch.distributed as dist
 
-    on = dist.is_available() and dist.is_initialized()
+    on = _initialised()
     sync()
     if on:
         dist.barrier(group)

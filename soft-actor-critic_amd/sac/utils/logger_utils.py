@@ -1,26 +1,40 @@
-"""Run-artifact helpers (reference sac/utils/logger_utils.py:7-60)."""
+"""Run-artifact helpers (API of reference sac/utils/logger_utils.py:7-60).
+
+``episode_rewards.npy`` is float32 and ``episode_lengths.npy`` int32, as the
+reference writes them; the run directory is created if missing."""
 from __future__ import annotations
 
 from pathlib import Path
-from typing import Sequence
+from typing import List, Optional, Sequence
 
 import numpy as np
 
 
-def save_rewards(run_dir, rewards: Sequence[float]) -> Path:
-    path = Path(run_dir) / "episode_rewards.npy"
-    np.save(path, np.asarray(rewards, dtype=np.float64))
-    return path
+def save_rewards(run_dir, rewards: Sequence[float]) -> None:
+    run_dir = Path(run_dir)
+    run_dir.mkdir(parents=True, exist_ok=True)
+    np.save(run_dir / "episode_rewards.npy", np.array(rewards, dtype=np.float32))
 
 
-def save_lengths(run_dir, lengths: Sequence[int]) -> Path:
-    path = Path(run_dir) / "episode_lengths.npy"
-    np.save(path, np.asarray(lengths, dtype=np.int64))
-    return path
+def save_lengths(run_dir, lengths: Sequence[int]) -> None:
+    run_dir = Path(run_dir)
+    run_dir.mkdir(parents=True, exist_ok=True)
+    np.save(run_dir / "episode_lengths.npy", np.array(lengths, dtype=np.int32))
 
 
-def make_and_save_graph(values: Sequence[float], title: str, ylabel: str, path) -> None:
-    """Plot a curve to ``path`` when matplotlib is available (no-op otherwise)."""
+def load_rewards(run_dir) -> List[float]:
+    return np.load(Path(run_dir) / "episode_rewards.npy").astype(float).tolist()
+
+
+def load_lengths(run_dir) -> List[int]:
+    return np.load(Path(run_dir) / "episode_lengths.npy").astype(int).tolist()
+
+
+def make_and_save_graph(number_of_curves: int, data: list, title: str, xlabel: str, ylabel: str, filename: str,
+                        run_dir, legend: Optional[List[str]] = None) -> None:
+    """``number_of_curves`` curves of ``data`` to ``run_dir/filename`` (needs
+    matplotlib; a no-op without it).  The reference joins ``run_dir + "/" +
+    filename``, which fails for the Path its logger passes; this joins paths."""
     try:
         import matplotlib
 
@@ -28,10 +42,13 @@ def make_and_save_graph(values: Sequence[float], title: str, ylabel: str, path) 
         import matplotlib.pyplot as plt
     except Exception:  # pragma: no cover - optional dependency
         return
-    fig, ax = plt.subplots()
-    ax.plot(np.asarray(values))
-    ax.set_title(title)
-    ax.set_xlabel("Episode")
-    ax.set_ylabel(ylabel)
-    fig.savefig(path)
-    plt.close(fig)
+    plt.figure()
+    for i in range(number_of_curves):
+        plt.plot(data[i])
+    plt.title(title)
+    plt.xlabel(xlabel)
+    plt.ylabel(ylabel)
+    if legend:
+        plt.legend(legend)
+    plt.savefig(str(Path(run_dir) / filename))
+    plt.close()

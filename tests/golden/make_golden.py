@@ -407,6 +407,97 @@ def capture_loop() -> dict:
     return out
 
 
+LOGGER_CFG = {"enabled": True, "env_name": "Det", "agent_name": "SAC", "run_name": "pin", "use_timestamp": False,
+              "timestamp_format": "%Y", "flush_secs": 10, "log_episode_stats": True, "log_q_values": True,
+              "save_model": {"enabled": False, "path": None}}
+
+
+def _recording_writer(rec: list):
+    class Writer:  # stands in for SummaryWriter: every call, in order, as data
+        def __init__(self, log_dir=None, flush_secs=None, filename_suffix=""):
+            self.suffix = filename_suffix
+
+        def add_scalar(self, tag, value, step=None):
+            rec.append(["add_scalar", self.suffix, tag, float(value), step])
+
+        def add_hparams(self, hparam_dict, metric_dict, *a, **k):
+            rec.append(["add_hparams", self.suffix, dict(hparam_dict), dict(metric_dict)])
+
+        def flush(self):
+            rec.append(["flush", self.suffix])
+
+        def close(self):
+            rec.append(["close", self.suffix])
+
+    return Writer
+
+
+def capture_logger(tmp: str) -> dict:
+    """the reference ExperimentLogger's writer calls
+    (sac/utils/experiment_logger.py:54-148), recorded through a stand-in
+    SummaryWriter:
+      api/<case>: direct calls -- episode metrics, Q values, log_hparams with
+        the full SAC config (nested dicts, lists, None, bools) and metrics,
+        a repeated log_hparams (ignored), log_hparams with no metrics
+        (placeholder_metric), the log_q_values / log_episode_stats gates off,
+        flush / close;
+      loop: run_training_loop (agent.py:329-418) on DetEnv with the logger on
+        and training_step replaced by a no-op (Q values depend on the policy's
+        random actions, so only their tags and steps are compared)."""
+    import sac.utils.experiment_logger as xl
+    from sac.agent import SAC
+
+    sys.path.insert(0, OUT)
+    from det_env import DetEnv
+
+    out = {}
+    c = dict(obs=3, act=2, q_hidden=[16, 16], pi_hidden=[16, 16], batch=8, auto=True)
+    full_cfg = _cfg(c)
+    full_cfg["logger"] = dict(LOGGER_CFG, log_dir=tmp)
+    cases = {
+        "all_on": dict(LOGGER_CFG),
+        "gates_off": dict(LOGGER_CFG, log_q_values=False, log_episode_stats=False),
+    }
+    orig = xl.SummaryWriter
+    try:
+        for name, lc in cases.items():
+            rec: list = []
+            xl.SummaryWriter = _recording_writer(rec)
+            lg = xl.ExperimentLogger(dict(lc, log_dir=tmp))
+            lg.log_episode_metrics(0, 1.5, 10)
+            lg.log_episode_metrics(1, -2.25, 7)
+            lg.log_q_values(0.25, -0.5, 3)
+            lg.log_q_values(1.0, 2.0, 4)
+            lg.log_hparams(full_cfg, {"total_episodes": 2, "best_avg_return": 1.5, "final_avg_return": -0.375})
+            lg.log_hparams(full_cfg, {"ignored": 1.0})
+            lg.flush()
+            lg.close()
+            rec.append(["lists", lg.episode_rewards, lg.episode_lengths, lg.q1_values, lg.q2_values])
+            out[f"api/{name}"] = rec
+            rec2: list = []
+            xl.SummaryWriter = _recording_writer(rec2)
+            lg2 = xl.ExperimentLogger(dict(lc, log_dir=tmp))
+            lg2.log_hparams({"a": {"b": [1, 2], "c": None, "d": True, "e": 2.5, "f": "x"}, "g": 3}, {})
+            out[f"api/{name}/empty_metrics"] = rec2
+        rec3: list = []
+        xl.SummaryWriter = _recording_writer(rec3)
+        cfg = _cfg(c)
+        cfg["logger"] = dict(LOGGER_CFG, log_dir=tmp)
+        cfg["train"].update(warming_steps=10)  # >= the batch: the no-op step stands in for a real one
+        agent = SAC(DetEnv(c["obs"], c["act"]), cfg)
+        agent.training_step = lambda: None
+        metrics = agent.run_training_loop(4, tqdm_disable=True)
+        out["loop"] = [[r[0], r[1], r[2], None if r[2].startswith("QValues") else r[3], r[4]]
+                       if r[0] == "add_scalar" else r for r in rec3]
+        out["loop_metrics"] = {k: float(v) for k, v in metrics.items()}
+        out["loop_config"] = cfg
+        out["npy_dtypes"] = {f: str(np.load(os.path.join(agent.logger.run_dir, f"episode_{f}.npy")).dtype)
+                             for f in ("rewards", "lengths")}
+    finally:
+        xl.SummaryWriter = orig
+    return out
+
+
 def main() -> None:
     _install_stubs()
     sys.path.insert(0, REF)
@@ -427,6 +518,14 @@ def main() -> None:
     if not only or "loop" in only:
         np.savez_compressed(os.path.join(OUT, "ref_loop.npz"), **capture_loop())
         print("ref_loop written")
+    if not only or "logger" in only:
+        import tempfile
+
+        with tempfile.TemporaryDirectory() as tmp:
+            rec = json.loads(json.dumps(capture_logger(tmp)).replace(tmp, "<log_dir>"))  # run-independent
+        with open(os.path.join(OUT, "ref_logger.json"), "w") as f:
+            json.dump(rec, f, indent=1, sort_keys=True)
+        print("ref_logger.json written")
 
 
 if __name__ == "__main__":

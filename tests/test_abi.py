@@ -188,3 +188,22 @@ def test_host_sampler_is_uniform(lib):
     chi1 = ((first - exp1) ** 2 / exp1).sum()
     assert chi1 < size + 5 * np.sqrt(2 * size), chi1
     assert len(seen) == steps
+
+
+@pytest.mark.parametrize("seed,step,B,A", [(0, 0, 256, 4), (7, 12345, 1000, 3), (2**40 + 5, 2**33 + 1, 64, 1),
+                                           (3, 17, 4096, 2)])
+def test_host_eps_matches_oracle(lib, seed, step, B, A):
+    """The device RNG's eps (sac_debug_eps_host: the fused step's inline
+    philox_normal2 compiled for the host) against oracle/sampler_oracle.py's
+    independent numpy restatement: the same Philox words and fp32 Box-Muller,
+    so equal up to the libm / numpy float32 log, sin, cos (2 ulps)."""
+    from oracle import sampler_oracle as S
+
+    f = lib.sac_debug_eps_host
+    f.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p]
+    out = np.zeros((2, B, A), np.float32)
+    assert f(seed, step, B, A, out.ctypes.data) == 0
+    want = S.eps_draws(seed, step, B, A)
+    np.testing.assert_allclose(out, want, rtol=1e-6, atol=1e-6)
+    assert np.mean(out == want) > 0.5
+    assert f(seed, step, 0, A, out.ctypes.data) == -1  # empty batch rejected

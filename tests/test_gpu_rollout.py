@@ -5,10 +5,14 @@ produce the same replay rows and the same engine state bit for bit; with N envs
 the batched action kernel and the single-copy push must equal their per-row
 forms."""
 import copy
+import os
+import sys
 
 import numpy as np
 import pytest
 import torch
+
+from _fixtures import GOLDEN
 
 pytestmark = pytest.mark.gpu
 
@@ -171,3 +175,82 @@ def _group(scalars):
     for tag, v, step in scalars:
         out.setdefault(tag, []).append((step, v))
     return out
+
+
+def _rec_writer(rec):
+    from test_logger_pins import recording_writer
+
+    return recording_writer(rec)
+
+
+def test_training_loop_logger_matches_reference(tmp_path, monkeypatch):
+    """SURVEY f4/f2 against the reference's own run_training_loop record
+    (tests/golden/ref_logger.json 'loop': DetEnv, logger on, log_q_values on,
+    4 episodes): the same writer calls per tag -- QValues/Q1, QValues/Q2 at
+    every env step (values from this run's critics: the reference's came from
+    its random policy), Episode/Reward and Episode/Length per episode with the
+    reference's values, and one add_hparams of the flattened config and the
+    returned metrics (train/device 'cuda' here) -- while the Q values come
+    through QValueLog with no .item() inside the loop."""
+    import json
+
+    import torch
+
+    from sac import agent as agent_mod
+    from sac.agent import SAC
+    from sac.utils import experiment_logger as xl
+    from test_logger_pins import LOGGER_CFG
+
+    sys.path.insert(0, GOLDEN)
+    from det_env import DetEnv
+
+    ref = json.load(open(os.path.join(GOLDEN, "ref_logger.json")))
+    cfg = json.loads(json.dumps(ref["loop_config"]).replace("<log_dir>", str(tmp_path)))
+    cfg["train"]["device"] = "cuda"
+    rec = []
+    monkeypatch.setattr(xl, "_writer_cls", lambda: _rec_writer(rec))
+    agent = SAC(DetEnv(3, 2), cfg)
+    # eager per-step values at record time (the reference's q.mean().item()), for comparison
+    eager = []
+    orig_record = agent_mod.QValueLog.record
+
+    def spy(self, states, actions, first_step):
+        with torch.no_grad():
+            s = torch.as_tensor(np.asarray(states, np.float32)).reshape(1, -1).to(agent.device)
+            a = torch.as_tensor(np.asarray(actions, np.float32)).reshape(1, -1).to(agent.device)
+            eager.append((first_step, self.agent.q_net1(s, a).mean(), self.agent.q_net2(s, a).mean()))
+        return orig_record(self, states, actions, first_step)
+
+    monkeypatch.setattr(agent_mod.QValueLog, "record", spy)
+    items = []
+    orig_item = torch.Tensor.item
+    monkeypatch.setattr(torch.Tensor, "item", lambda t: items.append(1) or orig_item(t))
+    m = agent.run_training_loop(4, tqdm_disable=True)
+    n_items = len(items)
+    monkeypatch.setattr(torch.Tensor, "item", orig_item)
+    assert n_items == 0, "a .item() host sync ran inside the training loop"
+    assert agent.engine.steps_done > 0  # updates ran (warming_steps 10)
+    assert {k: float(v) for k, v in m.items()} == ref["loop_metrics"]
+    norm = json.loads(json.dumps(rec).replace(str(tmp_path), "<log_dir>"))
+    want = ref["loop"]
+
+    def by_tag(calls):
+        out = {}
+        for c in calls:
+            key = c[2] if c[0] == "add_scalar" else c[0]
+            out.setdefault(key, []).append(c)
+        return out
+
+    got_t, want_t = by_tag(norm), by_tag(want)
+    assert sorted(got_t) == sorted(want_t)
+    for tag in ("Episode/Reward", "Episode/Length"):
+        assert got_t[tag] == want_t[tag], tag
+    for tag in ("QValues/Q1", "QValues/Q2"):
+        assert [c[4] for c in got_t[tag]] == [c[4] for c in want_t[tag]], tag  # steps
+    (gh,), (wh,) = got_t["add_hparams"], want_t["add_hparams"]
+    assert gh[2].pop("train/device") == "cuda" and wh[2].pop("train/device") == "cpu"
+    assert gh == wh
+    # the async values are the per-step eager ones
+    e = {st: (q1.item(), q2.item()) for st, q1, q2 in eager}
+    for c1, c2 in zip(got_t["QValues/Q1"], got_t["QValues/Q2"]):
+        assert (c1[3], c2[3]) == e[c1[4]]
