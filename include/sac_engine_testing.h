@@ -25,6 +25,10 @@ int sac_engine_uses_roles(const sac_engine *e);
 /* 1 if phases A/C run the hidden-split role kernels (sac_split.h: two
  * workgroups per role and row tile, each with half of the 256-wide layer 1). */
 int sac_engine_uses_split(const sac_engine *e);
+/* Workgroups of the fused-step launch (sac_persist.h: the four phases of a
+ * step in ONE launch, counters between them) when the engine uses it, else 0
+ * (four launches per step). */
+int sac_engine_uses_fused_step(const sac_engine *e);
 /* Host evaluation of the device sampler (the same inline code as the sampler
  * inside sac_engine_train and sac_replay_sample_indices): out[b] = b-th element
  * of the Philox-keyed Feistel permutation of [0, size) for RNG (seed, step). */

@@ -34,6 +34,7 @@
 
 #include "sac_phases.h"
 #include "sac_split.h"
+#include "sac_persist.h"
 
 // ============================================================================ params / replay
 template <typename T>
@@ -312,6 +313,11 @@ struct sac_engine {
   size_t upd_lds = 0;  // dynamic LDS of an update tile (SAC_UPD_LDS_FOR(upd_slots))
   int nrt = 0;
   int fused = 0;  // 0: A B C D per step; 1: D inside the next A's launch; 2: also B inside C's
+  // persistent step (sac_persist.h): one launch of G workgroups per run of steps
+  int persist = 0;
+  int ncu = 256;  // compute units of the device (the persistent grid's bound)
+  int G = 0;
+  std::vector<PTask> hostP;
   // graph cache
   hipGraphExec_t gexec = nullptr;
   hipGraph_t graph = nullptr;
@@ -355,6 +361,7 @@ static int validate(const sac_engine_config* c) {
 
 // Lays out everything; when e != nullptr also fills e->h pointers (base = workspace).
 static void xcd_order(std::vector<TileDesc>& tiles);
+static void plan_persist(sac_engine* e, int esz);
 static bool xcd_order_parts(std::vector<TileDesc>& tiles, int P);
 
 static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
@@ -441,7 +448,7 @@ static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
   h.gstride = SAC_ROWS * (A + 1);
   h.gran = (uint64_t*)P(lay.take((size_t)G_COUNT * nrt * h.gstride * 8));
   h.stg_stride = (16 + 2 * SAC_ROWS * O + SAC_ROWS * A + 2 * SAC_ROWS + 15) / 16 * 16;
-  h.stg = (float*)P(lay.take((size_t)nrt * h.stg_stride * 4));
+  h.stg = (float*)P(lay.take((size_t)2 * nrt * h.stg_stride * 4));  // two records per row tile: by step parity
   h.split = split;
   h.gs2 = SAC_ROWS * std::max(2 * A, A + 1);
   h.gran2 = (uint64_t*)P(lay.take((size_t)GS_COUNT * nrt * SPLIT_GP * h.gs2 * 8));
@@ -486,6 +493,9 @@ static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
       (ni == NET_PI ? nD : nB) += t * parts;
       nhalf += t * (parts - 1);  // producer parts: one 1024-granule slot each
     }
+  // persistent step: readiness counters (+ the exit word) and the task table
+  const size_t o_pctr = lay.take((size_t)(PC_COUNT * PC_SHARDS * PC_STRIDE + PC_STRIDE) * 4);
+  const size_t o_ptask = lay.take((size_t)1024 * sizeof(PTask));
   const size_t o_tB = lay.take((size_t)nB * sizeof(TileDesc));
   const size_t o_tD = lay.take((size_t)nD * sizeof(TileDesc));
   const size_t o_part = lay.take((size_t)nhalf * 1024 * 8);  // batch-half partial dW granules of split tiles
@@ -603,6 +613,8 @@ static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
     e->h.nB = nB;
     e->h.nD = nD;
     e->lds_bytes = (size_t)lo * 4;
+    e->h.pctr = (uint32_t*)(base + o_pctr);
+    e->h.ptasks = (const void*)(base + o_ptask);
     {  // update tiles stage up to 4 batch chunks of 512 B per operand row per round
        // (every tile reduces over at most Bp columns: split layer 0 is two half tiles)
       const int bch = 512 / esz;
@@ -723,8 +735,81 @@ static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
       if (fuse == 2 && nB + 3 * nrt > 256) fuse = 1;
       e->fused = fuse;
     }
+    plan_persist(e, esz);
   }
   return total + 256;
+}
+
+// The persistent step's task table (sac_persist.h).  Workgroup w runs phase-A
+// role w (the role kernels' block order: pi(s') parts, target critics,
+// critics, pi(s)); the other phases' tasks go to the workgroups that are free
+// when those tasks can start:
+//   B tiles      -> pi(s') workgroups (done first), target critics, spares, pi(s), critics
+//   C pi roles   -> pi(s') workgroups (after their B tile; they then wait for the critics)
+//   C critics    -> critic workgroups (no B tile), pi(s), spares, target critics, pi(s')
+//   D tiles      -> target-critic workgroups (idle until the next step's pi(s')), spares, ...
+// so the next step's pi(s') workgroups carry no phase-D tile and can sample and
+// gather their rows while phase D runs.  Lists are concatenations of whole
+// classes (multiples of 8 workgroups at C2/C4), so a tile keeps the XCD bucket
+// xcd_order gave its position (blocks are dealt round-robin over the XCDs).
+#ifndef SAC_FUSED_DEFAULT
+#define SAC_FUSED_DEFAULT 0  // four launches per step stay the default until the fused step measures faster
+#endif
+static void plan_persist(sac_engine* e, int esz) {
+  e->persist = 0;
+  if (!e->h.split) return;
+  int on = SAC_FUSED_DEFAULT;
+  if (const char* v = getenv("SAC_PERSIST")) on = atoi(v) != 0;
+  if (!on) return;
+  const int nrt = e->h.nrt, WP = split_wpi(esz), W = split_wc(esz);
+  const int nA = (WP + 10) * nrt, nCq = 2 * W * nrt, nCp = W * nrt, nB = e->nB, nD1 = e->nD + 1;
+  int G = e->ncu;
+  if (const char* v = getenv("SAC_PERSIST_G")) G = std::max(1, atoi(v));
+  G = std::min(G, 1024);
+  if (nA > G || nB > G || nCq + nCp > G || nD1 > G) return;
+  std::vector<int> pis2, qt, cr, pis, spare;
+  for (int w = 0; w < G; ++w) {
+    if (w < WP * nrt) pis2.push_back(w);
+    else if (w < (WP + 4) * nrt) qt.push_back(w);
+    else if (w < (WP + 8) * nrt) cr.push_back(w);
+    else if (w < nA) pis.push_back(w);
+    else spare.push_back(w);
+  }
+  auto cat = [](std::initializer_list<const std::vector<int>*> ls) {
+    std::vector<int> o;
+    for (const auto* l : ls) o.insert(o.end(), l->begin(), l->end());
+    return o;
+  };
+  std::vector<PTask> t((size_t)G, PTask{-1, -1, -1, -1});
+  for (int w = 0; w < nA; ++w) t[w].a = (int16_t)w;
+  const std::vector<int> ob = cat({&pis2, &qt, &spare, &pis, &cr});
+  for (int i = 0; i < nB; ++i) t[ob[i]].b = (int16_t)i;
+  for (int i = 0; i < nCp; ++i) t[ob[i]].c = (int16_t)(nCq + i);
+  int ic = 0;
+  for (int w : cat({&cr, &pis, &spare, &qt, &pis2}))
+    if (ic < nCq && t[w].c < 0) t[w].c = (int16_t)ic++;
+  // stagers (phase C, E.stage): the next step's batch per row tile, on
+  // workgroups left without a phase-C task (target critics: between their B
+  // and D tiles)
+  int is = 0;
+  const int nS = e->h.stage ? nrt : 0;
+  for (int w : cat({&qt, &spare, &pis, &cr, &pis2}))
+    if (is < nS && t[w].c < 0) t[w].c = (int16_t)(nCq + nCp + is++);
+  if (is < nS) return;
+  const std::vector<int> od = cat({&qt, &spare, &cr, &pis, &pis2});
+  for (int i = 0; i < nD1; ++i) t[od[i]].d = (int16_t)i;
+  e->hostP = t;
+  e->G = G;
+  e->h.pc_n[PC_AQ] = (uint32_t)(8 * nrt);
+  e->h.pc_n[PC_PS] = (uint32_t)(2 * nrt);
+  e->h.pc_n[PC_BQ1] = (uint32_t)e->h.nBq[0];
+  e->h.pc_n[PC_BQ2] = (uint32_t)e->h.nBq[1];
+  e->h.pc_n[PC_CP] = (uint32_t)nCp;
+  e->h.pc_n[PC_D] = (uint32_t)nD1;
+  e->h.pc_n[PC_AQP] = (uint32_t)(4 * nrt);  // critic roles (2 critics x 2 halves x nrt)
+  e->h.o_pflag = (int)((std::max(e->lds_bytes, e->upd_lds) + 15) / 16 * 4);
+  if ((size_t)e->h.o_pflag * 4 + 16 > 160 * 1024) return;
+  e->persist = 1;
 }
 
 // Update-tile order for the XCDs (speed only; any order gives the same bits).
@@ -814,6 +899,7 @@ static void set_lds_attrs(size_t bytes) {
   (void)hipFuncSetAttribute((const void*)sac_actor_split<T>, hipFuncAttributeMaxDynamicSharedMemorySize, b);
   (void)hipFuncSetAttribute((const void*)sac_critic_update<T>, hipFuncAttributeMaxDynamicSharedMemorySize, b);
   (void)hipFuncSetAttribute((const void*)sac_actor_update<T>, hipFuncAttributeMaxDynamicSharedMemorySize, b);
+  (void)hipFuncSetAttribute((const void*)sac_persist<T>, hipFuncAttributeMaxDynamicSharedMemorySize, b);
 }
 
 // empty kernel: the dispatch + event gap of sac_engine_time_phases
@@ -869,10 +955,31 @@ static void launch_kind(sac_engine* e, int kind, const sac_replay* rb, const int
   }
 }
 
+// Fused-step launches of n consecutive steps (one step per launch, sac_persist.h).
+static void launch_persist(sac_engine* e, const sac_replay* rb, int n, const int32_t* indices, const float* eps,
+                           hipStream_t s) {
+  const size_t B = e->cfg.batch, A = e->cfg.act_dim;
+  const size_t lds = (size_t)e->h.o_pflag * 4 + 16;
+  for (int k = 0; k < n; ++k) {  // one step per launch (sac_persist.h)
+    const int32_t* ix = indices ? indices + (size_t)k * B : nullptr;
+    const float* ep = eps ? eps + (size_t)k * 2 * B * A : nullptr;
+    if (e->cfg.precision == SAC_PREC_BF16)
+      sac_persist<bf16><<<e->G, SAC_THREADS, lds, s>>>(e->d, *rb, ix, ep);
+    else
+      sac_persist<float><<<e->G, SAC_THREADS, lds, s>>>(e->d, *rb, ix, ep);
+  }
+}
+
 // The launches of n consecutive steps (and, per launch, its kind in *kinds).
+// persistent: one launch for the n steps (per-launch kinds / events: the four
+// phase launches, profiling only).
 static void launch_steps(sac_engine* e, const sac_replay* rb, int n, const int32_t* indices, const float* eps,
                          hipStream_t s, std::vector<int>* kinds = nullptr, std::vector<hipEvent_t>* ev = nullptr) {
   const size_t B = e->cfg.batch, A = e->cfg.act_dim;
+  if (e->persist && !kinds && !ev) {
+    if (n > 0) launch_persist(e, rb, n, indices, eps, s);
+    return;
+  }
   auto go = [&](int kind, int step) {
     const int32_t* ix = indices ? indices + (size_t)step * B : nullptr;
     const float* ep = eps ? eps + (size_t)step * 2 * B * A : nullptr;
@@ -971,6 +1078,12 @@ int sac_engine_create(const sac_engine_config* cfg, const sac_engine_buffers* bu
   sac_engine* e = new sac_engine();
   e->cfg = *cfg;
   e->buf = *buf;
+  {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) == hipSuccess &&
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0)
+      e->ncu = n;
+  }
   plan(cfg, e, (char*)buf->workspace);
   if (std::max(e->lds_bytes, e->upd_lds) > 160 * 1024) {
     const size_t lb = e->lds_bytes;
@@ -982,6 +1095,8 @@ int sac_engine_create(const sac_engine_config* cfg, const sac_engine_buffers* bu
   if (err == hipSuccess) err = hipMemcpyAsync(e->d, &e->h, sizeof(EngineDev), hipMemcpyHostToDevice, s);
   if (err == hipSuccess) err = hipMemcpyAsync(e->tilesB, e->hostB.data(), e->hostB.size() * sizeof(TileDesc), hipMemcpyHostToDevice, s);
   if (err == hipSuccess) err = hipMemcpyAsync(e->tilesD, e->hostD.data(), e->hostD.size() * sizeof(TileDesc), hipMemcpyHostToDevice, s);
+  if (err == hipSuccess && e->persist)
+    err = hipMemcpyAsync((void*)e->h.ptasks, e->hostP.data(), e->hostP.size() * sizeof(PTask), hipMemcpyHostToDevice, s);
   if (err == hipSuccess) err = hipStreamSynchronize(s);
   if (err != hipSuccess) {
     delete e;
@@ -1217,6 +1332,8 @@ int sac_debug_eps_device(uint64_t seed, uint64_t step, int32_t batch, int32_t ac
 int sac_engine_uses_roles(const sac_engine* e) { return e && e->h.roles ? 1 : 0; }
 
 int sac_engine_uses_split(const sac_engine* e) { return e && e->h.split ? 1 : 0; }
+
+int sac_engine_uses_fused_step(const sac_engine* e) { return e && e->persist ? e->G : 0; }
 
 int sac_engine_phase_layout(const sac_engine* e) { return e ? e->fused : 0; }
 

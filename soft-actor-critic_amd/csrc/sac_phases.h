@@ -32,6 +32,14 @@ __device__ __forceinline__ float ldf(const float* p) {
 __device__ __forceinline__ void coh_storef(float* p, float v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+// COH ? sc1 (write-through) : plain store of a float another workgroup of the launch reads
+template <bool COH>
+__device__ __forceinline__ void st_f(float* p, float v) {
+  if constexpr (COH)
+    coh_storef(p, v);
+  else
+    *GP(float, p) = v;
+}
 // weight-stream fragment: sc1 when the matrix was written earlier in the same launch
 template <typename T, bool COH>
 __device__ __forceinline__ typename MM<T>::Frag coh_frag(__amdgpu_buffer_rsrc_t rs, uint32_t byte_off) {
@@ -121,10 +129,27 @@ struct EngineDev {
   int gs2;
   int o_red;        // LDS: SAC_NW x 256 floats of k-split partial tiles
   int spin_limit;  // polls before a hand-off wait gives up and sets SYNC_TIMEOUT (~0.3 s at 1 << 22)
+  // persistent step (sac_persist.h): readiness counters [PC_COUNT][8 shards][16]
+  // + 1 exit word, the per-workgroup task table, producers per step of every
+  // counter, and an LDS word for the wait verdict (past every phase's layout)
+  uint32_t* pctr;
+  const void* ptasks;
+  uint32_t pc_n[8];
+  int o_pflag;
   // LDS layout (float offsets)
   int o_X, o_Y, o_P1[SAC_DEV_LAYERS], ldp1[SAC_DEV_LAYERS], o_P2[SAC_DEV_LAYERS], ldp2[SAC_DEV_LAYERS];
   int o_s, o_s2, o_a, o_a2, o_r, o_d, o_et, o_ea, o_out, o_outp, o_out2, o_outp2, o_lp, o_qt, o_y, o_g, o_g2,
       o_ga, o_gout, o_slot;
+};
+
+// The gradient step a phase body works on: its device RNG step (indices, eps),
+// hand-off epoch (granule tags) and parity (double-buffered per-step state).
+// The per-phase kernels read them from memory at launch; the persistent step
+// (sac_persist.h) passes step k of its launch.
+struct StepCtx {
+  uint64_t step;
+  uint32_t ep;
+  int par;
 };
 
 // One 32x32 weight tile of the update phases, self-contained so a block needs a
@@ -669,7 +694,9 @@ __device__ __forceinline__ void layer_bwd(const lf* G, int ldg, const AS_C Layer
 // dst[k][col0 + r] = x[r][k] (0 for k >= K or r >= nvalid), k < Kp, where
 // x[r][k] = src[r][k] * rowscale[r] (rowscale == null: 1); with dbp != null also
 // dbp[col0 / SAC_ROWS][k] = sum_{r<nvalid} x[r][k] (k < K).
-template <typename T, int ROWS>
+// COH (persistent step): sc1 (write-through) stores, for consumers in other
+// workgroups of the same launch (they load with sc1 loads after a counter).
+template <typename T, int ROWS, bool COH = false>
 __device__ __forceinline__ void store_T(const lf* __restrict__ src, int lds_ld, int Kp, int K, void* dst_,
                                                  int Bp, int col0, int nvalid, float* dbp_,
                                                  const lf* __restrict__ rowscale = nullptr, int dbp_ld = 0) {
@@ -701,7 +728,11 @@ __device__ __forceinline__ void store_T(const lf* __restrict__ src, int lds_ld, 
     }
     if (live) {
       AS_G T* d = dst + (size_t)k * Bp + col0 + ch * 8;
-      if constexpr (sizeof(T) == 2) {
+      if constexpr (COH) {
+        const uint32_t off = (uint32_t)(((size_t)k * Bp + col0 + ch * 8) * sizeof(T));
+        coh_store16<true>(dst_, off, *(const u32x4*)v);
+        if constexpr (sizeof(T) == 4) coh_store16<true>(dst_, off + 16, *(const u32x4*)(v + 4));
+      } else if constexpr (sizeof(T) == 2) {
         *(AS_G u32x4*)d = *(const u32x4*)v;
       } else {
         *(AS_G u32x4*)d = *(const u32x4*)v;
@@ -711,7 +742,13 @@ __device__ __forceinline__ void store_T(const lf* __restrict__ src, int lds_ld, 
     if (dbp) {
 #pragma unroll
       for (int o = 1; o < CH; o <<= 1) s += __shfl_xor(s, o, 64);
-      if (live && ch == 0 && k < K) dbp[(size_t)(col0 / SAC_ROWS) * (dbp_ld ? dbp_ld : K) + k] = s;
+      if (live && ch == 0 && k < K) {
+        AS_G float* bp = dbp + (size_t)(col0 / SAC_ROWS) * (dbp_ld ? dbp_ld : K) + k;
+        if constexpr (COH)
+          coh_storef((float*)bp, s);
+        else
+          *bp = s;
+      }
     }
   }
 }
@@ -856,9 +893,33 @@ __device__ __forceinline__ void count_done(uint32_t* counter) {
 // (>= the alpha block's 5 x 1024 floats)
 #define SAC_UPD_SLOT_BYTES (64 * 528)
 #define SAC_UPD_LDS_FOR(slots) ((slots) * SAC_UPD_SLOT_BYTES + 2 * 32 * 33 * 4 + 32 * 17 * 4)
-template <typename T, int UT, bool COH, int GS = 1>
+// Persistent mode (the whole step in one launch, sac_persist.h): the tile's
+// operands were written earlier in the same launch by other workgroups with
+// sc1 (write-through) stores, so every load of them is an sc1 buffer load
+// (MI355X_MICROARCH.md visibility, write-through form); its own element state
+// (masters, moments, targets: only this tile's workgroup writes them) is
+// loaded BEFORE waiting for the operands' producers; the step's Adam scalars
+// come from the caller (computed per step, no phase-A block); the biases and
+// the critics' W2 row (read by role workgroups) are stored sc1.
+struct UpdStep {
+  float neg_step, bc2s;  // this step's -lr / bias_correction1, sqrt(bias_correction2)
+  uint32_t ep;           // hand-off epoch of this step (batch-part granules)
+};
+struct NoWait {
+  template <typename... X>
+  __device__ __forceinline__ void operator()(X...) const {}
+};
+template <bool P>
+__device__ __forceinline__ u32x4 opnd16(const void* base, uint32_t byte_off) {
+  if constexpr (P)
+    return __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(coh_rsrc(base, 0xFFFFFFF0u), (int)byte_off,
+                                                                          0, 16));
+  return *(const AS_G u32x4*)((const AS_G char*)base + byte_off);
+}
+template <typename T, int UT, bool COH, int GS = 1, bool P = false, typename Wait = NoWait>
 __device__ __forceinline__ void dw_adam_tile(const AS_C EngineDev& E, const TileDesc* tdp_, bool polyak, int par,
-                                             int par_x, lf* lds) {
+                                             int par_x, lf* lds, const UpdStep* us = nullptr,
+                                             const Wait& wait = Wait()) {
   static_assert(GS == 1 || sizeof(T) == 4, "dY parts are summed in fp32 only");
   constexpr int KC = MM<T>::KC, KL = MM<T>::KL;
   constexpr int EPR = 16 / sizeof(T);  // elements per 16-B piece (= KL)
@@ -876,9 +937,9 @@ __device__ __forceinline__ void dw_adam_tile(const AS_C EngineDev& E, const Tile
   lf* accs = lds + (nslot * slot_el * (int)sizeof(T) + 15) / 16 * 4;
   lf* tgts = accs + 32 * 33;
   lf* red = tgts + 32 * 33;
-  // this step's Adam scalars (written by phase A)
-  const float neg_step = GPC(float, E.adam_sc)[par * 6 + td.opt * 2];
-  const float bc2s = GPC(float, E.adam_sc)[par * 6 + td.opt * 2 + 1];
+  // this step's Adam scalars (written by phase A; persistent: the caller's)
+  const float neg_step = P ? us->neg_step : GPC(float, E.adam_sc)[par * 6 + td.opt * 2];
+  const float bc2s = P ? us->bc2s : GPC(float, E.adam_sc)[par * 6 + td.opt * 2 + 1];
   // ---- 1. loads: the first round of staged operands, then element state + bias
   // state + bias partials, all before the first wait (one round trip; the bias
   // sums below wait for everything issued before them, in issue order)
@@ -899,7 +960,8 @@ __device__ __forceinline__ void dw_adam_tile(const AS_C EngineDev& E, const Tile
   const long goff = GS > 1 ? td.goff : 0;
   const int ldg = td.ld, ldx = td.ldx;
   // round r0's slot sl -> rg[sl] (16-B pieces of the 32 dY^T rows of every part, then of the 32 X^T rows)
-  auto issue = [&](int r0, auto slc) {
+  // what: 1 operands, 2 seeds, 3 both
+  auto issue = [&](int r0, auto slc, int what = 3) {
     constexpr int sl = decltype(slc)::value;
     const int b0 = r0 + sl * SAC_UPD_BCH;
     if (sl < ns && b0 < Bp) {  // uniform
@@ -912,13 +974,23 @@ __device__ __forceinline__ void dw_adam_tile(const AS_C EngineDev& E, const Tile
           const int i = threadIdx.x + pi * UT;
           const int row = i / per_row, pc = i % per_row;
           const AS_G T* src = op < GS ? gsrc + op * goff + (size_t)row * ldg : xsrc + (size_t)row * ldx;
-          if (i < 32 * per_row) rg[sl][op][pi] = *(const AS_G u32x4*)(src + b0 + pc * EPR);
-          if constexpr (sizeof(T) == 4)
-            if (op == 0 && seedp && i < 32 * per_row) sdr[sl][pi] = *(const AS_G f32x4*)(seedp + b0 + pc * EPR);
+          if constexpr (P) {  // uniform bases, per-lane byte offsets: sc1 buffer loads
+            const AS_G T* base = op < GS ? gsrc : xsrc;
+            const uint32_t off = (uint32_t)((src - base + b0 + pc * EPR) * sizeof(T));
+            if ((what & 1) && i < 32 * per_row) rg[sl][op][pi] = opnd16<true>((const void*)base, off);
+            if constexpr (sizeof(T) == 4)
+              if ((what & 2) && op == 0 && seedp && i < 32 * per_row)
+                sdr[sl][pi] = __builtin_bit_cast(f32x4, opnd16<true>((const void*)seedp,
+                                                                      (uint32_t)((b0 + pc * EPR) * 4)));
+          } else {
+            if (i < 32 * per_row) rg[sl][op][pi] = *(const AS_G u32x4*)(src + b0 + pc * EPR);
+            if constexpr (sizeof(T) == 4)
+              if (op == 0 && seedp && i < 32 * per_row) sdr[sl][pi] = *(const AS_G f32x4*)(seedp + b0 + pc * EPR);
+          }
         }
     }
   };
-  static_for<MAXS>([&](auto sl) { issue(0, sl); });
+  if (!P) static_for<MAXS>([&](auto sl) { issue(0, sl); });
   AS_G float* W = GP(float, td.W);
   AS_G float* Wm = GP(float, td.Wm);
   AS_G float* Wv = GP(float, td.Wv);
@@ -933,7 +1005,7 @@ __device__ __forceinline__ void dw_adam_tile(const AS_C EngineDev& E, const Tile
     ok[e] = n < td.N && k < td.K;
     idx[e] = ok[e] ? (size_t)n * td.K + k : 0;
     if (td.kpart < 2) {  // uniform: a producer part only computes its partial dW
-      p[e] = W[idx[e]];
+      p[e] = ldf<P>((const float*)(W + idx[e]));  // persistent: may have been stored sc1 (W2 row)
       m[e] = Wm[idx[e]];
       v[e] = Wv[idx[e]];
       tp[e] = polyak ? tW[idx[e]] : 0.f;
@@ -944,10 +1016,19 @@ __device__ __forceinline__ void dw_adam_tile(const AS_C EngineDev& E, const Tile
   const bool do_bias = td.k0 == 0 && td.kpart <= 1;
   float pb = 0.f, mb = 0.f, vb = 0.f, tbv = 0.f;
   if (do_bias && tid < 32 && td.n0 + tid < td.N) {
-    pb = GPC(float, td.b)[td.n0 + tid];
+    pb = ldf<P>((const float*)td.b + td.n0 + tid);
     mb = GPC(float, td.bm)[td.n0 + tid];
     vb = GPC(float, td.bv)[td.n0 + tid];
-    if (polyak) tbv = GPC(float, td.tb)[td.n0 + tid];
+    if (polyak) tbv = ldf<P>((const float*)td.tb + td.n0 + tid);
+  }
+  if constexpr (P) {  // the operands' producers, then the operands themselves
+    // wait(0): what the operands need (fp32 critics' layers 0 / 1: the
+    // unit-seed dY^T and X^T, stored before y is known); wait(1): everything
+    // (the seeds, the bias partials)
+    wait(0);
+    static_for<MAXS>([&](auto sl) { issue(0, sl, 1); });
+    wait(1);
+    static_for<MAXS>([&](auto sl) { issue(0, sl, 2); });
   }
   // bias gradient: the row tiles' partial sums, 16 partial lanes per column
   // (512 lanes, BPT per thread: the same sums for 4-, 8- and 16-wave blocks);
@@ -966,7 +1047,7 @@ __device__ __forceinline__ void dw_adam_tile(const AS_C EngineDev& E, const Tile
 #pragma unroll
         for (int u = 0; u < BU; ++u) {
           const int rt = rt0 + 16 * u;
-          pv[u] = rt < td.nrt ? dbp[(size_t)rt * td.N] : 0.f;
+          pv[u] = rt < td.nrt ? ldf<P>((const float*)(dbp + (size_t)rt * td.N)) : 0.f;
         }
 #pragma unroll
         for (int u = 0; u < BU; ++u)
@@ -1073,7 +1154,7 @@ __device__ __forceinline__ void dw_adam_tile(const AS_C EngineDev& E, const Tile
   }
   __syncthreads();
   if (td.kpart) {  // hidden-split layer 0: the batch parts of this tile meet here
-    const uint32_t ep = *GPC(uint32_t, E.sync) + 1u;  // per launch (B and D have their own granules)
+    const uint32_t ep = P ? us->ep : *GPC(uint32_t, E.sync) + 1u;  // per launch (B and D have their own granules)
     if (td.kpart >= 2) {
       AS_G uint64_t* mine = GP(uint64_t, td.part) + (size_t)(td.kpart - 2) * 1024;
       for (int el = tid; el < 1024; el += UT) {
@@ -1124,7 +1205,10 @@ __device__ __forceinline__ void dw_adam_tile(const AS_C EngineDev& E, const Tile
     tn[e] = 0.f;
     if (ok[e]) {
       pn[e] = adam_elem(p[e], m[e], v[e], accs[(el >> 5) * 33 + (el & 31)], w1, b2, w2, bc2s, eps, neg_step);
-      W[idx[e]] = p[e];
+      if (P && polyak && td.N == 1)  // a critic's W2 row: the role workgroups read the fp32 master
+        coh_storef((float*)(W + idx[e]), p[e]);
+      else
+        W[idx[e]] = p[e];
       Wm[idx[e]] = m[e];
       Wv[idx[e]] = v[e];
       if (polyak) {
@@ -1150,13 +1234,26 @@ __device__ __forceinline__ void dw_adam_tile(const AS_C EngineDev& E, const Tile
       GP(float, td.b)[td.n0 + tid] = pb;
     GP(float, td.bm)[td.n0 + tid] = mb;
     GP(float, td.bv)[td.n0 + tid] = vb;
-    if (polyak) GP(float, td.tb)[td.n0 + tid] = tau * pbn + omt * tbv;
+    if (polyak) GP(float, td.tb)[td.n0 + tid] = tau * pbn + omt * tbv;  // read by the next step's launch only
   }
   __syncthreads();
   // ---- packed copies as 16-B pieces: Wc / tWc rows n (EPR consecutive k), WTc rows k
   constexpr int PPR = 32 / EPR;  // pieces per 32-element tile row
   for (int mat = 0; mat < (polyak ? 3 : 2); ++mat) {  // uniform: one buffer descriptor per matrix
     const void* base = mat == 0 ? td.Wc : mat == 1 ? td.WTc : td.tWc;
+    // the fused step reads the online critics' copies in the same launch (phase
+    // C); the targets' only in the next launch: plain write-back stores for those
+    if (P && mat == 2) {
+      for (int i = tid; i < 32 * PPR; i += UT) {
+        const int row = i / PPR, pc = i % PPR;
+        T vv[EPR];
+#pragma unroll
+        for (int j = 0; j < EPR; ++j) vv[j] = MM<T>::cvt(tgts[row * 33 + pc * EPR + j]);
+        coh_store16<false>(base, (uint32_t)(packed_off<T>(td.n0 + row, td.k0 + pc * EPR, td.Kp) * sizeof(T)),
+                           *(const u32x4*)vv);
+      }
+      continue;
+    }
     for (int i = tid; i < 32 * PPR; i += UT) {
       const int row = i / PPR, pc = i % PPR;
       T vv[EPR];
@@ -1177,15 +1274,16 @@ __device__ __forceinline__ void dw_adam_tile(const AS_C EngineDev& E, const Tile
 }
 
 // a tile with summed dY parts (fp32 hidden-split layer 0) runs its own instance
-template <typename T, int UT, bool COH>
+template <typename T, int UT, bool COH, bool P = false, typename Wait = NoWait>
 __device__ __forceinline__ void dw_adam_tile_any(const AS_C EngineDev& E, const TileDesc* tdp_, bool polyak, int par,
-                                                 int par_x, lf* lds) {
+                                                 int par_x, lf* lds, const UpdStep* us = nullptr,
+                                                 const Wait& wait = Wait()) {
   if constexpr (sizeof(T) == 4) {
     const int gs = ((const AS_C TileDesc*)tdp_)->gsum;  // uniform
-    if (gs == 4) return dw_adam_tile<T, UT, COH, 4>(E, tdp_, polyak, par, par_x, lds);
-    if (gs == 2) return dw_adam_tile<T, UT, COH, 2>(E, tdp_, polyak, par, par_x, lds);
+    if (gs == 4) return dw_adam_tile<T, UT, COH, 4, P>(E, tdp_, polyak, par, par_x, lds, us, wait);
+    if (gs == 2) return dw_adam_tile<T, UT, COH, 2, P>(E, tdp_, polyak, par, par_x, lds, us, wait);
   }
-  dw_adam_tile<T, UT, COH, 1>(E, tdp_, polyak, par, par_x, lds);
+  dw_adam_tile<T, UT, COH, 1, P>(E, tdp_, polyak, par, par_x, lds, us, wait);
 }
 
 // One block: reduces the step's loss partials into stats[0..3] and runs the
@@ -1193,24 +1291,32 @@ __device__ __forceinline__ void dw_adam_tile_any(const AS_C EngineDev& E, const 
 // (no early exit: the caller's completion barrier follows).  alpha_state is
 // stored sc1: the critics of a phase A sharing the launch read alpha after the
 // completion counter.
-__device__ __forceinline__ void alpha_and_losses(const AS_C EngineDev& E, int par, lf* red) {
+// P (persistent step): log pi, the loss partials and the alpha state were
+// stored sc1 earlier in the launch: sc1 loads; bc[2] = this step's alpha Adam
+// bias corrections (else read from E.alpha_sc, written by phase A).
+__device__ __forceinline__ double ldd_coh(const double* p) {
+  return __hip_atomic_load((double*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <bool P = false>
+__device__ __forceinline__ void alpha_and_losses(const AS_C EngineDev& E, int par, lf* red, const double* bc = nullptr) {
   const int tid = threadIdx.x, NT = blockDim.x, B = E.B;
   const float H = E.target_entropy;
   AS_G double* st = GP(double, E.alpha_state);
-  const float la32 = (float)st[0];
+  const double st0 = P ? ldd_coh((const double*)st) : st[0];
+  const float la32 = (float)st0;
   const float mB = -1.0f / (float)B;
   const AS_G float* lp = GPC(float, E.lp_st) + par * E.Br;
   const AS_G float* lossp = GPC(float, E.lossp) + par * E.nrt * 4;
   float sg = 0.f, sl = 0.f, l0 = 0.f, l1 = 0.f, l2 = 0.f;
   for (int b = tid; b < B; b += NT) {
-    const float term = lp[b] + H;
+    const float term = ldf<P>((const float*)(lp + b)) + H;
     sg += mB * term;
     sl += la32 * term;
   }
   for (int rt = tid; rt < E.nrt; rt += NT) {
-    l0 += lossp[rt * 4 + 0];
-    l1 += lossp[rt * 4 + 1];
-    l2 += lossp[rt * 4 + 2];
+    l0 += ldf<P>((const float*)(lossp + rt * 4 + 0));
+    l1 += ldf<P>((const float*)(lossp + rt * 4 + 1));
+    l2 += ldf<P>((const float*)(lossp + rt * 4 + 2));
   }
   red[0 * NT + tid] = sg;
   red[1 * NT + tid] = sl;
@@ -1232,11 +1338,13 @@ __device__ __forceinline__ void alpha_and_losses(const AS_C EngineDev& E, int pa
     if (E.auto_entropy && E.alpha_update) {
       const double gr = (double)red[0];
       const double b1 = (double)E.beta1, b2 = (double)E.beta2;
-      const double m = st[2] + (1.0 - b1) * (gr - st[2]);
-      const double v = st[3] * b2 + (1.0 - b2) * gr * gr;
-      const double bc1 = GPC(double, E.alpha_sc)[par * 2], bc2 = GPC(double, E.alpha_sc)[par * 2 + 1];
+      const double st2 = P ? ldd_coh((const double*)st + 2) : st[2], st3 = P ? ldd_coh((const double*)st + 3) : st[3];
+      const double m = st2 + (1.0 - b1) * (gr - st2);
+      const double v = st3 * b2 + (1.0 - b2) * gr * gr;
+      const double bc1 = P ? bc[0] : GPC(double, E.alpha_sc)[par * 2];
+      const double bc2 = P ? bc[1] : GPC(double, E.alpha_sc)[par * 2 + 1];
       const double denom = sqrt(v) / sqrt(bc2) + (double)E.adam_eps;
-      const double la = st[0] + (-(E.alpha_lr / bc1)) * m / denom;
+      const double la = st0 + (-(E.alpha_lr / bc1)) * m / denom;
       double* sd = (double*)E.alpha_state;
       __hip_atomic_store(sd + 0, la, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(sd + 1, exp(la), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1507,11 +1615,18 @@ __device__ __forceinline__ void gather_rows(const sac_replay& rb, const AS_L int
 // Stager block (phase C): step t+1's rows of row tile rbi into E.stg.  Phase C
 // is the step's last reader of the previous record (phase A of step t consumed
 // it before this launch began); the next launch sees the stores.
-__device__ __forceinline__ void stage_next_batch(const AS_C EngineDev& E, const sac_replay& rb, int rbi, lf* lds) {
+// The record of step s is slot s & 1 (stage_rec): the stager of step t + 1
+// never overwrites the record step t's phase A reads (the fused step stages
+// inside the same launch as that phase A).
+__device__ __forceinline__ size_t stage_rec(const AS_C EngineDev& E, uint64_t step, int rbi) {
+  return ((size_t)(step & 1) * E.nrt + rbi) * E.stg_stride;
+}
+__device__ __forceinline__ void stage_next_batch(const AS_C EngineDev& E, const sac_replay& rb, int rbi, lf* lds,
+                                                 uint64_t cur_step) {
   constexpr int R = SAC_ROWS;
-  const uint64_t step = *GPC(uint64_t, E.rng_step) + 1;  // advanced at the end of this launch
+  const uint64_t step = cur_step + 1;  // the batch is step t + 1's
   const int64_t rb_size = GPC(int64_t, rb.state)[0], rb_pos = GPC(int64_t, rb.state)[1];
-  AS_G float* rec = GP(float, E.stg) + (size_t)rbi * E.stg_stride;
+  AS_G float* rec = GP(float, E.stg) + stage_rec(E, step, rbi);
   AS_G uint64_t* hdr = (AS_G uint64_t*)rec;
   if (rb_size < E.B) {  // nothing to sample: leave no matching record
     if (threadIdx.x == 0) hdr[0] = ~0ull;
@@ -1650,7 +1765,7 @@ __device__ __forceinline__ void target_critic_body(const EngineDev* __restrict__
   bool staged = false;
   if (E.stage && !inj_idx) {  // the record phase C staged for this step: copied speculatively,
     // its loads in flight together with the step / replay-state loads above
-    const AS_G float* rec = GPC(float, E.stg) + (size_t)rbi * E.stg_stride;
+    const AS_G float* rec = GPC(float, E.stg) + stage_rec(E, step, rbi);
     const AS_C uint64_t* hdr = (const AS_C uint64_t*)rec;
     const AS_G float* p = rec + 16;
     if (late_ph1) {  // uniform: the record's loads, then layer 1's fragments, then the record's stores
@@ -2237,7 +2352,7 @@ __global__ void __launch_bounds__(SAC_THREADS) sac_actor(const EngineDev* __rest
                                        (lf*)lds_raw);
     count_done((uint32_t*)E.sync + SYNC_BDONE + 16 * (td.opt - 1));
   } else if (bid >= nrole) {
-    stage_next_batch(E, rb, bid - nrole, (lf*)lds_raw);
+    stage_next_batch(E, rb, bid - nrole, (lf*)lds_raw, *GPC(uint64_t, E.rng_step));
   } else {
     actor_body<T, ROLES, WITH_B>(Ep, bid);
   }

@@ -283,11 +283,16 @@ __device__ __forceinline__ void gemm_ksplit(const lf* __restrict__ A, int lda, c
 }
 
 // ---------------------------------------------------------------------------- phase A
-template <typename T>
+// P (fused step, sac_persist.h): bidA and the step context come from the
+// fused launch, and everything the role hands to workgroups of the launch's
+// later phases is stored sc1 (their loads are sc1).  Phase A opens the launch,
+// so its inputs (the previous launch's weights, the batch staged for it) need
+// no wait.
+template <typename T, bool P = false, typename RoleWait = NoWait>
 __device__ __forceinline__ void target_critic_split_body(const EngineDev* __restrict__ Ep, const sac_replay& rb,
                                                          const int32_t* __restrict__ inj_idx_,
-                                                         const float* __restrict__ inj_eps_) {
-  PREFETCH_ARG(Ep);
+                                                         const float* __restrict__ inj_eps_, int bidA,
+                                                         const StepCtx& sc, const RoleWait& role_wait = RoleWait()) {
   const AS_C EngineDev& E = *(const AS_C EngineDev*)Ep;
   extern __shared__ float lds_raw[];
   lf* lds = (lf*)lds_raw;
@@ -300,7 +305,6 @@ __device__ __forceinline__ void target_critic_split_body(const EngineDev* __rest
   // blocks: pi(s') as WP parts x nrt, then roles 1..5 as 2 halves x nrt each
   constexpr int WP = split_wpi(sizeof(T));
   const int n2 = 2 * E.nrt, n0 = WP * E.nrt;
-  const int bidA = (int)blockIdx.x;
   const int grp = bidA < n0 ? 0 : 1 + (bidA - n0) / n2;
   const int idx = bidA < n0 ? bidA : (bidA - n0) % n2;
   const int h = bidA < n0 ? idx % WP : idx & 1, rbi = bidA < n0 ? idx / WP : idx >> 1;
@@ -326,7 +330,7 @@ __device__ __forceinline__ void target_critic_split_body(const EngineDev* __rest
   const int B = E.B, Bp = E.Bp, O = E.O, A = E.A, ld = E.ld, ldo = E.ldo;
   const int r0 = rbi * R;
   const int nvalid = min(R, B - r0);
-  const uint32_t ep = *GPC(uint32_t, E.sync) + 1u;
+  const uint32_t ep = sc.ep;
   const AS_G int32_t* inj_idx = GPC(int32_t, inj_idx_);
   const AS_G float* inj_eps = GPC(float, inj_eps_);
   lf* Xb = lds + E.o_X;           // layer-0 input [R][ld]; later dY0 partial
@@ -350,12 +354,12 @@ __device__ __forceinline__ void target_critic_split_body(const EngineDev* __rest
   AS_L int64_t* slotB = (AS_L int64_t*)(lds + E.o_slot);
   AS_G float* stats = GP(float, E.stats);
 
-  const uint64_t step = *GPC(uint64_t, E.rng_step);
-  const int par = (int)(step & 1);
+  const uint64_t step = sc.step;
+  const int par = sc.par;
 #ifndef SAC_ADAM_LAST
 #define SAC_ADAM_LAST 1
 #endif
-  const bool adam_blk = SAC_ADAM_LAST ? (role == 5 && rbi == E.nrt - 1 && h == 1) : (role == 0 && rbi == 0 && h == 0);
+  const bool adam_blk = !P && (SAC_ADAM_LAST ? (role == 5 && rbi == E.nrt - 1 && h == 1) : (role == 0 && rbi == 0 && h == 0));
   if (adam_blk && tid < 4 && (tid < 3 || (E.auto_entropy && E.alpha_update))) {
     // optimizer step counters and this step's Adam bias corrections (torch adam.py), read
     // by phases B and D only: done by the last pi(s) workgroup, off the y chain (a load
@@ -376,7 +380,7 @@ __device__ __forceinline__ void target_critic_split_body(const EngineDev* __rest
   bool staged = false;
   bool h1_issued = false;
   if (E.stage && !inj_idx) {
-    const AS_G float* rec = GPC(float, E.stg) + (size_t)rbi * E.stg_stride;
+    const AS_G float* rec = GPC(float, E.stg) + stage_rec(E, step, rbi);
     const AS_C uint64_t* hdr = (const AS_C uint64_t*)rec;
     const AS_G float* p = rec + 16;
     constexpr int NS = (R * 32 + SAC_THREADS - 1) / SAC_THREADS;
@@ -458,6 +462,7 @@ __device__ __forceinline__ void target_critic_split_body(const EngineDev* __rest
     }
   }
   __syncthreads();
+  if constexpr (P) role_wait(role);  // the fused step's hook (phase A waits for nothing: it opens the launch)
   STAMP(1);
 
   // pi's squashed-Gaussian head (models.py:79-87) from two layer-2 partials:
@@ -467,12 +472,12 @@ __device__ __forceinline__ void target_critic_split_body(const EngineDev* __rest
   // (outB) and the peer half's granules g1, in half order
   auto head = [&](const AS_G uint64_t* g0, const AS_G uint64_t* g1, bool tgt, lf* actB, lf* lpOut, bool stash) {
     const AS_C NetDev& pn = E.net[NET_PI];
-    const AS_G float* b2 = GPC(float, pn.l[2].bias);
+    const float* b2 = pn.l[2].bias;
     const int AP = A <= 1 ? 1 : 1 << (32 - __builtin_clz(A - 1));
     const int rpp = SAC_THREADS / AP;
     const int jj = tid % AP;
     // this lane's head biases, loaded before the polls (not one more round trip after them)
-    const float b2mu = jj < A ? b2[jj] : 0.f, b2ls = jj < A ? b2[A + jj] : 0.f;
+    const float b2mu = jj < A ? ldf<P>(b2 + jj) : 0.f, b2ls = jj < A ? ldf<P>(b2 + A + jj) : 0.f;
     for (int base = 0; base < R; base += rpp) {
       const int r = base + tid / AP, j = jj;
       const bool live = r < R && j < A;
@@ -518,12 +523,12 @@ __device__ __forceinline__ void target_critic_split_body(const EngineDev* __rest
         actB[r * A + j] = act_v;
         if (stash) {
           const int b = r0 + r;
-          AS_G float* hs = GP(float, E.head_st) + (size_t)b * 4 * A;
-          hs[j] = mu;
-          hs[A + j] = lsr;
-          hs[2 * A + j] = z;
-          hs[3 * A + j] = e;
-          GP(float, E.a_st)[(size_t)b * A + j] = act_v;
+          float* hs = E.head_st + (size_t)b * 4 * A;
+          st_f<P>(hs + j, mu);
+          st_f<P>(hs + A + j, lsr);
+          st_f<P>(hs + 2 * A + j, z);
+          st_f<P>(hs + 3 * A + j, e);
+          st_f<P>(E.a_st + (size_t)b * A + j, act_v);
         }
       }
       for (int o = 1; o < AP; o <<= 1) {
@@ -540,7 +545,7 @@ __device__ __forceinline__ void target_critic_split_body(const EngineDev* __rest
   auto forward01 = [&](bool keepP, bool stXT, bool pi_actor, auto&& after_l1) {
     // layer 0: X [R][Kp0] -> P0 / H0 [R][H]
     const int act = net.hid_act;
-    gemm_hs<T, 2, HC0>(Xb, ld, w0, &h0, [&](int j, int col, const f32x4& acc) {
+    gemm_hs<T, 2, HC0, P>(Xb, ld, w0, &h0, [&](int j, int col, const f32x4& acc) {
       const bool nv = col < L0.N;
       const float bn = h0.b[j];
 #pragma unroll
@@ -554,15 +559,15 @@ __device__ __forceinline__ void target_critic_split_body(const EngineDev* __rest
     if (act != ACT_RELU && act != ACT_ID) act_pass_fwd<R>(H0, ld, L0.Np >> 4, act);
     __syncthreads();
     if (pi_actor && h == 0) {  // pi's layer-0 pre-activations for phase C's relu masks
-      AS_G float* ps = GP(float, L0.pstash) + (size_t)r0 * L0.Np;
-      for (int i = tid; i < R * L0.Np; i += SAC_THREADS) ps[i] = P0[(i / L0.Np) * ldp0 + i % L0.Np];
+      float* ps = L0.pstash + (size_t)r0 * L0.Np;
+      for (int i = tid; i < R * L0.Np; i += SAC_THREADS) st_f<P>(ps + i, P0[(i / L0.Np) * ldp0 + i % L0.Np]);
     }
     if (stXT && h == 0)
-      store_T<T, R>(H0, ld, L1.Kp, L1.K, (T*)L1.XT + (pi_actor ? par * L1.xt_par : 0), Bp, r0, nvalid, nullptr);
+      store_T<T, R, P>(H0, ld, L1.Kp, L1.K, (T*)L1.XT + (pi_actor ? par * L1.xt_par : 0), Bp, r0, nvalid, nullptr);
     STAMP(2);
-    if (sizeof(T) == 4 && !kh2.ok) ks_issue<T>(kh2, w2n);  // fp32: under layer 1 (target critics: before the poll)
+    if (sizeof(T) == 4 && !kh2.ok) ks_issue<T, KsHeld<T>::MAXC, P>(kh2, w2n);  // fp32: under layer 1 (target critics: before the poll)
     // layer 1, this half: H0 -> P1 / H1 [R][HH]
-    gemm_hs<T, 1, NCH_H>(H0, ld, w1, &h1, [&](int j, int col, const f32x4& acc) {
+    gemm_hs<T, 1, NCH_H, P>(H0, ld, w1, &h1, [&](int j, int col, const f32x4& acc) {
       const float bn = h1.b[j];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
@@ -576,15 +581,15 @@ __device__ __forceinline__ void target_critic_split_body(const EngineDev* __rest
     if (act != ACT_RELU && act != ACT_ID) act_pass_fwd<R>(H1, ldh1, HHr >> 4, act);
     __syncthreads();
     if (pi_actor) {  // this half's layer-1 pre-activations
-      AS_G float* ps = GP(float, L1.pstash) + (size_t)r0 * L1.Np + h * HH;
-      for (int i = tid; i < R * HH; i += SAC_THREADS) ps[(i / HH) * L1.Np + i % HH] = P1[(i / HH) * ldp1 + i % HH];
+      float* ps = L1.pstash + (size_t)r0 * L1.Np + h * HH;
+      for (int i = tid; i < R * HH; i += SAC_THREADS) st_f<P>(ps + (i / HH) * L1.Np + i % HH, P1[(i / HH) * ldp1 + i % HH]);
     }
     if (stXT)  // layer 2's input, this half's rows of X^T
-      store_T<T, R>(H1, ldh1, HH, HH, (T*)L2.XT + (pi_actor ? par * L2.xt_par : 0) + (size_t)h * HH * Bp, Bp, r0,
-                    nvalid, nullptr);
+      store_T<T, R, P>(H1, ldh1, HH, HH, (T*)L2.XT + (pi_actor ? par * L2.xt_par : 0) + (size_t)h * HH * Bp, Bp, r0,
+                       nvalid, nullptr);
     STAMP(3);
     // layer 2, this half's partial sum: outB [R][Np2]
-    gemm_ksplit<T, false, decltype(kh2)::MAXC>(H1, ldh1, w2n, red, outB, ldo, &kh2);
+    gemm_ksplit<T, P, decltype(kh2)::MAXC>(H1, ldh1, w2n, red, outB, ldo, &kh2);
     STAMP(4);
   };
 
@@ -598,6 +603,8 @@ __device__ __forceinline__ void target_critic_split_body(const EngineDev* __rest
     __syncthreads();
   };
 
+  // alpha (agent.py:203): the previous step's phase D wrote it (the previous
+  // launch, also in the fused step)
   const float alpha32 = (float)*GPC(double, E.alpha_state + 1);
   if (role == 0) {
     // ---- pi(s'): the critical path's head
@@ -609,24 +616,24 @@ __device__ __forceinline__ void target_critic_split_body(const EngineDev* __rest
   } else if (role == 5) {
     // ---- pi(s): the actor sample for phase C (stashes), X^T of pi's layers
     if (h == 0)
-      for (int i = tid; i < R * O; i += SAC_THREADS) GP(float, E.s_st)[(size_t)r0 * O + i] = sB[i];
+      for (int i = tid; i < R * O; i += SAC_THREADS) st_f<P>(E.s_st + (size_t)r0 * O + i, sB[i]);
     build_x(sB, aB, 0);
     // layer-0 input X^T: both halves store it (columns h Bp + r0: the partial dW layout)
-    store_T<T, R>(Xb, ld, L0.Kp, L0.K, (T*)L0.XT + par * L0.xt_par, 2 * Bp, h * Bp + r0, nvalid, nullptr);
+    store_T<T, R, P>(Xb, ld, L0.Kp, L0.K, (T*)L0.XT + par * L0.xt_par, 2 * Bp, h * Bp + r0, nvalid, nullptr);
     forward01(true, true, true, no_hook);
     AS_G uint64_t* g = gs_at(E, GS_PS, rbi, h);
     for (int i = tid; i < R * 2 * A; i += SAC_THREADS) gran_put(g + i, outB[(i / (2 * A)) * ldo + i % (2 * A)], ep);
     head(nullptr, gs_at(E, GS_PS, rbi, 1 - h), false, a2B, lpB, h == 0);
     if (h == 0 && tid < nvalid) {
       const int b = r0 + tid;
-      GP(float, E.lp_st)[par * E.Br + b] = lpB[tid];
+      st_f<P>(E.lp_st + par * E.Br + b, lpB[tid]);
       stats[4 + B + b] = lpB[tid];
     }
     STAMP(6);
   } else if (role == 1 || role == 2) {
     // ---- target critic t (agent.py:195-211): a~', log pi' from pi(s')'s two partials
     const int t = role - 1;
-    if (sizeof(T) == 4) ks_issue<T>(kh2, w2n);
+    if (sizeof(T) == 4) ks_issue<T, KsHeld<T>::MAXC, P>(kh2, w2n);
     head(gs_at(E, GS_PI, rbi, 0), nullptr, true, a2B, lpB, false);
     if (t == 0 && h == 0 && tid < R) gran_put(gs_at(E, GS_LP, rbi, 0) + tid, lpB[tid], ep);
     STAMP(7);
@@ -643,14 +650,14 @@ __device__ __forceinline__ void target_critic_split_body(const EngineDev* __rest
     // bf16: held from the start too; fp32 (no register room: 51 VGPRs would
     // spill) issued as soon as layer 1's forward GEMM has freed h1's registers.
     // W2's element for this thread's column n = tid % HH
-    if constexpr (sizeof(T) == 2) ht_issue<T, 2, NCH_HH>(ht1, wt1);
+    if constexpr (sizeof(T) == 2) ht_issue<T, 2, NCH_HH, P>(ht1, wt1);
     static_assert(SAC_THREADS % SPLIT_HH == 0, "one W2 column per thread in the unit-seed loop");
-    const float w2n = GPC(float, net.P + L2.w_off)[h * HH + tid % HH];  // W2 [1][H] fp32 master
+    const float w2n = ldf<P>(net.P + L2.w_off + h * HH + tid % HH);  // W2 [1][H] fp32 master
     build_x(sB, aB, A);
     // layer-0 input X^T is shared by Q1 and Q2: Q1's halves store it (columns h Bp + r0)
-    if (qi == 0) store_T<T, R>(Xb, ld, L0.Kp, L0.K, L0.XT, 2 * Bp, h * Bp + r0, nvalid, nullptr);
+    if (qi == 0) store_T<T, R, P>(Xb, ld, L0.Kp, L0.K, L0.XT, 2 * Bp, h * Bp + r0, nvalid, nullptr);
     forward01(true, true, false, [&] {
-      if constexpr (sizeof(T) == 4) ht_issue<T, 2, NCH_HH>(ht1, wt1);
+      if constexpr (sizeof(T) == 4) ht_issue<T, 2, NCH_HH, P>(ht1, wt1);
     });
     if (tid < R) gran_put(gs_at(E, qi ? GS_QA2 : GS_QA1, rbi, h) + tid, outB[tid * ldo], ep);
     // unit-seed backward (every layer's dY is linear in the row's seed 2(q - y)/B):
@@ -661,7 +668,7 @@ __device__ __forceinline__ void target_critic_split_body(const EngineDev* __rest
         U1[r * ldu1 + n] = act_bwd(net.hid_act, P1[r * ldp1 + n], w2n);
       }
       __syncthreads();
-      gemm_hs<T, 2, NCH_HH>(U1, ldu1, wt1, &ht1, [&](int j, int col, const f32x4& acc) {
+      gemm_hs<T, 2, NCH_HH, P>(U1, ldu1, wt1, &ht1, [&](int j, int col, const f32x4& acc) {
         const bool kv = col < L1.K;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
@@ -680,18 +687,21 @@ __device__ __forceinline__ void target_critic_split_body(const EngineDev* __rest
       // fp32: layers 1 and 0's unit-seed dY^T stored now, while y is still on its
       // way; phase B scales each batch column by its row's seed (E.seedq) as it
       // stages them, and sums their bias gradients itself
-      store_T<T, R>(U1, ldu1, HH, HH, (T*)L1.GT + (size_t)h * HH * Bp, Bp, r0, nvalid, nullptr);
-      store_T<T, R>(Xb, ld, L0.Np, L0.N, L0.GT, 2 * Bp, h * Bp + r0, nvalid, nullptr);
+      store_T<T, R, P>(U1, ldu1, HH, HH, (T*)L1.GT + (size_t)h * HH * Bp, Bp, r0, nvalid, nullptr);
+      store_T<T, R, P>(Xb, ld, L0.Np, L0.N, L0.GT, 2 * Bp, h * Bp + r0, nvalid, nullptr);
     }
+    // fused step: the operands phase B can fetch before y is known are stored
+    // (fp32: X^T and the unit-seed dY^T of layers 0 / 1)
+    if constexpr (P) role_wait(-1);
     if (tid < 64) {  // wave 0: q, y, loss partial, seed dL/dq = 2(q - y)/B  (mse_loss backward)
       float sq = 0.f;
       if (tid < R) {
         const int b = r0 + tid;
         const bool v = tid < nvalid;
-        const float b2 = GPC(float, L2.bias)[0];
+        const float b2 = ldf<P>(L2.bias);
         const AS_C NetDev& t1 = E.net[NET_Q1T];
         const AS_C NetDev& t2 = E.net[NET_Q2T];
-        const float bt1 = GPC(float, t1.l[2].bias)[0], bt2 = GPC(float, t2.l[2].bias)[0];  // before the poll
+        const float bt1 = ldf<P>(t1.l[2].bias), bt2 = ldf<P>(t2.l[2].bias);  // before the poll
         const float mine = outB[tid * ldo];
         // every granule this row needs, polled together: peer half's q partial,
         // both target critics' two halves, log pi(a'|s')
@@ -716,10 +726,10 @@ __device__ __forceinline__ void target_critic_split_body(const EngineDev* __rest
         float seed = v ? (2.0f / (float)B) * d : 0.f;
         if (net.out_act != ACT_ID) seed = act_bwd(net.out_act, qpre, seed);
         qtB[tid] = seed;
-        if (sizeof(T) == 4 && h == 0) GP(float, E.seedq)[qi * Bp + b] = seed;
+        if (sizeof(T) == 4 && h == 0) st_f<P>(E.seedq + qi * Bp + b, seed);
       }
       sq = wave_sum(sq);
-      if (tid == 0 && h == 0) GP(float, E.lossp)[(par * E.nrt + rbi) * 4 + qi] = sq;
+      if (tid == 0 && h == 0) st_f<P>(E.lossp + (par * E.nrt + rbi) * 4 + qi, sq);
     }
     __syncthreads();
     STAMP(15);
@@ -728,11 +738,11 @@ __device__ __forceinline__ void target_critic_split_body(const EngineDev* __rest
       lf* g2 = outB;
       for (int i = tid; i < R * 32; i += SAC_THREADS) g2[(i / 32) * ldo + i % 32] = (i % 32) == 0 ? 1.f : 0.f;
       __syncthreads();
-      store_T<T, R>(g2, ldo, L2.Np, L2.N, L2.GT, Bp, r0, nvalid, L2.dbp, qtB);
+      store_T<T, R, P>(g2, ldo, L2.Np, L2.N, L2.GT, Bp, r0, nvalid, L2.dbp, qtB);
     }
     if constexpr (sizeof(T) == 2) {
-      store_T<T, R>(U1, ldu1, HH, HH, (T*)L1.GT + (size_t)h * HH * Bp, Bp, r0, nvalid, L1.dbp + h * HH, qtB, L1.N);
-      store_T<T, R>(Xb, ld, L0.Np, L0.N, L0.GT, 2 * Bp, h * Bp + r0, nvalid, L0.dbp, qtB);
+      store_T<T, R, P>(U1, ldu1, HH, HH, (T*)L1.GT + (size_t)h * HH * Bp, Bp, r0, nvalid, L1.dbp + h * HH, qtB, L1.N);
+      store_T<T, R, P>(Xb, ld, L0.Np, L0.N, L0.GT, 2 * Bp, h * Bp + r0, nvalid, L0.dbp, qtB);
     }
     STAMP(11 + 2 * qi);
   }
@@ -742,15 +752,24 @@ template <typename T>
 __global__ void __launch_bounds__(SAC_THREADS) sac_target_critic_split(const EngineDev* __restrict__ Ep, sac_replay rb,
                                                                         const int32_t* __restrict__ inj_idx_,
                                                                         const float* __restrict__ inj_eps_) {
-  target_critic_split_body<T>(Ep, rb, inj_idx_, inj_eps_);
+  PREFETCH_ARG(Ep);
+  const AS_C EngineDev& E0 = *(const AS_C EngineDev*)Ep;
+  const uint64_t step = *GPC(uint64_t, E0.rng_step);
+  const StepCtx sc{step, *GPC(uint32_t, E0.sync) + 1u, (int)(step & 1)};
+  target_critic_split_body<T>(Ep, rb, inj_idx_, inj_eps_, (int)blockIdx.x, sc);
   const AS_C EngineDev& E = *(const AS_C EngineDev*)Ep;
   (void)E;
   END_STAMP(60);
 }
 
 // ---------------------------------------------------------------------------- phase C
-template <typename T>
-__device__ __forceinline__ void actor_split_body(const EngineDev* __restrict__ Ep, int bid) {
+// P (persistent step): wait(0) = pi(s) of this step done (the stashes), wait(1 +
+// qi) = critic qi updated by this step's phase B, wait(3) = both critics
+// updated; every load of data written earlier in the launch is sc1, and what
+// phase D reads is stored sc1.
+template <typename T, bool P = false, typename CWait = NoWait>
+__device__ __forceinline__ void actor_split_body(const EngineDev* __restrict__ Ep, int bid, const StepCtx& sc,
+                                                 const CWait& wait = CWait()) {
   const AS_C EngineDev& E = *(const AS_C EngineDev*)Ep;
   extern __shared__ float lds_raw[];
   lf* lds = (lf*)lds_raw;
@@ -771,8 +790,8 @@ __device__ __forceinline__ void actor_split_body(const EngineDev* __restrict__ E
   const int B = E.B, Bp = E.Bp, O = E.O, A = E.A, ld = E.ld, ldo = E.ldo;
   const int r0 = rbi * R;
   const int nvalid = min(R, B - r0);
-  const uint32_t ep = *GPC(uint32_t, E.sync) + 1u;
-  const int par = (int)(*GPC(uint64_t, E.rng_step) & 1);
+  const uint32_t ep = sc.ep;
+  const int par = sc.par;
   lf* Xb = lds + E.o_X;
   lf* H0 = lds + E.o_Y;
   lf* P0 = lds + E.o_P1[0];
@@ -789,7 +808,7 @@ __device__ __forceinline__ void actor_split_body(const EngineDev* __restrict__ E
   lf* goutB = lds + E.o_gout;
   lf* g1B = lds + E.o_g;
   lf* g2B = lds + E.o_g2;
-  const float alpha32 = (float)*GPC(double, E.alpha_state + 1);
+  const float alpha32 = (float)*GPC(double, E.alpha_state + 1);  // the previous launch's phase D
 
   if (!is_pi) {
     // ---- critic qi on (s, a~) with the UPDATED weights (agent.py:244-248), then d Q / d a~
@@ -801,13 +820,15 @@ __device__ __forceinline__ void actor_split_body(const EngineDev* __restrict__ E
     const GemmW w1 = gw_sub<T>(L1.Wc, L1.Kp, h * HH, HH, 0, L1.Kp, L1.bias + h * HH, HH);
     HTiles<T, 2, HC0> h0;
     HTiles<T, 1, NCH_H> h1;
-    ht_issue<T, 2, HC0>(h0, w0);
-    ht_issue<T, 1, NCH_H>(h1, w1);
     // layer-1 dX operand of this half, held from the start as well (its fetch
     // would otherwise sit between the forward pass and the backward GEMM)
     const GemmW wt1 = gw_sub<T>(L1.WTc, L1.Np, 0, L1.Kp, h * HH, HH, nullptr, 0);
     HTiles<T, 2, NCH_HH> ht1;
-    ht_issue<T, 2, NCH_HH>(ht1, wt1);
+    if constexpr (!P) {
+      ht_issue<T, 2, HC0>(h0, w0);
+      ht_issue<T, 1, NCH_H>(h1, w1);
+      ht_issue<T, 2, NCH_HH>(ht1, wt1);
+    }
     // the two k-split steps of the critic's chain (layer 2's partial q, then
     // layer 0's dX for the action columns) read weights phase B has just
     // written: held (issued behind the inputs), not a cold round trip each
@@ -821,12 +842,24 @@ __device__ __forceinline__ void actor_split_body(const EngineDev* __restrict__ E
     kc2.ok = kc0.ok = false;
     // the W2 (fp32 master) element of this thread's column n = tid % HH of the unit-seed backward
     static_assert(SAC_THREADS % HH == 0, "one W2 column per thread in the unit-seed loop");
-    const float w2n = GPC(float, net.P + L2.w_off)[h * HH + tid % HH];
-    for (int i = tid; i < R * O; i += SAC_THREADS) sB[i] = GPC(float, E.s_st)[(size_t)r0 * O + i];
-    for (int i = tid; i < R * A; i += SAC_THREADS) aB[i] = GPC(float, E.a_st)[(size_t)r0 * A + i];
+    float w2n = 0.f;
+    if constexpr (P) {  // the stashes of pi(s), then (once phase B has updated this critic) its weights
+      wait(0);
+      for (int i = tid; i < R * O; i += SAC_THREADS) sB[i] = ldf<true>(E.s_st + (size_t)r0 * O + i);
+      for (int i = tid; i < R * A; i += SAC_THREADS) aB[i] = ldf<true>(E.a_st + (size_t)r0 * A + i);
+      wait(1 + qi);
+      ht_issue<T, 2, HC0, true>(h0, w0);
+      ht_issue<T, 1, NCH_H, true>(h1, w1);
+      ht_issue<T, 2, NCH_HH, true>(ht1, wt1);
+      w2n = ldf<true>(net.P + L2.w_off + h * HH + tid % HH);
+    } else {
+      w2n = GPC(float, net.P + L2.w_off)[h * HH + tid % HH];
+      for (int i = tid; i < R * O; i += SAC_THREADS) sB[i] = GPC(float, E.s_st)[(size_t)r0 * O + i];
+      for (int i = tid; i < R * A; i += SAC_THREADS) aB[i] = GPC(float, E.a_st)[(size_t)r0 * A + i];
+    }
     if (SAC_KS_C) {  // behind the inputs: waiting for s / a~ must not wait for these (loads retire in order)
-      ks_issue<T>(kc2, w2);
-      if (sizeof(T) == 2) ks_issue<T>(kc0, wt0);  // fp32: after layer 1 (its held W1 part is dead then; from here it spilled)
+      ks_issue<T, decltype(kc2)::MAXC, P>(kc2, w2);
+      if (sizeof(T) == 2) ks_issue<T, decltype(kc0)::MAXC, P>(kc0, wt0);  // fp32: after layer 1 (its held W1 part is dead then; from here it spilled)
     }
     __syncthreads();
     const int Kp0 = L0.Kp;
@@ -837,7 +870,7 @@ __device__ __forceinline__ void actor_split_body(const EngineDev* __restrict__ E
     __syncthreads();
     STAMP(33);
     const int act = net.hid_act;
-    gemm_hs<T, 2, HC0>(Xb, ld, w0, &h0, [&](int j, int col, const f32x4& acc) {
+    gemm_hs<T, 2, HC0, P>(Xb, ld, w0, &h0, [&](int j, int col, const f32x4& acc) {
       const bool nv = col < L0.N;
       const float bn = h0.b[j];
 #pragma unroll
@@ -850,7 +883,7 @@ __device__ __forceinline__ void actor_split_body(const EngineDev* __restrict__ E
     });
     if (act != ACT_RELU && act != ACT_ID) act_pass_fwd<R>(H0, ld, L0.Np >> 4, act);
     __syncthreads();
-    gemm_hs<T, 1, NCH_H>(H0, ld, w1, &h1, [&](int j, int col, const f32x4& acc) {
+    gemm_hs<T, 1, NCH_H, P>(H0, ld, w1, &h1, [&](int j, int col, const f32x4& acc) {
       const float bn = h1.b[j];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
@@ -860,10 +893,10 @@ __device__ __forceinline__ void actor_split_body(const EngineDev* __restrict__ E
         H1[r * ldh1 + col] = act == ACT_RELU ? (p > 0.f ? p : 0.f) : p;
       }
     });
-    if (SAC_KS_C && sizeof(T) == 4) ks_issue<T>(kc0, wt0);
+    if (SAC_KS_C && sizeof(T) == 4) ks_issue<T, decltype(kc0)::MAXC, P>(kc0, wt0);
     if (act != ACT_RELU && act != ACT_ID) act_pass_fwd<R>(H1, ldh1, HH >> 4, act);
     __syncthreads();
-    gemm_ksplit<T, false, decltype(kc2)::MAXC>(H1, ldh1, w2, red, outB, ldo, &kc2);  // partial q
+    gemm_ksplit<T, P, decltype(kc2)::MAXC>(H1, ldh1, w2, red, outB, ldo, &kc2);  // partial q
     STAMP(36 + qi);
     // unit-seed backward down to a~ (the pi role applies the min-Q weights and act'(q))
     {
@@ -872,7 +905,7 @@ __device__ __forceinline__ void actor_split_body(const EngineDev* __restrict__ E
         U1[r * ldu1 + n] = act_bwd(act, P1[r * ldp1 + n], w2n);
       }
       __syncthreads();
-      gemm_hs<T, 2, NCH_HH>(U1, ldu1, wt1, &ht1, [&](int j, int col, const f32x4& acc) {
+      gemm_hs<T, 2, NCH_HH, P>(U1, ldu1, wt1, &ht1, [&](int j, int col, const f32x4& acc) {
         const bool kv = col < L1.K;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
@@ -885,7 +918,7 @@ __device__ __forceinline__ void actor_split_body(const EngineDev* __restrict__ E
       if (act != ACT_RELU && act != ACT_ID) act_pass_bwd<R>(Xb, ld, P0, ldp0, L1.Kp >> 4, L1.K, act);
       __syncthreads();
       // dX of layer 0 for the action columns: the 16-row tiles of W0^T holding [O, O + A)
-      gemm_ksplit<T, false, decltype(kc0)::MAXC>(Xb, ld, wt0, red, H0, ld, &kc0);  // H0 [R][k1 - k0]: partial dX0
+      gemm_ksplit<T, P, decltype(kc0)::MAXC>(Xb, ld, wt0, red, H0, ld, &kc0);  // H0 [R][k1 - k0]: partial dX0
       AS_G uint64_t* g = gs_at(E, GS_C1 + qi, rbi, h);
       for (int i = tid; i < R * A; i += SAC_THREADS) gran_put(g + i, H0[(i / A) * ld + (O - k0) + i % A], ep);
       if (tid < R) gran_put(g + R * A + tid, outB[tid * ldo], ep);
@@ -905,24 +938,28 @@ __device__ __forceinline__ void actor_split_body(const EngineDev* __restrict__ E
   const GemmW wt1 = gw_sub<T>(L1.WTc, L1.Np, 0, L1.Kp, h * HH, HH, nullptr, 0);
   HTiles<T, 1, NCH_32> ht2;
   HTiles<T, 2, NCH_HH> ht1;
-  ht_issue<T, 1, NCH_32>(ht2, wt2);
-  ht_issue<T, 2, NCH_HH>(ht1, wt1);
+  if (P) wait(0);  // pi(s) of this step: its stashes (and, before it, the phase D that wrote pi's weights)
+  ht_issue<T, 1, NCH_32, P>(ht2, wt2);
+  ht_issue<T, 2, NCH_HH, P>(ht1, wt1);
   {  // relu masks: pi's pre-activations stashed by phase A's pi(s) role
-    const AS_G float* p0 = GPC(float, L0.pstash) + (size_t)r0 * L0.Np;
-    for (int i = tid; i < R * L0.Np; i += SAC_THREADS) P0[(i / L0.Np) * ldp0 + i % L0.Np] = p0[i];
-    const AS_G float* p1 = GPC(float, L1.pstash) + (size_t)r0 * L1.Np + h * HH;
-    for (int i = tid; i < R * HH; i += SAC_THREADS) P1[(i / HH) * ldp1 + i % HH] = p1[(i / HH) * L1.Np + i % HH];
-    if (tid < R) lpB[tid] = GPC(float, E.lp_st)[par * E.Br + r0 + tid];
+    const float* p0 = L0.pstash + (size_t)r0 * L0.Np;
+    for (int i = tid; i < R * L0.Np; i += SAC_THREADS) P0[(i / L0.Np) * ldp0 + i % L0.Np] = ldf<P>(p0 + i);
+    const float* p1 = L1.pstash + (size_t)r0 * L1.Np + h * HH;
+    for (int i = tid; i < R * HH; i += SAC_THREADS)
+      P1[(i / HH) * ldp1 + i % HH] = ldf<P>(p1 + (i / HH) * L1.Np + i % HH);
+    if (tid < R) lpB[tid] = ldf<P>(E.lp_st + par * E.Br + r0 + tid);
   }
   // the head stash of this thread's (row, dim) and the critics' output biases,
   // loaded now: after the critics' hand-off they would be one more round trip
   float hsv[4] = {0.f, 0.f, 0.f, 0.f};
   if (tid < R * A && r0 + tid / A < E.Br) {
-    const AS_G float* hs = GPC(float, E.head_st) + (size_t)(r0 + tid / A) * 4 * A;
+    const float* hs = E.head_st + (size_t)(r0 + tid / A) * 4 * A;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) hsv[q] = hs[q * A + tid % A];
+    for (int q = 0; q < 4; ++q) hsv[q] = ldf<P>(hs + q * A + tid % A);
   }
-  const float bq1 = GPC(float, E.net[NET_Q1].l[2].bias)[0], bq2 = GPC(float, E.net[NET_Q2].l[2].bias)[0];
+  // fused step: the critics' output biases once this step's phase B has written them
+  if (P) wait(3);
+  const float bq1 = ldf<P>(E.net[NET_Q1].l[2].bias), bq2 = ldf<P>(E.net[NET_Q2].l[2].bias);
   __syncthreads();
   STAMP(34);
   // combine the critics' unit-seed partials with the min-Q weights (L_pi = mean(alpha logpi - min Q))
@@ -977,7 +1014,7 @@ __device__ __forceinline__ void actor_split_body(const EngineDev* __restrict__ E
         if (q2n.out_act != ACT_ID) w2 = act_bwd(q2n.out_act, q2p, w2);
       }
       term = wave_sum(term);
-      if (tid == 0 && h == 0) GP(float, E.lossp)[(par * E.nrt + rbi) * 4 + 2] = term;
+      if (tid == 0 && h == 0) st_f<P>(E.lossp + (par * E.nrt + rbi) * 4 + 2, term);
       const float w1r = __shfl(w1, r, 64), w2r = __shfl(w2, r, 64);
       if (live) {
         float da1 = gv[0], da2 = gv[W];
@@ -1026,7 +1063,7 @@ __device__ __forceinline__ void actor_split_body(const EngineDev* __restrict__ E
       g2B[tid] = w2;
     }
     term = wave_sum(term);
-    if (tid == 0 && h == 0) GP(float, E.lossp)[(par * E.nrt + rbi) * 4 + 2] = term;
+    if (tid == 0 && h == 0) st_f<P>(E.lossp + (par * E.nrt + rbi) * 4 + 2, term);
   }
   __syncthreads();
   for (int i = tid; i < R * A; i += SAC_THREADS) {
@@ -1085,10 +1122,10 @@ __device__ __forceinline__ void actor_split_body(const EngineDev* __restrict__ E
   }
   __syncthreads();
   // layer 2 dY^T (= dOut) + bias partials: half 0
-  if (h == 0) store_T<T, R>(goutB, ldo, L2.Np, L2.N, L2.GT, Bp, r0, nvalid, L2.dbp);
+  if (h == 0) store_T<T, R, P>(goutB, ldo, L2.Np, L2.N, L2.GT, Bp, r0, nvalid, L2.dbp);
   // dY1 (this half) = act'(P1) * (dOut W2[:, half])
   const int act = pi.hid_act;
-  gemm_hs<T, 1, NCH_32>(goutB, ldo, wt2, &ht2, [&](int j, int col, const f32x4& acc) {
+  gemm_hs<T, 1, NCH_32, P>(goutB, ldo, wt2, &ht2, [&](int j, int col, const f32x4& acc) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int r = (((threadIdx.x & 63) >> 4) << 2) + i;
@@ -1099,9 +1136,9 @@ __device__ __forceinline__ void actor_split_body(const EngineDev* __restrict__ E
   });
   if (act != ACT_RELU && act != ACT_ID) act_pass_bwd<R>(U1, ldu1, P1, ldp1, HH >> 4, HH, act);
   __syncthreads();
-  store_T<T, R>(U1, ldu1, HH, HH, (T*)L1.GT + (size_t)h * HH * Bp, Bp, r0, nvalid, L1.dbp + h * HH, nullptr, L1.N);
+  store_T<T, R, P>(U1, ldu1, HH, HH, (T*)L1.GT + (size_t)h * HH * Bp, Bp, r0, nvalid, L1.dbp + h * HH, nullptr, L1.N);
   // dY0 partial = act'(P0) * (dY1 W1[half])
-  gemm_hs<T, 2, NCH_HH>(U1, ldu1, wt1, &ht1, [&](int j, int col, const f32x4& acc) {
+  gemm_hs<T, 2, NCH_HH, P>(U1, ldu1, wt1, &ht1, [&](int j, int col, const f32x4& acc) {
     const bool kv = col < L1.K;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -1113,7 +1150,7 @@ __device__ __forceinline__ void actor_split_body(const EngineDev* __restrict__ E
   });
   if (act != ACT_RELU && act != ACT_ID) act_pass_bwd<R>(Xb, ld, P0, ldp0, L1.Kp >> 4, L1.K, act);
   __syncthreads();
-  store_T<T, R>(Xb, ld, L0.Np, L0.N, L0.GT, W * Bp, h * Bp + r0, nvalid, L0.dbp);
+  store_T<T, R, P>(Xb, ld, L0.Np, L0.N, L0.GT, W * Bp, h * Bp + r0, nvalid, L0.dbp);
   STAMP(35);
 }
 
@@ -1124,10 +1161,12 @@ __global__ void __launch_bounds__(SAC_THREADS) sac_actor_split(const EngineDev* 
   extern __shared__ float lds_raw[];
   const int bid = (int)blockIdx.x;
   const int nrole = 3 * split_wc(sizeof(T)) * E.nrt;  // 3 roles x parts x nrt
-  if (bid >= nrole)
-    stage_next_batch(E, rb, bid - nrole, (lf*)lds_raw);
-  else
-    actor_split_body<T>(Ep, bid);
+  if (bid >= nrole) {
+    stage_next_batch(E, rb, bid - nrole, (lf*)lds_raw, *GPC(uint64_t, E.rng_step));
+  } else {
+    const uint64_t step = *GPC(uint64_t, E.rng_step);
+    actor_split_body<T>(Ep, bid, StepCtx{step, *GPC(uint32_t, E.sync) + 1u, (int)(step & 1)});
+  }
   phase_c_done(E);
   END_STAMP(61);
 }

@@ -517,3 +517,37 @@ def test_hidden_split_is_used_and_close_to_unsplit(lib, precision, monkeypatch):
     for k in out["1"]:
         a, b = out["1"][k].double(), out["0"][k].double()
         assert torch.allclose(a, b, rtol=tol, atol=tol), (k, (a - b).abs().max().item())
+
+
+# ---------------------------------------------------------------- fused step (round 3)
+@pytest.mark.parametrize("cfg,precision", [("c2", "fp32"), ("c2", "bf16"), ("c4", "fp32"), ("c4", "bf16")])
+def test_fused_step_equals_four_launches(lib, cfg, precision, monkeypatch):
+    """The fused step (sac_persist.h: the four phases of a step in one launch
+    of one workgroup per CU, readiness counters in place of the kernel
+    boundaries, every cross-workgroup byte stored and loaded sc1) runs the
+    phase kernels' own device code: device-sampled steps, graph-replayed
+    steps, injected indices + eps, a replay push in between -- the same bits
+    as four launches per step."""
+    lib.sac_engine_uses_fused_step.argtypes = [ctypes.c_void_p]
+    out = {}
+    for fused in ("1", "0"):
+        monkeypatch.setenv("SAC_PERSIST", fused)
+        eng, rb, c = _engine(cfg, precision, capacity=5000)
+        g_ = lib.sac_engine_uses_fused_step(eng.handle)
+        assert (g_ > 0) == (fused == "1"), g_
+        eng.train(rb, 3)
+        eng.train_graph(rb, 6, chunk=3)
+        g = np.random.default_rng(3)
+        B, A = c["batch"], c["act"]
+        idx = torch.from_numpy(g.choice(len(rb), size=(2, B), replace=False).astype(np.int32))
+        eps = torch.from_numpy(g.standard_normal((2, 2, B, A)).astype(np.float32))
+        eng.train(rb, 2, indices=idx, eps=eps)
+        n = 5
+        rb.push_batch(g.standard_normal((n, c["obs"]), dtype=np.float32), g.uniform(-1, 1, (n, A)),
+                      g.standard_normal(n), g.standard_normal((n, c["obs"]), dtype=np.float32), g.random(n) < 0.1)
+        eng.train(rb, 2)
+        eng.check()
+        out[fused] = {k: v.clone() for k, v in eng.state_tensors().items()}
+        out[fused]["stats"] = eng.stats.clone()
+    for k in out["1"]:
+        assert torch.equal(out["1"][k], out["0"][k]), (k, (out["1"][k].double() - out["0"][k].double()).abs().max())
