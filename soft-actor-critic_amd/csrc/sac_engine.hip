@@ -463,7 +463,14 @@ static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
   // block (TileDesc.gsum), which also sees every batch column of the tile -- the
   // seeded bias sums of TileDesc.seed rely on that; bf16: a block per dY part
   // with a granule hand-off to part 1
+  // fp32 split layer 0 (wc / 2 summed dY parts: the longest tiles of phases D /
+  // B, 5 / 3 operand row sets) is also split into pi0_parts / q0_parts batch
+  // parts with a granule hand-off (the critics' producer parts also hand over
+  // their seeded bias sums): 2 parts measured D 8.3 -> 7.6 us on C2
   const bool gsum_on = esz == 4;
+  int pi0_parts = 2, q0_parts = 2;
+  if (const char* v = getenv("SAC_PI0_PARTS")) pi0_parts = std::max(1, std::min(4, atoi(v)));
+  if (const char* v = getenv("SAC_Q0_PARTS")) q0_parts = std::max(1, std::min(4, atoi(v)));
   int tilesBD[2] = {0, 0};  // [critics (B), policy (D)]
   for (int ni = NET_PI; ni <= NET_Q2; ++ni)
     for (int l = 0; l < h.net[ni].L; ++l)
@@ -482,7 +489,7 @@ static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
   };
   const int bpartsB = batch_parts(tilesBD[0], 0), bpartsD = batch_parts(tilesBD[1], 1);
   auto tile_parts = [&](int ni, int l) {
-    if (l == 0 && split) return gsum_on ? 1 : ni == NET_PI ? wc : 2;
+    if (l == 0 && split) return gsum_on ? std::min(ni == NET_PI ? pi0_parts : q0_parts, Bp / 32) : ni == NET_PI ? wc : 2;
     return ni == NET_PI ? bpartsD : bpartsB;
   };
   int nB = 0, nD = 0, nhalf = 0;
@@ -491,14 +498,14 @@ static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
       const int t = (h.net[ni].l[l].Np / 32) * (h.net[ni].l[l].Kp / 32);
       const int parts = tile_parts(ni, l);
       (ni == NET_PI ? nD : nB) += t * parts;
-      nhalf += t * (parts - 1);  // producer parts: one 1024-granule slot each
+      nhalf += t * (parts - 1);  // producer parts: one granule slot each
     }
   // persistent step: readiness counters (+ the exit word) and the task table
   const size_t o_pctr = lay.take((size_t)(PC_COUNT * PC_SHARDS * PC_STRIDE + PC_STRIDE) * 4);
   const size_t o_ptask = lay.take((size_t)1024 * sizeof(PTask));
   const size_t o_tB = lay.take((size_t)nB * sizeof(TileDesc));
   const size_t o_tD = lay.take((size_t)nD * sizeof(TileDesc));
-  const size_t o_part = lay.take((size_t)nhalf * 1024 * 8);  // batch-half partial dW granules of split tiles
+  const size_t o_part = lay.take((size_t)nhalf * SAC_PART_STRIDE * 8);  // batch-half partial dW granules of split tiles
   const size_t total = lay.take(0);
 
   // LDS layout (floats)
@@ -683,15 +690,19 @@ static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
             const int parts = tile_parts(ni, l);
             if (parts > 1) {
               // consumer part 1 (batch columns [0, bpp)) + producer parts 2..P ([(p-1) bpp, p bpp))
-              const bool xsame = l == 0 && split;  // split layer 0: X^T columns [0, Bp) serve every part
+              // bf16 split layer 0: a part per dY part, X^T columns [0, Bp) serve every part;
+              // fp32 (gsum) split layer 0: batch parts of the summed operands
+              const bool xsame = l == 0 && split && !gsum_on;
               const int total = xsame ? parts * Bp : Bp;
               const int bpp = xsame ? Bp : rup((Bp + parts - 1) / parts, 32);
-              t.ld = xsame ? parts * Bp : Bp;
-              t.ldx = xsame ? 2 * Bp : Bp;
+              if (!(l == 0 && split && gsum_on)) {
+                t.ld = xsame ? parts * Bp : Bp;
+                t.ldx = xsame ? 2 * Bp : Bp;
+              }
               t.bp = bpp;
               t.kpart = 1;
               t.nparts = parts;
-              t.part = (uint64_t*)(base + o_part) + (size_t)ihalf * 1024;
+              t.part = (uint64_t*)(base + o_part) + (size_t)ihalf * SAC_PART_STRIDE;
               ihalf += parts - 1;
               for (int pp = 2; pp <= parts; ++pp) {
                 TileDesc pt = t;

@@ -246,17 +246,21 @@ __global__ void __launch_bounds__(SAC_THREADS) sac_persist(const EngineDev* __re
   // workgroup counts itself out after its last task)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (threadIdx.x == 0) {
+  if (threadIdx.x < 64) {  // wave 0: lane 0 counts the workgroup out; the last one's lanes reset in parallel
     const AS_C EngineDev& E = *(const AS_C EngineDev*)fresh_ptr(Ep);
     uint32_t* done = E.pctr + PC_COUNT * PC_SHARDS * PC_STRIDE;
-    const uint32_t n = __hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    uint32_t n = 0;
+    if (threadIdx.x == 0) n = __hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    n = __shfl(n, 0, 64);
     if (n == gridDim.x - 1) {
-      for (int i = 0; i <= PC_COUNT * PC_SHARDS * PC_STRIDE; ++i) E.pctr[i] = 0u;
-      *GP(uint64_t, E.rng_step) += 1;
-      GP(uint32_t, E.sync)[SYNC_EPOCH] += 1u;
-      AS_G double* o = GP(double, E.opt_steps);
-      for (int i = 0; i < 3; ++i) o[i] += 1.0;
-      if (E.auto_entropy && E.alpha_update) o[3] += 1.0;
+      const int lane = threadIdx.x;
+      if (lane < PC_COUNT * PC_SHARDS) E.pctr[lane * PC_STRIDE] = 0u;  // the word each shard uses
+      if (lane == 63) {
+        *done = 0u;
+        *GP(uint64_t, E.rng_step) += 1;
+        GP(uint32_t, E.sync)[SYNC_EPOCH] += 1u;
+      }
+      if (lane < 3 || (lane == 3 && E.auto_entropy && E.alpha_update)) GP(double, E.opt_steps)[lane] += 1.0;
     }
   }
   {

@@ -154,6 +154,7 @@ struct StepCtx {
 
 // One 32x32 weight tile of the update phases, self-contained so a block needs a
 // single descriptor fetch before its first HBM load.
+#define SAC_PART_STRIDE 1056  // granules per producer part: 32 x 32 partial dW, then 32 bias partials
 struct TileDesc {
   const void* GT;  // row n0 of d(pre-act)^T  [.][Bp]
   const void* XT;  // row k0 of input^T       [.][Bp]
@@ -180,6 +181,8 @@ struct TileDesc {
   // + (kpart - 2) * 1024: {value, launch epoch}, one 8-B sc1 store each, no
   // drain or flag); part 1 polls them, adds them to its own (parts in order)
   // and runs Adam.  kpart 0: a whole tile.
+  // A seeded tile's producer parts also publish their 32 bias-column partial
+  // sums (granules 1024..1055 of the part's slot of SAC_PART_STRIDE).
   int kpart, nparts;
   uint64_t* part;
   // fp32 hidden-split layer 0, one block (kpart 0): the gsum parts' partial dY
@@ -1014,6 +1017,8 @@ __device__ __forceinline__ void dw_adam_tile(const AS_C EngineDev& E, const Tile
     }
   }
   const bool do_bias = td.k0 == 0 && td.kpart <= 1;
+  // the seeded bias gradient is summed from the staged rows: every part sums its own columns
+  const bool bias_acc = td.k0 == 0 && (td.kpart <= 1 || seedp);
   float pb = 0.f, mb = 0.f, vb = 0.f, tbv = 0.f;
   if (do_bias && tid < 32 && td.n0 + tid < td.N) {
     pb = ldf<P>((const float*)td.b + td.n0 + tid);
@@ -1097,7 +1102,7 @@ __device__ __forceinline__ void dw_adam_tile(const AS_C EngineDev& E, const Tile
         issue(r0 + rstep, slc);
         __syncthreads();
         if (r0 == 0 && sl == 0) STAMP(polyak ? 51 : 55);
-        if (seedp && do_bias) {  // bias gradient: this lane's columns of the slot's scaled dY rows
+        if (seedp && bias_acc) {  // bias gradient: this lane's columns of the slot's scaled dY rows
 #pragma unroll
           for (int j = 0; j < BPT; ++j) {
             const int t = tid + j * UT, bn = t >> 4, bs = t & 15;
@@ -1150,45 +1155,68 @@ __device__ __forceinline__ void dw_adam_tile(const AS_C EngineDev& E, const Tile
 #pragma unroll
   for (int j = 0; j < BPT; ++j) {
     const int t = tid + j * UT;
-    if (do_bias && t < 512) red[(t >> 4) * 17 + (t & 15)] = bsum[j];
+    if (bias_acc && t < 512) red[(t >> 4) * 17 + (t & 15)] = bsum[j];
   }
   __syncthreads();
+  float gbx[3] = {0.f, 0.f, 0.f};  // seeded bias: the producer parts' column sums (consumer, tid < 32)
   if (td.kpart) {  // hidden-split layer 0: the batch parts of this tile meet here
     const uint32_t ep = P ? us->ep : *GPC(uint32_t, E.sync) + 1u;  // per launch (B and D have their own granules)
     if (td.kpart >= 2) {
-      AS_G uint64_t* mine = GP(uint64_t, td.part) + (size_t)(td.kpart - 2) * 1024;
+      AS_G uint64_t* mine = GP(uint64_t, td.part) + (size_t)(td.kpart - 2) * SAC_PART_STRIDE;
       for (int el = tid; el < 1024; el += UT) {
         const uint64_t x = (uint64_t)__float_as_uint(accs[(el >> 5) * 33 + (el & 31)]) | ((uint64_t)ep << 32);
         __hip_atomic_store((uint64_t*)(mine + el), x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
+      if (seedp && bias_acc && tid < 32) {
+        float gb = 0.f;
+        for (int q = 0; q < 16; ++q) gb += red[tid * 17 + q];
+        const uint64_t x = (uint64_t)__float_as_uint(gb) | ((uint64_t)ep << 32);
+        __hip_atomic_store((uint64_t*)(mine + 1024 + tid), x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
       return;  // uniform: part 1 runs Adam on the sum
     }
-    for (int el = tid; el < 1024; el += UT) {
-      float v[3] = {0.f, 0.f, 0.f};
-      const int np = td.nparts - 1;  // producer parts (1..3)
-      for (int it = 0;; ++it) {
-        bool all = true;
+    // each thread polls all of its 1024 / UT elements' granules of every
+    // producer part in one batch of loads per attempt (one round trip, not one
+    // per element); parts are added in order
+    constexpr int EL = 1024 / UT;
+    static_assert(EL * UT == 1024 && EL <= 4, "granules per thread");
+    const int np = td.nparts - 1;  // producer parts (1..3)
+    const bool pb_here = seedp && do_bias && tid < 32;
+    float v[3][EL];
+    for (int it = 0;; ++it) {
+      bool all = true;
 #pragma unroll
-        for (int q = 0; q < 3; ++q)
-          if (q < np) {
-            const uint64_t x = __hip_atomic_load(td.part + (size_t)q * 1024 + el, __ATOMIC_RELAXED,
-                                                 __HIP_MEMORY_SCOPE_AGENT);
+      for (int q = 0; q < 3; ++q)
+        if (q < np) {
+#pragma unroll
+          for (int j = 0; j < EL; ++j) {
+            const uint64_t x = __hip_atomic_load(td.part + (size_t)q * SAC_PART_STRIDE + tid + j * UT,
+                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             all = all && (uint32_t)(x >> 32) == ep;
-            v[q] = __uint_as_float((uint32_t)x);
+            v[q][j] = __uint_as_float((uint32_t)x);
           }
-        if (all) break;
-        if (it > E.spin_limit) {  // a producer part never ran: flag the error, do not hang
-          __hip_atomic_store((uint32_t*)GP(uint32_t, E.sync) + 1 /* SYNC_TIMEOUT */, 1u, __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_AGENT);
-          break;
+          if (pb_here) {
+            const uint64_t x = __hip_atomic_load(td.part + (size_t)q * SAC_PART_STRIDE + 1024 + tid,
+                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            all = all && (uint32_t)(x >> 32) == ep;
+            gbx[q] = __uint_as_float((uint32_t)x);
+          }
         }
-        __builtin_amdgcn_s_sleep(1);
+      if (all) break;
+      if (it > E.spin_limit) {  // a producer part never ran: flag the error, do not hang
+        __hip_atomic_store((uint32_t*)GP(uint32_t, E.sync) + 1 /* SYNC_TIMEOUT */, 1u, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+        break;
       }
-      const int o = (el >> 5) * 33 + (el & 31);
+      __builtin_amdgcn_s_sleep(1);
+    }
+#pragma unroll
+    for (int j = 0; j < EL; ++j) {
+      const int el = tid + j * UT, o = (el >> 5) * 33 + (el & 31);
       float sum = accs[o];
 #pragma unroll
       for (int q = 0; q < 3; ++q)
-        if (q < np) sum += v[q];
+        if (q < np) sum += v[q][j];
       accs[o] = sum;
     }
     __syncthreads();
@@ -1227,6 +1255,11 @@ __device__ __forceinline__ void dw_adam_tile(const AS_C EngineDev& E, const Tile
   if (do_bias && tid < 32 && td.n0 + tid < td.N) {
     float gb = 0.f;
     for (int q = 0; q < 16; ++q) gb += red[tid * 17 + q];
+    if (seedp && td.kpart) {  // the other batch parts' sums, in part order
+#pragma unroll
+      for (int q = 0; q < 3; ++q)
+        if (q < td.nparts - 1) gb += gbx[q];
+    }
     const float pbn = adam_elem(pb, mb, vb, gb, w1, b2, w2, bc2s, eps, neg_step);
     if (COH)
       coh_storef((float*)td.b + td.n0 + tid, pb);

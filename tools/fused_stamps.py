@@ -73,5 +73,10 @@ for cname, rng in classes.items():
             if col.size:
                 vals.append(np.median(col - t0) / 100.0)
         if vals:
-            line.append(f"{names[i]} {np.median(vals):.2f}")
+            mx = np.median([(r[list(rng), i][r[list(rng), i] > 0].max() - r[r > 0].min()) / 100.0
+                            for r in runs if (r[list(rng), i] > 0).any()])
+            line.append(f"{names[i]} {np.median(vals):.2f}/{mx:.2f}")
     print(f"[{cname:7s}] " + " | ".join(line))
+print("(median / max over the class's workgroups, each the median over steps)")
+last = [np.unravel_index(np.argmax(r), r.shape) for r in runs]
+print("last stamp of the launch (workgroup, stamp id) per step:", [(int(w), int(i)) for w, i in last])
