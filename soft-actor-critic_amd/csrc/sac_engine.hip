@@ -573,6 +573,11 @@ static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
       while (xs < 8 && nrt * xs * 2 <= 256) xs *= 2;
       if (const char* v = getenv("SAC_XS")) xs = std::max(1, atoi(v));
       h.xs = xs;
+      // phase A's weight parts on one or two XCDs each: A's fetched bytes 11.0 -> 5.1
+      // MB per launch, phase B 8.6 -> 8.1 us, +1.2% steps/s (C2 fp32,
+      // profiles/r03_ab_role_xcd.txt)
+      h.role_xcd = split && (10 + split_wpi(esz)) * nrt % 8 == 0;
+      if (const char* v = getenv("SAC_ROLE_XCD")) h.role_xcd = h.role_xcd && atoi(v) != 0;
       // role split of phases A/C: 6 * nrt workgroups must be co-resident (one per CU)
       h.roles = roles;
       // phase C stages the next step's batch (SAC_STAGE=0 turns it off)
@@ -818,6 +823,8 @@ static void plan_persist(sac_engine* e, int esz) {
   e->h.pc_n[PC_CP] = (uint32_t)nCp;
   e->h.pc_n[PC_D] = (uint32_t)nD1;
   e->h.pc_n[PC_AQP] = (uint32_t)(4 * nrt);  // critic roles (2 critics x 2 halves x nrt)
+  e->h.p_aqp = 1;
+  if (const char* v = getenv("SAC_PERSIST_AQP")) e->h.p_aqp = atoi(v) != 0;
   e->h.o_pflag = (int)((std::max(e->lds_bytes, e->upd_lds) + 15) / 16 * 4);
   if ((size_t)e->h.o_pflag * 4 + 16 > 160 * 1024) return;
   e->persist = 1;

@@ -158,10 +158,11 @@ __global__ void __launch_bounds__(SAC_THREADS) sac_persist(const EngineDev* __re
     if (a >= 0) {
       int role_done = -1;
       target_critic_split_body<T, true>(Ek, rb, inj_idx_, inj_eps_, a, step_now(E), [&](int role) {
-        if (role < 0)
-          pc_arrive(E, PC_AQP);  // a critic's pre-seed operands are stored
-        else
+        if (role < 0) {
+          if (E.p_aqp) pc_arrive(E, PC_AQP);  // a critic's pre-seed operands are stored
+        } else {
           role_done = role;
+        }
       });
       if (role_done >= 1 && role_done <= 4) pc_arrive(E, PC_AQ);
       else if (role_done == 5) pc_arrive(E, PC_PS);
@@ -179,7 +180,7 @@ __global__ void __launch_bounds__(SAC_THREADS) sac_persist(const EngineDev* __re
       const UpdStep us = upd_step(E, opt, GPC(double, E.opt_steps)[opt] + 1.0, sc.ep);
       // fp32 layers 0 / 1: operands once every critic role has stored its pre-seed
       // operands (PC_AQP), the rest once the critics and targets are done (PC_AQ)
-      const bool pre = sizeof(T) == 4 && ((const AS_C TileDesc*)td)->N > 1;
+      const bool pre = sizeof(T) == 4 && E.p_aqp && ((const AS_C TileDesc*)td)->N > 1;
       dw_adam_tile_any<T, SAC_THREADS, true, true>(E, td, true, sc.par, 0, lds, &us, [&](int stage) {
         if (stage == 0 && pre) {
           pc_wait(E, PC_AQP, E.pc_n[PC_AQP], -1, 0, flag);

@@ -79,6 +79,7 @@ struct EngineDev {
   // once): blocks are dealt round-robin over the 8 XCDs, so xs > 1 packs the
   // tiles onto 8/xs XCDs whose L2s then share one weight stream (speed only).
   int xs;
+  int role_xcd;  // phase A role kernel: a weight part's workgroups on at most two XCDs (SAC_ROLE_XCD)
   int roles;  // phases A / C split into per-network workgroups (see "role hand-offs")
   int gstride;     // granules per (kind, row tile): SAC_ROWS * (act_dim + 1)
   uint64_t* gran;  // [G_COUNT][nrt][gstride] data-tagged hand-off granules (gran_put)
@@ -132,6 +133,7 @@ struct EngineDev {
   // persistent step (sac_persist.h): readiness counters [PC_COUNT][8 shards][16]
   // + 1 exit word, the per-workgroup task table, producers per step of every
   // counter, and an LDS word for the wait verdict (past every phase's layout)
+  int p_aqp;       // fused step: phase B's layers 0 / 1 start on the critics' pre-seed arrivals (PC_AQP)
   uint32_t* pctr;
   const void* ptasks;
   uint32_t pc_n[8];

@@ -287,7 +287,8 @@ __device__ __forceinline__ void gemm_ksplit(const lf* __restrict__ A, int lda, c
 // fused launch, and everything the role hands to workgroups of the launch's
 // later phases is stored sc1 (their loads are sc1).  Phase A opens the launch,
 // so its inputs (the previous launch's weights, the batch staged for it) need
-// no wait.
+// no wait, and its weight and bias loads stay plain (L2-cached): nothing in the
+// launch writes them before phase A's last reader has arrived.
 template <typename T, bool P = false, typename RoleWait = NoWait>
 __device__ __forceinline__ void target_critic_split_body(const EngineDev* __restrict__ Ep, const sac_replay& rb,
                                                          const int32_t* __restrict__ inj_idx_,
@@ -477,7 +478,7 @@ __device__ __forceinline__ void target_critic_split_body(const EngineDev* __rest
     const int rpp = SAC_THREADS / AP;
     const int jj = tid % AP;
     // this lane's head biases, loaded before the polls (not one more round trip after them)
-    const float b2mu = jj < A ? ldf<P>(b2 + jj) : 0.f, b2ls = jj < A ? ldf<P>(b2 + A + jj) : 0.f;
+    const float b2mu = jj < A ? ldf<false>(b2 + jj) : 0.f, b2ls = jj < A ? ldf<false>(b2 + A + jj) : 0.f;
     for (int base = 0; base < R; base += rpp) {
       const int r = base + tid / AP, j = jj;
       const bool live = r < R && j < A;
@@ -545,7 +546,7 @@ __device__ __forceinline__ void target_critic_split_body(const EngineDev* __rest
   auto forward01 = [&](bool keepP, bool stXT, bool pi_actor, auto&& after_l1) {
     // layer 0: X [R][Kp0] -> P0 / H0 [R][H]
     const int act = net.hid_act;
-    gemm_hs<T, 2, HC0, P>(Xb, ld, w0, &h0, [&](int j, int col, const f32x4& acc) {
+    gemm_hs<T, 2, HC0, false>(Xb, ld, w0, &h0, [&](int j, int col, const f32x4& acc) {
       const bool nv = col < L0.N;
       const float bn = h0.b[j];
 #pragma unroll
@@ -565,9 +566,9 @@ __device__ __forceinline__ void target_critic_split_body(const EngineDev* __rest
     if (stXT && h == 0)
       store_T<T, R, P>(H0, ld, L1.Kp, L1.K, (T*)L1.XT + (pi_actor ? par * L1.xt_par : 0), Bp, r0, nvalid, nullptr);
     STAMP(2);
-    if (sizeof(T) == 4 && !kh2.ok) ks_issue<T, KsHeld<T>::MAXC, P>(kh2, w2n);  // fp32: under layer 1 (target critics: before the poll)
+    if (sizeof(T) == 4 && !kh2.ok) ks_issue<T, KsHeld<T>::MAXC, false>(kh2, w2n);  // fp32: under layer 1 (target critics: before the poll)
     // layer 1, this half: H0 -> P1 / H1 [R][HH]
-    gemm_hs<T, 1, NCH_H, P>(H0, ld, w1, &h1, [&](int j, int col, const f32x4& acc) {
+    gemm_hs<T, 1, NCH_H, false>(H0, ld, w1, &h1, [&](int j, int col, const f32x4& acc) {
       const float bn = h1.b[j];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
@@ -589,7 +590,7 @@ __device__ __forceinline__ void target_critic_split_body(const EngineDev* __rest
                        nvalid, nullptr);
     STAMP(3);
     // layer 2, this half's partial sum: outB [R][Np2]
-    gemm_ksplit<T, P, decltype(kh2)::MAXC>(H1, ldh1, w2n, red, outB, ldo, &kh2);
+    gemm_ksplit<T, false, decltype(kh2)::MAXC>(H1, ldh1, w2n, red, outB, ldo, &kh2);
     STAMP(4);
   };
 
@@ -633,7 +634,7 @@ __device__ __forceinline__ void target_critic_split_body(const EngineDev* __rest
   } else if (role == 1 || role == 2) {
     // ---- target critic t (agent.py:195-211): a~', log pi' from pi(s')'s two partials
     const int t = role - 1;
-    if (sizeof(T) == 4) ks_issue<T, KsHeld<T>::MAXC, P>(kh2, w2n);
+    if (sizeof(T) == 4) ks_issue<T, KsHeld<T>::MAXC, false>(kh2, w2n);
     head(gs_at(E, GS_PI, rbi, 0), nullptr, true, a2B, lpB, false);
     if (t == 0 && h == 0 && tid < R) gran_put(gs_at(E, GS_LP, rbi, 0) + tid, lpB[tid], ep);
     STAMP(7);
@@ -650,14 +651,14 @@ __device__ __forceinline__ void target_critic_split_body(const EngineDev* __rest
     // bf16: held from the start too; fp32 (no register room: 51 VGPRs would
     // spill) issued as soon as layer 1's forward GEMM has freed h1's registers.
     // W2's element for this thread's column n = tid % HH
-    if constexpr (sizeof(T) == 2) ht_issue<T, 2, NCH_HH, P>(ht1, wt1);
+    if constexpr (sizeof(T) == 2) ht_issue<T, 2, NCH_HH, false>(ht1, wt1);
     static_assert(SAC_THREADS % SPLIT_HH == 0, "one W2 column per thread in the unit-seed loop");
-    const float w2n = ldf<P>(net.P + L2.w_off + h * HH + tid % HH);  // W2 [1][H] fp32 master
+    const float w2n = ldf<false>(net.P + L2.w_off + h * HH + tid % HH);  // W2 [1][H] fp32 master
     build_x(sB, aB, A);
     // layer-0 input X^T is shared by Q1 and Q2: Q1's halves store it (columns h Bp + r0)
     if (qi == 0) store_T<T, R, P>(Xb, ld, L0.Kp, L0.K, L0.XT, 2 * Bp, h * Bp + r0, nvalid, nullptr);
     forward01(true, true, false, [&] {
-      if constexpr (sizeof(T) == 4) ht_issue<T, 2, NCH_HH, P>(ht1, wt1);
+      if constexpr (sizeof(T) == 4) ht_issue<T, 2, NCH_HH, false>(ht1, wt1);
     });
     if (tid < R) gran_put(gs_at(E, qi ? GS_QA2 : GS_QA1, rbi, h) + tid, outB[tid * ldo], ep);
     // unit-seed backward (every layer's dY is linear in the row's seed 2(q - y)/B):
@@ -668,7 +669,7 @@ __device__ __forceinline__ void target_critic_split_body(const EngineDev* __rest
         U1[r * ldu1 + n] = act_bwd(net.hid_act, P1[r * ldp1 + n], w2n);
       }
       __syncthreads();
-      gemm_hs<T, 2, NCH_HH, P>(U1, ldu1, wt1, &ht1, [&](int j, int col, const f32x4& acc) {
+      gemm_hs<T, 2, NCH_HH, false>(U1, ldu1, wt1, &ht1, [&](int j, int col, const f32x4& acc) {
         const bool kv = col < L1.K;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
@@ -698,10 +699,10 @@ __device__ __forceinline__ void target_critic_split_body(const EngineDev* __rest
       if (tid < R) {
         const int b = r0 + tid;
         const bool v = tid < nvalid;
-        const float b2 = ldf<P>(L2.bias);
+        const float b2 = ldf<false>(L2.bias);
         const AS_C NetDev& t1 = E.net[NET_Q1T];
         const AS_C NetDev& t2 = E.net[NET_Q2T];
-        const float bt1 = ldf<P>(t1.l[2].bias), bt2 = ldf<P>(t2.l[2].bias);  // before the poll
+        const float bt1 = ldf<false>(t1.l[2].bias), bt2 = ldf<false>(t2.l[2].bias);  // before the poll
         const float mine = outB[tid * ldo];
         // every granule this row needs, polled together: peer half's q partial,
         // both target critics' two halves, log pi(a'|s')
@@ -756,13 +757,31 @@ __global__ void __launch_bounds__(SAC_THREADS) sac_target_critic_split(const Eng
   const AS_C EngineDev& E0 = *(const AS_C EngineDev*)Ep;
   const uint64_t step = *GPC(uint64_t, E0.rng_step);
   const StepCtx sc{step, *GPC(uint32_t, E0.sync) + 1u, (int)(step & 1)};
-  target_critic_split_body<T>(Ep, rb, inj_idx_, inj_eps_, (int)blockIdx.x, sc);
+  int bidA = (int)blockIdx.x;
+  if (E0.role_xcd) {  // uniform
+    // blocks are dealt round-robin to the 8 XCDs (block b on XCD b % 8): XCD x
+    // takes units [x G/8, (x+1) G/8) of the part-major order (every row tile of
+    // pi(s') quarter 0, of quarter 1, ..., of each role half), so the 16
+    // workgroups that stream one weight part share at most two XCDs' L2s
+    constexpr int WP = split_wpi(sizeof(T));
+    const int nrt = E0.nrt, n0 = WP * nrt, n2 = 2 * nrt;
+    const int u = (bidA % 8) * ((int)gridDim.x / 8) + bidA / 8;
+    if (u < n0) {
+      bidA = (u % nrt) * WP + u / nrt;
+    } else {
+      const int v = u - n0, w = v % n2;
+      bidA = n0 + (v / n2) * n2 + (w % nrt) * 2 + w / nrt;
+    }
+  }
+  target_critic_split_body<T>(Ep, rb, inj_idx_, inj_eps_, bidA, sc);
   const AS_C EngineDev& E = *(const AS_C EngineDev*)Ep;
   (void)E;
   END_STAMP(60);
 }
 
 // ---------------------------------------------------------------------------- phase C
+// pi's weights are read with plain loads in either mode (the previous launch's
+// phase D wrote them; this launch's D waits for every pi role).
 // P (persistent step): wait(0) = pi(s) of this step done (the stashes), wait(1 +
 // qi) = critic qi updated by this step's phase B, wait(3) = both critics
 // updated; every load of data written earlier in the launch is sc1, and what
@@ -939,8 +958,8 @@ __device__ __forceinline__ void actor_split_body(const EngineDev* __restrict__ E
   HTiles<T, 1, NCH_32> ht2;
   HTiles<T, 2, NCH_HH> ht1;
   if (P) wait(0);  // pi(s) of this step: its stashes (and, before it, the phase D that wrote pi's weights)
-  ht_issue<T, 1, NCH_32, P>(ht2, wt2);
-  ht_issue<T, 2, NCH_HH, P>(ht1, wt1);
+  ht_issue<T, 1, NCH_32, false>(ht2, wt2);
+  ht_issue<T, 2, NCH_HH, false>(ht1, wt1);
   {  // relu masks: pi's pre-activations stashed by phase A's pi(s) role
     const float* p0 = L0.pstash + (size_t)r0 * L0.Np;
     for (int i = tid; i < R * L0.Np; i += SAC_THREADS) P0[(i / L0.Np) * ldp0 + i % L0.Np] = ldf<P>(p0 + i);
@@ -1125,7 +1144,7 @@ __device__ __forceinline__ void actor_split_body(const EngineDev* __restrict__ E
   if (h == 0) store_T<T, R, P>(goutB, ldo, L2.Np, L2.N, L2.GT, Bp, r0, nvalid, L2.dbp);
   // dY1 (this half) = act'(P1) * (dOut W2[:, half])
   const int act = pi.hid_act;
-  gemm_hs<T, 1, NCH_32, P>(goutB, ldo, wt2, &ht2, [&](int j, int col, const f32x4& acc) {
+  gemm_hs<T, 1, NCH_32, false>(goutB, ldo, wt2, &ht2, [&](int j, int col, const f32x4& acc) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int r = (((threadIdx.x & 63) >> 4) << 2) + i;
@@ -1138,7 +1157,7 @@ __device__ __forceinline__ void actor_split_body(const EngineDev* __restrict__ E
   __syncthreads();
   store_T<T, R, P>(U1, ldu1, HH, HH, (T*)L1.GT + (size_t)h * HH * Bp, Bp, r0, nvalid, L1.dbp + h * HH, nullptr, L1.N);
   // dY0 partial = act'(P0) * (dY1 W1[half])
-  gemm_hs<T, 2, NCH_HH, P>(U1, ldu1, wt1, &ht1, [&](int j, int col, const f32x4& acc) {
+  gemm_hs<T, 2, NCH_HH, false>(U1, ldu1, wt1, &ht1, [&](int j, int col, const f32x4& acc) {
     const bool kv = col < L1.K;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {

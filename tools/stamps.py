@@ -81,10 +81,24 @@ if SPLIT:  # sac_split.h stamps
 WPI = (4 if prec == "fp32" else 2) if SPLIT else 1  # phase A: pi(s') parts (split_wpi)
 
 
+# phase A's split kernel places each weight part's workgroups on one or two XCDs
+# (EngineDev::role_xcd, default on): hardware block -> the body's block id
+ROLE_XCD = SPLIT and os.environ.get("SAC_ROLE_XCD", "1") != "0" and (10 + WPI) * nrt % 8 == 0
+
+
+def _role_xcd_bid(b):
+    n0, n2, G = WPI * nrt, 2 * nrt, (10 + WPI) * nrt
+    u = (b % 8) * (G // 8) + b // 8
+    v = u - n0
+    return np.where(u < n0, (u % nrt) * WPI + u // nrt, n0 + (v // n2) * n2 + (v % n2 % nrt) * 2 + v % n2 // nrt)
+
+
 def role_of(ph, b, G):
     """Role index of phase-relative block ids b (phase A: pi(s') has WPI parts per row tile)."""
     if ph == "A" and SPLIT:
         n0 = WPI * nrt
+        if ROLE_XCD:
+            b = _role_xcd_bid(np.asarray(b))
         return np.where(b < n0, 0, 1 + (b - n0) // G)
     return b // G
 
