@@ -192,8 +192,9 @@ struct TileDesc {
   // part order, and reduced once against X -- no batch parts, no hand-off
   long goff;
   int gsum, pad_;
-  // fp32 split critics' layers 0 / 1: dY^T holds the unit-seed backward (phase A
-  // stores it before y is known); every batch column b is scaled by seed[b]
+  // fp32 split critics (every layer): dY^T holds the unit-seed backward (phase
+  // A's critic roles store it without waiting for y); every batch column b is
+  // scaled by seed[b] (phase A's first target-critic half computes the seeds)
   // while staging, and the bias gradient is summed from the scaled rows here
   const float* seed;
 };

@@ -642,6 +642,49 @@ __device__ __forceinline__ void target_critic_split_body(const EngineDev* __rest
     forward01(false, false, false, no_hook);
     if (tid < R) gran_put(gs_at(E, t ? GS_QT2 : GS_QT1, rbi, h) + tid, outB[tid * ldo], ep);
     STAMP(9);
+    if (sizeof(T) == 4 && t == 0 && h == 0 && tid < 64) {
+      // fp32: this half (Qt1, half 0) computes the row tile's targets y and both
+      // critics' seeds dL/dq = 2 (q - y) / B and loss partials (agent.py:
+      // 195-236; the critic roles, which used to wait for y, store unit-seed
+      // operands and finish).  Same float operations as the critics' code below.
+      float sq[2] = {0.f, 0.f};
+      if (tid < R) {
+        const int b = r0 + tid;
+        const bool v = tid < nvalid;
+        const AS_C NetDev& t1 = E.net[NET_Q1T];
+        const AS_C NetDev& t2 = E.net[NET_Q2T];
+        const float bt1 = ldf<false>(t1.l[2].bias), bt2 = ldf<false>(t2.l[2].bias);
+        const float bq[2] = {ldf<false>(E.net[NET_Q1].l[2].bias), ldf<false>(E.net[NET_Q2].l[2].bias)};
+        const AS_G uint64_t* gg[7] = {gs_at(E, GS_QT1, rbi, 1) + tid, gs_at(E, GS_QT2, rbi, 0) + tid,
+                                      gs_at(E, GS_QT2, rbi, 1) + tid, gs_at(E, GS_QA1, rbi, 0) + tid,
+                                      gs_at(E, GS_QA1, rbi, 1) + tid, gs_at(E, GS_QA2, rbi, 0) + tid,
+                                      gs_at(E, GS_QA2, rbi, 1) + tid};
+        float gv[7];
+        gran_getn<7>(E, gg, ep, gv);
+        const float q1tp = outB[tid * ldo] + gv[0] + bt1;
+        const float q2tp = gv[1] + gv[2] + bt2;
+        const float q1t = t1.out_act == ACT_ID ? q1tp : act_fwd(t1.out_act, q1tp);
+        const float q2t = t2.out_act == ACT_ID ? q2tp : act_fwd(t2.out_act, q2tp);
+        const float y = rB[tid] + (E.gamma * (1.f - dB[tid])) * (fmin_nan(q1t, q2t) - alpha32 * lpB[tid]);
+        if (b < B) stats[4 + b] = y;
+#pragma unroll
+        for (int qi = 0; qi < 2; ++qi) {
+          const AS_C NetDev& qn = E.net[NET_Q1 + qi];
+          const float qpre = (gv[3 + 2 * qi] + gv[4 + 2 * qi]) + bq[qi];
+          const float q = qn.out_act == ACT_ID ? qpre : act_fwd(qn.out_act, qpre);
+          const float d = q - y;
+          sq[qi] = v ? d * d : 0.f;
+          float seed = v ? (2.0f / (float)B) * d : 0.f;
+          if (qn.out_act != ACT_ID) seed = act_bwd(qn.out_act, qpre, seed);
+          st_f<P>(E.seedq + qi * Bp + b, seed);
+        }
+      }
+#pragma unroll
+      for (int qi = 0; qi < 2; ++qi) {
+        const float s2 = wave_sum(sq[qi]);
+        if (tid == 0) st_f<P>(E.lossp + (par * E.nrt + rbi) * 4 + qi, s2);
+      }
+    }
   } else {
     // ---- critic qi (agent.py:213-236): forward, unit-seed backward, seed once y is known
     const int qi = role - 3;
@@ -685,63 +728,68 @@ __device__ __forceinline__ void target_critic_split_body(const EngineDev* __rest
     }
     STAMP(16);
     if constexpr (sizeof(T) == 4) {
-      // fp32: layers 1 and 0's unit-seed dY^T stored now, while y is still on its
-      // way; phase B scales each batch column by its row's seed (E.seedq) as it
-      // stages them, and sums their bias gradients itself
+      // fp32: the role does not wait for y.  It stores every layer's UNIT-seed
+      // dY^T (layer 2's: the indicator row); phase B scales each batch column
+      // by the seed the first target-critic half computed (E.seedq) and sums
+      // the bias gradients from the scaled rows.
       store_T<T, R, P>(U1, ldu1, HH, HH, (T*)L1.GT + (size_t)h * HH * Bp, Bp, r0, nvalid, nullptr);
       store_T<T, R, P>(Xb, ld, L0.Np, L0.N, L0.GT, 2 * Bp, h * Bp + r0, nvalid, nullptr);
-    }
-    // fused step: the operands phase B can fetch before y is known are stored
-    // (fp32: X^T and the unit-seed dY^T of layers 0 / 1)
-    if constexpr (P) role_wait(-1);
-    if (tid < 64) {  // wave 0: q, y, loss partial, seed dL/dq = 2(q - y)/B  (mse_loss backward)
-      float sq = 0.f;
-      if (tid < R) {
-        const int b = r0 + tid;
-        const bool v = tid < nvalid;
-        const float b2 = ldf<false>(L2.bias);
-        const AS_C NetDev& t1 = E.net[NET_Q1T];
-        const AS_C NetDev& t2 = E.net[NET_Q2T];
-        const float bt1 = ldf<false>(t1.l[2].bias), bt2 = ldf<false>(t2.l[2].bias);  // before the poll
-        const float mine = outB[tid * ldo];
-        // every granule this row needs, polled together: peer half's q partial,
-        // both target critics' two halves, log pi(a'|s')
-        const AS_G uint64_t* gg[6] = {gs_at(E, qi ? GS_QA2 : GS_QA1, rbi, 1 - h) + tid,
-                                      gs_at(E, GS_QT1, rbi, 0) + tid, gs_at(E, GS_QT1, rbi, 1) + tid,
-                                      gs_at(E, GS_QT2, rbi, 0) + tid, gs_at(E, GS_QT2, rbi, 1) + tid,
-                                      gs_at(E, GS_LP, rbi, 0) + tid};
-        float gv[6];
-        gran_getn<6>(E, gg, ep, gv);
-        const float peer = gv[0];
-        const float qpre = (h == 0 ? mine + peer : peer + mine) + b2;
-        const float q = net.out_act == ACT_ID ? qpre : act_fwd(net.out_act, qpre);
-        const float q1tp = gv[1] + gv[2] + bt1;
-        const float q2tp = gv[3] + gv[4] + bt2;
-        const float q1t = t1.out_act == ACT_ID ? q1tp : act_fwd(t1.out_act, q1tp);
-        const float q2t = t2.out_act == ACT_ID ? q2tp : act_fwd(t2.out_act, q2tp);
-        const float lp2 = gv[5];
-        const float y = rB[tid] + (E.gamma * (1.f - dB[tid])) * (fmin_nan(q1t, q2t) - alpha32 * lp2);
-        if (qi == 0 && h == 0 && b < B) stats[4 + b] = y;
-        const float d = q - y;
-        sq = v ? d * d : 0.f;
-        float seed = v ? (2.0f / (float)B) * d : 0.f;
-        if (net.out_act != ACT_ID) seed = act_bwd(net.out_act, qpre, seed);
-        qtB[tid] = seed;
-        if (sizeof(T) == 4 && h == 0) st_f<P>(E.seedq + qi * Bp + b, seed);
+      if (h == 0) {
+        lf* g2 = outB;  // this half's q partial went out as a granule above
+        for (int i = tid; i < R * 32; i += SAC_THREADS) g2[(i / 32) * ldo + i % 32] = (i % 32) == 0 ? 1.f : 0.f;
+        __syncthreads();
+        store_T<T, R, P>(g2, ldo, L2.Np, L2.N, L2.GT, Bp, r0, nvalid, nullptr);
       }
-      sq = wave_sum(sq);
-      if (tid == 0 && h == 0) st_f<P>(E.lossp + (par * E.nrt + rbi) * 4 + qi, sq);
-    }
-    __syncthreads();
-    STAMP(15);
-    // dY^T of every layer (seed x unit dY) + bias partials for phase B
-    if (h == 0) {  // layer 2: dY2 = seed (N = 1)
-      lf* g2 = outB;
-      for (int i = tid; i < R * 32; i += SAC_THREADS) g2[(i / 32) * ldo + i % 32] = (i % 32) == 0 ? 1.f : 0.f;
+      if constexpr (P) role_wait(-1);
+      STAMP(15);
+    } else {
+      if constexpr (P) role_wait(-1);
+      if (tid < 64) {  // wave 0: q, y, loss partial, seed dL/dq = 2(q - y)/B  (mse_loss backward)
+        float sq = 0.f;
+        if (tid < R) {
+          const int b = r0 + tid;
+          const bool v = tid < nvalid;
+          const float b2 = ldf<false>(L2.bias);
+          const AS_C NetDev& t1 = E.net[NET_Q1T];
+          const AS_C NetDev& t2 = E.net[NET_Q2T];
+          const float bt1 = ldf<false>(t1.l[2].bias), bt2 = ldf<false>(t2.l[2].bias);  // before the poll
+          const float mine = outB[tid * ldo];
+          // every granule this row needs, polled together: peer half's q partial,
+          // both target critics' two halves, log pi(a'|s')
+          const AS_G uint64_t* gg[6] = {gs_at(E, qi ? GS_QA2 : GS_QA1, rbi, 1 - h) + tid,
+                                        gs_at(E, GS_QT1, rbi, 0) + tid, gs_at(E, GS_QT1, rbi, 1) + tid,
+                                        gs_at(E, GS_QT2, rbi, 0) + tid, gs_at(E, GS_QT2, rbi, 1) + tid,
+                                        gs_at(E, GS_LP, rbi, 0) + tid};
+          float gv[6];
+          gran_getn<6>(E, gg, ep, gv);
+          const float peer = gv[0];
+          const float qpre = (h == 0 ? mine + peer : peer + mine) + b2;
+          const float q = net.out_act == ACT_ID ? qpre : act_fwd(net.out_act, qpre);
+          const float q1tp = gv[1] + gv[2] + bt1;
+          const float q2tp = gv[3] + gv[4] + bt2;
+          const float q1t = t1.out_act == ACT_ID ? q1tp : act_fwd(t1.out_act, q1tp);
+          const float q2t = t2.out_act == ACT_ID ? q2tp : act_fwd(t2.out_act, q2tp);
+          const float lp2 = gv[5];
+          const float y = rB[tid] + (E.gamma * (1.f - dB[tid])) * (fmin_nan(q1t, q2t) - alpha32 * lp2);
+          if (qi == 0 && h == 0 && b < B) stats[4 + b] = y;
+          const float d = q - y;
+          sq = v ? d * d : 0.f;
+          float seed = v ? (2.0f / (float)B) * d : 0.f;
+          if (net.out_act != ACT_ID) seed = act_bwd(net.out_act, qpre, seed);
+          qtB[tid] = seed;
+        }
+        sq = wave_sum(sq);
+        if (tid == 0 && h == 0) st_f<P>(E.lossp + (par * E.nrt + rbi) * 4 + qi, sq);
+      }
       __syncthreads();
-      store_T<T, R, P>(g2, ldo, L2.Np, L2.N, L2.GT, Bp, r0, nvalid, L2.dbp, qtB);
-    }
-    if constexpr (sizeof(T) == 2) {
+      STAMP(15);
+      // dY^T of every layer (seed x unit dY) + bias partials for phase B
+      if (h == 0) {  // layer 2: dY2 = seed (N = 1)
+        lf* g2 = outB;
+        for (int i = tid; i < R * 32; i += SAC_THREADS) g2[(i / 32) * ldo + i % 32] = (i % 32) == 0 ? 1.f : 0.f;
+        __syncthreads();
+        store_T<T, R, P>(g2, ldo, L2.Np, L2.N, L2.GT, Bp, r0, nvalid, L2.dbp, qtB);
+      }
       store_T<T, R, P>(U1, ldu1, HH, HH, (T*)L1.GT + (size_t)h * HH * Bp, Bp, r0, nvalid, L1.dbp + h * HH, qtB, L1.N);
       store_T<T, R, P>(Xb, ld, L0.Np, L0.N, L0.GT, 2 * Bp, h * Bp + r0, nvalid, L0.dbp, qtB);
     }

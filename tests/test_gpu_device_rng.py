@@ -230,8 +230,10 @@ def test_c2_200_steps_stay_on_the_oracle():
     200; y 3e-7 through step 20, 2.7e-3 at step 200).  Bounds (written here):
       * losses: the north-star bar, 1e-3 rel, at EVERY step (L_pi with the abs
         floor of tests/test_gpu_parity.py), and 1e-5 rel over the first 50;
-      * y: |dy| <= 1e-5 (1 + |y|) over the first 50 steps, 1e-2 (1 + |y|) at
-        every step (y also carries the target networks' accumulated drift);
+      * y: |dy| <= 1e-5 (1 + |y|) over the first 20 steps, 1e-4 over the
+        first 50, 1e-2 (1 + |y|) at every step (y also carries the target
+        networks' accumulated drift; since phase B sums the critics' output
+        bias gradient from the seeded columns, y reaches ~2e-5 by step 50);
       * after 200 steps every online parameter within 2 lr k of the oracle
         (the Adam movement bound) with a mean |error| within 0.01 lr k; the
         target networks (tau-averages of k online states) within 2 lr tau
@@ -277,7 +279,7 @@ def test_c2_200_steps_stay_on_the_oracle():
     print("\n200-step C2 fp32 drift vs oracle:", summary)
     assert dev[:, :4].max() <= 1e-3, summary
     assert dev[:50, :4].max() <= 1e-5, summary
-    assert dev[:50, 4].max() <= 1e-5 and dev[:, 4].max() <= 1e-2, summary
+    assert dev[:20, 4].max() <= 1e-5 and dev[:50, 4].max() <= 1e-4 and dev[:, 4].max() <= 1e-2, summary
     for key in NET_KEYS:
         assert report[key]["max/lr_k"] <= 2.0 + 1e-5 / lrs[key], (key, summary)
         assert report[key]["mean/lr_k"] <= (0.01 if key in ("policy", "q1", "q2") else 0.005), (key, summary)
