@@ -1108,6 +1108,12 @@ int sac_engine_create(const sac_engine_config* cfg, const sac_engine_buffers* bu
     delete e;
     return fail(SAC_E_INVALID, "layer widths need " + std::to_string(lb) + " B of LDS per workgroup (max 163840)");
   }
+  if ((int)e->hostB.size() != e->nB || (int)e->hostD.size() != e->nD) {  // the grids launch nB / nD tiles
+    const std::string m = "internal: update tiles planned " + std::to_string(e->nB) + " / " + std::to_string(e->nD) +
+                          ", built " + std::to_string(e->hostB.size()) + " / " + std::to_string(e->hostD.size());
+    delete e;
+    return fail(SAC_E_INVALID, m);
+  }
   hipStream_t s = (hipStream_t)stream;
   hipError_t err = hipMemsetAsync(buf->workspace, 0, buf->workspace_bytes, s);
   if (err == hipSuccess) err = hipMemcpyAsync(e->d, &e->h, sizeof(EngineDev), hipMemcpyHostToDevice, s);

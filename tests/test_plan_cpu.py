@@ -1,0 +1,69 @@
+"""The engine's launch plan on the CPU (no GPU needed): sac_engine_create runs
+the whole planner -- phase layouts, update tiles with their batch parts and
+bias blocks, the fused step's task table -- before its first HIP call.  On a
+machine without a GPU it must therefore stop at that first HIP call
+(SAC_E_HIP), never at the planner's own consistency check ("internal: ...",
+SAC_E_INVALID): a mismatch between the tiles the planner counts (the grids of
+phases B and D) and the tiles it builds would make the update kernels read
+descriptors that do not exist.  Every bench config, both precisions, and the
+diagnostic layouts the env switches select."""
+import ctypes
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "soft-actor-critic_amd"))
+sys.path.insert(0, ROOT)
+
+import bench  # noqa: E402
+from sac import _engine as E  # noqa: E402
+
+SAC_E_INVALID, SAC_E_HIP = -1, -2
+
+
+def _cfg(name, precision):
+    c = bench.CONFIGS[name]
+    cfg = E.EngineConfig()
+    cfg.obs_dim, cfg.act_dim, cfg.batch = c["obs"], c["act"], c["batch"]
+    qd = [c["obs"] + c["act"]] + c["hidden"] + [1]
+    pd = [c["obs"]] + c["hidden"] + [2 * c["act"]]
+    cfg.q_layers, cfg.pi_layers = len(qd) - 1, len(pd) - 1
+    for i, d in enumerate(qd):
+        cfg.q_dims[i] = d
+    for i, d in enumerate(pd):
+        cfg.pi_dims[i] = d
+    cfg.q_hidden_act = cfg.pi_hidden_act = 1  # relu
+    cfg.q_out_act = cfg.pi_out_act = 0
+    cfg.gamma, cfg.tau = 0.99, 0.005
+    cfg.log_std_min, cfg.log_std_max, cfg.action_scale = -20.0, 2.0, 1.0
+    cfg.actor_lr = cfg.critic_lr = cfg.alpha_lr = 3e-4
+    cfg.beta1, cfg.beta2, cfg.adam_eps = 0.9, 0.999, 1e-8
+    cfg.auto_entropy, cfg.target_entropy = 1, -float(c["act"])
+    cfg.precision = E.PREC_FP32 if precision == "fp32" else E.PREC_BF16
+    cfg.seed = 0
+    return cfg
+
+
+@pytest.mark.parametrize("env", ["", "SAC_PERSIST=1", "SAC_STAGE=0", "SAC_PI0_PARTS=1", "SAC_ROLE_XCD=0",
+                                 "SAC_SPLIT=0", "SAC_BPARTS=4"])
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+@pytest.mark.parametrize("name", sorted(bench.CONFIGS))
+def test_plan_is_consistent(name, precision, env, monkeypatch):
+    if env:
+        k, v = env.split("=")
+        monkeypatch.setenv(k, v)
+    lib = E.load_library()
+    cfg = _cfg(name, precision)
+    ws = lib.sac_engine_workspace_bytes(ctypes.byref(cfg))
+    assert ws > 0, lib.sac_last_error()
+    bufs = E.EngineBuffers(*([0x1000] * 15), 0x100000, ws)  # never dereferenced before the first HIP call
+    out = ctypes.c_void_p()
+    rc = lib.sac_engine_create(ctypes.byref(cfg), ctypes.byref(bufs), None, ctypes.byref(out))
+    msg = lib.sac_last_error().decode()
+    if rc == 0:  # a GPU is present: the engine exists; destroy it
+        lib.sac_engine_destroy(out)
+        pytest.skip("GPU present: the planner ran for real")
+    assert "internal" not in msg, msg
+    assert rc == SAC_E_HIP, (rc, msg)
