@@ -17,6 +17,12 @@ Extra (optional) config keys, all under ``train``:
                'reference' (Python ``random.sample`` indices + torch eps draws,
                the reference's RNG consumption)
     graph_chunk: steps per captured hipGraph for ``train_steps`` (default 32)
+    engine_device: 'auto' (default) | 'cpu'.  The reference's ``device: cpu``
+               configs (e.g. hparam_search/configs/inverted_pendulum.yaml:38)
+               run unchanged: with 'auto' and a HIP device visible, the agent
+               trains on the engine (``cuda:<current device>``) and warns once;
+               'cpu' keeps the networks on the host, where the hot path raises
+               ``EngineUnavailable`` (there is no CPU fallback).
 
 After ``load_agent`` with auto-tuning, alpha stays frozen as in the reference
 (it rebinds ``log_alpha`` but not its optimizer, agent.py:550-554); the
@@ -31,6 +37,7 @@ import os
 import pprint
 import random
 import time
+import warnings
 from collections import deque
 from copy import deepcopy
 from typing import Any, Dict, Optional
@@ -55,6 +62,23 @@ def _make_logger(cfg, env_name, agent_name):
     from .utils.experiment_logger import ExperimentLogger
 
     return ExperimentLogger(cfg, env_name=env_name, agent_name=agent_name)
+
+
+def resolve_device(train_cfg: dict) -> torch.device:
+    """Device the agent trains on.  ``train.device`` as written, except that a
+    reference config asking for ``cpu`` moves to the HIP device when one is
+    visible (``train.engine_device: auto``, the default): the step only exists
+    as the engine, and the reference's CPU configs should drop in unchanged."""
+    dev = torch.device(train_cfg["device"])
+    mode = train_cfg.get("engine_device", "auto")
+    if mode not in ("auto", "cpu"):
+        raise ValueError(f"train.engine_device must be 'auto' or 'cpu', got {mode!r}")
+    if dev.type == "cpu" and mode == "auto" and torch.cuda.is_available():
+        gpu = torch.device("cuda", torch.cuda.current_device())
+        warnings.warn(f"train.device is 'cpu': the SAC step runs on the MI355X engine, training on {gpu} "
+                      "(train.engine_device: cpu keeps the host device)", stacklevel=3)
+        return gpu
+    return dev
 
 
 def due_updates(old_steps: int, new_steps: int, update_frequency: int, gradient_steps: int) -> int:
@@ -214,7 +238,7 @@ class SAC:
     def __init__(self, env, config: dict):
         self.env = env
         self.config = config
-        self.device = torch.device(config["train"]["device"])
+        self.device = resolve_device(config["train"])
         self.replay_buffer = ReplayBuffer(config["buffer"]["capacity"], device=self.device)
         self.obs_size = env.observation_space.shape[0]
         self.action_size = env.action_space.shape[0]

@@ -55,6 +55,23 @@ def test_hot_path_fails_loudly_without_gpu():
         agent.store_transition(np.zeros(meta["obs"]), np.zeros(meta["act"]), 0.0, np.zeros(meta["obs"]), False)
 
 
+def test_cpu_device_resolution(monkeypatch):
+    """``train.device: cpu`` (the reference's CPU configs) stays on the host
+    only without a HIP device or with ``engine_device: cpu``; with a device
+    visible it moves to the engine's GPU (the GPU side: test_gpu_rollout)."""
+    from sac.agent import resolve_device
+
+    assert resolve_device({"device": "cpu"}) == torch.device("cpu")  # no GPU in this container
+    with pytest.raises(ValueError):
+        resolve_device({"device": "cpu", "engine_device": "gpu"})
+    monkeypatch.setattr(torch.cuda, "is_available", lambda: True)
+    monkeypatch.setattr(torch.cuda, "current_device", lambda: 0)
+    with pytest.warns(UserWarning, match="MI355X engine"):
+        assert resolve_device({"device": "cpu"}) == torch.device("cuda", 0)
+    assert resolve_device({"device": "cpu", "engine_device": "cpu"}) == torch.device("cpu")
+    assert resolve_device({"device": "cuda:0"}) == torch.device("cuda", 0)
+
+
 def test_substeps_need_the_engine():
     """The reference sub-steps run on the engine's device state: without a GPU
     they fail loudly like the fused step (no CPU fallback)."""

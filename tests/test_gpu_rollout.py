@@ -254,3 +254,27 @@ def test_training_loop_logger_matches_reference(tmp_path, monkeypatch):
     e = {st: (q1.item(), q2.item()) for st, q1, q2 in eager}
     for c1, c2 in zip(got_t["QValues/Q1"], got_t["QValues/Q2"]):
         assert (c1[3], c2[3]) == e[c1[4]]
+
+
+def test_cpu_device_config_trains_on_the_engine():
+    """A reference config with ``train.device: cpu`` (hparam_search/configs/
+    inverted_pendulum.yaml:38) drops in: the agent moves to the HIP device,
+    builds the engine, and runs the reference loop bit-identically to the same
+    config written with ``device: cuda``."""
+    from sac.agent import SAC
+
+    cfg = _cfg()
+    cpu_cfg = copy.deepcopy(cfg)
+    cpu_cfg["train"]["device"] = "cpu"
+    with pytest.warns(UserWarning, match="runs on the MI355X engine"):
+        a = SAC(_env(), cpu_cfg)
+    assert a.device.type == "cuda" and a.engine is not None
+    assert a.config["train"]["device"] == "cpu"  # the logged hparam stays as written
+    b = SAC(_env(), copy.deepcopy(cfg))
+    a.run_training_loop(num_episodes=6, tqdm_disable=True)
+    b.run_training_loop(num_episodes=6, tqdm_disable=True)
+    torch.cuda.synchronize()
+    assert a.engine.steps_done == b.engine.steps_done > 0
+    sa, sb = a.engine.state_tensors(), b.engine.state_tensors()
+    for k in sa:
+        assert torch.equal(sa[k], sb[k]), k
