@@ -270,8 +270,9 @@ def test_cpu_device_config_trains_on_the_engine():
         a = SAC(_env(), cpu_cfg)
     assert a.device.type == "cuda" and a.engine is not None
     assert a.config["train"]["device"] == "cpu"  # the logged hparam stays as written
-    b = SAC(_env(), copy.deepcopy(cfg))
+    # one agent at a time: construction seeds the process-wide RNGs the loop draws from
     a.run_training_loop(num_episodes=6, tqdm_disable=True)
+    b = SAC(_env(), copy.deepcopy(cfg))
     b.run_training_loop(num_episodes=6, tqdm_disable=True)
     torch.cuda.synchronize()
     assert a.engine.steps_done == b.engine.steps_done > 0
