@@ -130,13 +130,45 @@ def test_baseline_config_matches_oracle(cfg, capacity, steps, precision):
     networks and log alpha, with this file's tolerances."""
     import bench
 
-    c = dict(bench.CONFIGS[cfg])
-    bench.CONFIGS[cfg] = dict(c, capacity=capacity)
+    _check_config_against_oracle(dict(bench.CONFIGS[cfg], capacity=capacity), precision, steps,
+                                 roles=cfg != "c3")
+
+
+# Shapes at the edges of the kernels' tiling, none of them a BASELINE config:
+# ragged last row tiles (B % 16 != 0) on each of the three phase-kernel layouts
+# (hidden split, per-network roles, one block per row tile), a one-row batch, an
+# input wider than the hidden layers (Kp 320 > 256) and four-layer nets.
+EDGE_SHAPES = {
+    "split_b250": dict(obs=24, act=4, hidden=[256, 256], batch=250, capacity=2048),
+    "roles_b17": dict(obs=5, act=1, hidden=[64, 64], batch=17, capacity=512),
+    "b1": dict(obs=3, act=2, hidden=[32, 32], batch=1, capacity=64),
+    "rowtile_b4001": dict(obs=24, act=4, hidden=[256, 256], batch=4001, capacity=8192),
+    "obs300": dict(obs=300, act=6, hidden=[256, 256], batch=64, capacity=1024),
+    "deep4": dict(obs=11, act=3, hidden=[128, 96, 64], batch=80, capacity=1024),
+}
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+@pytest.mark.parametrize("shape", sorted(EDGE_SHAPES))
+def test_edge_shapes_match_oracle(shape, precision):
+    """Ragged and extreme shapes against the oracle, with the same checks and
+    tolerances as the BASELINE configs (parity unpinned by the reference at
+    these shapes; the oracle is pinned by the 8 reference fixtures)."""
+    c = dict(EDGE_SHAPES[shape], name=shape)
+    _check_config_against_oracle(c, precision, 2 if c["batch"] > 1024 else 3)
+
+
+def _check_config_against_oracle(c, precision, steps, roles=None):
+    import bench
+
+    ckey = "_parity_" + c.get("name", "cfg")
+    bench.CONFIGS[ckey] = c
     try:
-        eng, rb, cc = bench.build_engine(cfg, precision, 3, torch.device("cuda", 0))
+        eng, rb, cc = bench.build_engine(ckey, precision, 3, torch.device("cuda", 0))
     finally:
-        bench.CONFIGS[cfg] = c
-    assert eng.roles == (cfg != "c3")
+        del bench.CONFIGS[ckey]
+    if roles is not None:
+        assert eng.roles == roles
     B, A = cc["batch"], cc["act"]
     sds = {k: {kk: v.detach().cpu().numpy().copy() for kk, v in m.state_dict().items()} for k, m in eng.nets.items()}
     hp = O.SacHyper(alpha=0.1, auto_entropy_tuning=True)  # bench.build_engine's hyper-parameters
@@ -159,7 +191,7 @@ def test_baseline_config_matches_oracle(cfg, capacity, steps, precision):
         got = eng.losses()
         floor = float(np.mean(np.abs(st.alpha * ref["log_pi"])) + np.mean(np.abs(ref["y"]))) + 1e-6
         for i, (gv, w) in enumerate(zip(got, ref["losses"])):
-            assert _loss_ok(gv, w, floor if i == 2 else 1e-3, rtol), (cfg, precision, k, i, gv, w)
+            assert _loss_ok(gv, w, floor if i == 2 else 1e-3, rtol), (ckey, precision, k, i, gv, w)
         y = eng.last_targets().cpu().numpy()
         lp = eng.last_log_pi().cpu().numpy()
         if precision == "fp32":
@@ -168,20 +200,20 @@ def test_baseline_config_matches_oracle(cfg, capacity, steps, precision):
         else:
             for gv, want in ((y, ref["y"]), (lp, ref["log_pi"])):
                 scale = np.abs(want).mean() + 1.0
-                assert np.abs(gv - want).mean() <= 1e-2 * scale, (cfg, k, np.abs(gv - want).mean(), scale)
+                assert np.abs(gv - want).mean() <= 1e-2 * scale, (ckey, k, np.abs(gv - want).mean(), scale)
         for key, ek in BENCH_NETS.items():
             mine = {kk: v.detach().cpu().numpy() for kk, v in eng.nets[ek].state_dict().items()}
             lr = lrs[key] * (k if key in ("policy", "q1", "q2") else k * (k + 1) / 2)
             ds = []
             for pk, want in _oracle_net(st, key).state_dict().items():
                 d = np.abs(mine[pk] - want)
-                assert d.max() <= 2 * lr + 1e-5, (cfg, precision, k, key, pk, d.max())
+                assert d.max() <= 2 * lr + 1e-5, (c.get('name'), precision, k, key, pk, d.max())
                 if precision == "fp32":
-                    assert np.mean(d <= 1e-6) >= 0.995, (cfg, k, key, pk, np.mean(d <= 1e-6))
+                    assert np.mean(d <= 1e-6) >= 0.995, (c.get('name'), k, key, pk, np.mean(d <= 1e-6))
                 ds.append(d.ravel())
             if precision == "bf16":
                 d = np.concatenate(ds)
-                assert d.mean() <= 0.05 * lr + 1e-7, (cfg, k, key, d.mean())
+                assert d.mean() <= 0.05 * lr + 1e-7, (c.get('name'), k, key, d.mean())
         la = float(eng.alpha_state[0].item())
         assert abs(la - st.log_alpha) <= (1e-7 if precision == "fp32" else 1e-5), (la, st.log_alpha)
     eng.check()
