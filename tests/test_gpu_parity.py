@@ -136,14 +136,15 @@ def test_baseline_config_matches_oracle(cfg, capacity, steps, precision):
 
 # Shapes at the edges of the kernels' tiling, none of them a BASELINE config:
 # ragged last row tiles (B % 16 != 0) on each of the three phase-kernel layouts
-# (hidden split, per-network roles, one block per row tile), a one-row batch, an
-# input wider than the hidden layers (Kp 320 > 256) and four-layer nets.
+# (hidden split, per-network roles, one block per row tile), a one-row batch,
+# the widest input the [256, 256] nets take (obs 256 + act 6: Kp 288 > 256 for
+# the critics) and four-layer nets.
 EDGE_SHAPES = {
     "split_b250": dict(obs=24, act=4, hidden=[256, 256], batch=250, capacity=2048),
     "roles_b17": dict(obs=5, act=1, hidden=[64, 64], batch=17, capacity=512),
     "b1": dict(obs=3, act=2, hidden=[32, 32], batch=1, capacity=64),
     "rowtile_b4001": dict(obs=24, act=4, hidden=[256, 256], batch=4001, capacity=8192),
-    "obs300": dict(obs=300, act=6, hidden=[256, 256], batch=64, capacity=1024),
+    "obs256": dict(obs=256, act=6, hidden=[256, 256], batch=64, capacity=1024),
     "deep4": dict(obs=11, act=3, hidden=[128, 96, 64], batch=80, capacity=1024),
 }
 
@@ -156,6 +157,28 @@ def test_edge_shapes_match_oracle(shape, precision):
     these shapes; the oracle is pinned by the 8 reference fixtures)."""
     c = dict(EDGE_SHAPES[shape], name=shape)
     _check_config_against_oracle(c, precision, 2 if c["batch"] > 1024 else 3)
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_too_wide_input_is_refused_cleanly(precision):
+    """An input the LDS layout cannot hold (obs 300 with [256, 256] nets: the
+    workgroup would need > 160 KiB) fails in engine creation with the size in
+    the message -- no launch, no fallback."""
+    import bench
+    from sac._engine import EngineError
+
+    bench.CONFIGS["_parity_obs300"] = dict(obs=300, act=6, hidden=[256, 256], batch=64, capacity=256)
+    try:
+        with pytest.raises(EngineError, match="B of LDS per workgroup"):
+            bench.build_engine("_parity_obs300", precision, 3, torch.device("cuda", 0))
+    finally:
+        del bench.CONFIGS["_parity_obs300"]
+
+
+def _engine_mlp(eng, key):
+    """Oracle MLP holding the engine's current parameters of one network."""
+    return O.MLP.from_state_dict({kk: v.detach().cpu().numpy().copy() for kk, v in eng.nets[key].state_dict().items()},
+                                 "relu")
 
 
 def _check_config_against_oracle(c, precision, steps, roles=None):
@@ -176,15 +199,20 @@ def _check_config_against_oracle(c, precision, steps, roles=None):
                           O.MLP.from_state_dict(sds["q2"], "relu"), hp, A)
     rows = {k: getattr(rb, k).cpu().numpy() for k in ("obs", "act", "rew", "next_obs", "done")}
     g = np.random.default_rng(11)
-    rtol = 1e-4 if precision == "fp32" else 2e-3
+    # bf16: 2e-3 at B >= 256; a loss over fewer rows averages fewer independent
+    # product roundings, so its relative error grows like 1 / sqrt(B)
+    rtol = 1e-4 if precision == "fp32" else 2e-3 * max(1.0, (256 / B) ** 0.5)
     lrs = {"policy": hp.actor_lr, "q1": hp.critic_lr, "q2": hp.critic_lr, "q1t": hp.critic_lr * hp.tau,
            "q2t": hp.critic_lr * hp.tau}
     for k in range(1, steps + 1):
         idx = g.choice(len(rb), size=B, replace=False).astype(np.int32)
         et = g.standard_normal((B, A)).astype(np.float32)
         ea = g.standard_normal((B, A)).astype(np.float32)
-        ref = O.training_step(st, hp, O.Batch(rows["obs"][idx], rows["act"][idx], rows["rew"][idx],
-                                              rows["next_obs"][idx], rows["done"][idx]), et, ea)
+        bt = O.Batch(rows["obs"][idx], rows["act"][idx], rows["rew"][idx], rows["next_obs"][idx], rows["done"][idx])
+        # the engine's own pre-step state, for the one-step (local) check of y and log pi
+        pre = {n: _engine_mlp(eng, n) for n in ("pi", "q1t", "q2t")}
+        alpha_pre = np.float32(eng.alpha_state[1].item())
+        ref = O.training_step(st, hp, bt, et, ea)
         eng.train(rb, 1, indices=torch.from_numpy(idx).reshape(1, B),
                   eps=torch.from_numpy(np.stack([et, ea])).reshape(1, 2, B, A))
         torch.cuda.synchronize()
@@ -195,8 +223,20 @@ def _check_config_against_oracle(c, precision, steps, roles=None):
         y = eng.last_targets().cpu().numpy()
         lp = eng.last_log_pi().cpu().numpy()
         if precision == "fp32":
-            np.testing.assert_allclose(y, ref["y"], rtol=1e-4, atol=1e-4)
-            np.testing.assert_allclose(lp, ref["log_pi"], rtol=1e-4, atol=1e-4)
+            # one step from the engine's own state: the kernels' arithmetic alone
+            _, lp_loc, _ = O.policy_sample(pre["pi"], bt.s, ea, hp.policy)
+            a2, lp2, _ = O.policy_sample(pre["pi"], bt.s2, et, hp.policy)
+            mq = np.minimum(O.q_forward(pre["q1t"], bt.s2, a2)[0], O.q_forward(pre["q2t"], bt.s2, a2)[0])
+            y_loc = (bt.r + (np.float32(hp.gamma) * (np.float32(1) - bt.d)) * (mq - alpha_pre * lp2)).astype(np.float32)
+            np.testing.assert_allclose(y, y_loc, rtol=1e-4, atol=1e-4)
+            np.testing.assert_allclose(lp, lp_loc, rtol=1e-4, atol=1e-4)
+            # against the oracle's own trajectory: from step 2 on, an Adam update
+            # whose gradient is ~0 may take the other sign under another
+            # summation order (that element moves +-lr instead of -+lr, inside
+            # the parameter bounds below); measured 6.1e-4 in log pi at obs 256, step 3
+            tol = 1e-4 if k == 1 else 2e-3
+            np.testing.assert_allclose(y, ref["y"], rtol=tol, atol=tol)
+            np.testing.assert_allclose(lp, ref["log_pi"], rtol=tol, atol=tol)
         else:
             for gv, want in ((y, ref["y"]), (lp, ref["log_pi"])):
                 scale = np.abs(want).mean() + 1.0

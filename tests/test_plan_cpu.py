@@ -67,3 +67,23 @@ def test_plan_is_consistent(name, precision, env, monkeypatch):
         pytest.skip("GPU present: the planner ran for real")
     assert "internal" not in msg, msg
     assert rc == SAC_E_HIP, (rc, msg)
+
+
+@pytest.mark.parametrize("obs,act,hidden", [(300, 6, [256, 256]), (24, 4, [512, 512]), (24, 4, [384, 384])])
+def test_shapes_past_the_lds_layout_are_refused(obs, act, hidden):
+    """Widths whose phase-kernel workgroup would need more than the CU's 160 KiB
+    of LDS (DESIGN §1: hidden layers up to 256 wide, as every reference config;
+    obs up to 256 with [256, 256] nets) are refused by sac_engine_create with
+    SAC_E_INVALID and the byte count, before any HIP call."""
+    bench.CONFIGS["_wide"] = dict(obs=obs, act=act, hidden=hidden, batch=64, capacity=256)
+    try:
+        cfg = _cfg("_wide", "fp32")
+    finally:
+        del bench.CONFIGS["_wide"]
+    lib = E.load_library()
+    ws = lib.sac_engine_workspace_bytes(ctypes.byref(cfg))
+    bufs = E.EngineBuffers(*([0x1000] * 15), 0x100000, ws)
+    out = ctypes.c_void_p()
+    rc = lib.sac_engine_create(ctypes.byref(cfg), ctypes.byref(bufs), None, ctypes.byref(out))
+    msg = lib.sac_last_error().decode()
+    assert rc == SAC_E_INVALID and "B of LDS per workgroup (max 163840)" in msg, (rc, msg)
