@@ -257,3 +257,70 @@ def _check_config_against_oracle(c, precision, steps, roles=None):
         la = float(eng.alpha_state[0].item())
         assert abs(la - st.log_alpha) <= (1e-7 if precision == "fp32" else 1e-5), (la, st.log_alpha)
     eng.check()
+
+
+def _oracle_state_from_engine(eng, act):
+    """The engine's full training state as an oracle SacState: parameters of the
+    five networks, Adam moments and step counts, and the alpha state."""
+    to_np = lambda t: t.detach().cpu().numpy().copy()  # noqa: E731
+    mlp = {k: _engine_mlp(eng, k) for k in ("pi", "q1", "q2", "q1t", "q2t")}
+    steps = eng.opt_steps.cpu().numpy()
+    opt = {}
+    for i, k in enumerate(("pi", "q1", "q2")):
+        m, v = eng.adam_views(k)
+        opt[k] = O.AdamState([to_np(x) for x in m], [to_np(x) for x in v], float(steps[i]))
+    al = eng.alpha_state.cpu().numpy()
+    return O.SacState(mlp["pi"], mlp["q1"], mlp["q2"], mlp["q1t"], mlp["q2t"], opt["pi"], opt["q1"], opt["q2"], act,
+                      log_alpha=float(al[0]), alpha=float(al[1]), opt_alpha_m=float(al[2]),
+                      opt_alpha_v=float(al[3]), opt_alpha_step=float(steps[3]))
+
+
+@pytest.mark.parametrize("shape", ["c2_split", "c4", "roles_b384", "rowtile_b2000"])
+def test_one_step_from_the_engine_state(shape, monkeypatch):
+    """Per-step parity without trajectory drift (fp32): before every step the
+    oracle is loaded with the engine's FULL state (parameters, Adam moments and
+    step counts, alpha), runs the same step, and every post-step parameter of
+    the five networks must match the engine's to 1e-6 for >= 99.9% of the
+    elements (a handful may sit where Adam divides a ~0 gradient by ~eps) and
+    to 2 lr everywhere; losses to 1e-5 rel (L_pi against the scale of its terms).  Four steps per shape, covering the
+    hidden-split, role and row-tile kernel layouts."""
+    import bench
+
+    c = {"c2_split": dict(obs=24, act=4, hidden=[256, 256], batch=256, capacity=2048),
+         "c4": dict(obs=32, act=2, hidden=[256, 256], batch=256, capacity=2048),
+         "roles_b384": dict(obs=24, act=4, hidden=[256, 256], batch=384, capacity=2048),
+         "rowtile_b2000": dict(obs=17, act=6, hidden=[128, 128], batch=2000, capacity=4096)}[shape]
+    if shape == "roles_b384":
+        monkeypatch.setenv("SAC_SPLIT", "0")
+    bench.CONFIGS["_local"] = c
+    try:
+        eng, rb, cc = bench.build_engine("_local", "fp32", 3, torch.device("cuda", 0))
+    finally:
+        del bench.CONFIGS["_local"]
+    B, A = cc["batch"], cc["act"]
+    hp = O.SacHyper(alpha=0.1, auto_entropy_tuning=True)
+    rows = {k: getattr(rb, k).cpu().numpy() for k in ("obs", "act", "rew", "next_obs", "done")}
+    g = np.random.default_rng(11)
+    lrs = {"pi": hp.actor_lr, "q1": hp.critic_lr, "q2": hp.critic_lr, "q1t": hp.critic_lr, "q2t": hp.critic_lr}
+    for k in range(1, 5):
+        idx = g.choice(len(rb), size=B, replace=False).astype(np.int32)
+        et = g.standard_normal((B, A)).astype(np.float32)
+        ea = g.standard_normal((B, A)).astype(np.float32)
+        st = _oracle_state_from_engine(eng, A)
+        ref = O.training_step(st, hp, O.Batch(rows["obs"][idx], rows["act"][idx], rows["rew"][idx],
+                                              rows["next_obs"][idx], rows["done"][idx]), et, ea)
+        eng.train(rb, 1, indices=torch.from_numpy(idx).reshape(1, B),
+                  eps=torch.from_numpy(np.stack([et, ea])).reshape(1, 2, B, A))
+        torch.cuda.synchronize()
+        # L_pi = mean(alpha log pi - min Q) cancels: its scale is that of its terms
+        floor = float(np.mean(np.abs(st.alpha * ref["log_pi"])) + np.mean(np.abs(ref["y"])))
+        for i, (gv, w) in enumerate(zip(eng.losses(), ref["losses"])):
+            assert abs(gv - w) <= 1e-5 * max(abs(w), floor if i == 2 else 1e-3), (shape, k, i, gv, w)
+        for n, net in (("pi", st.pi), ("q1", st.q1), ("q2", st.q2), ("q1t", st.q1t), ("q2t", st.q2t)):
+            mine = {kk: v.detach().cpu().numpy() for kk, v in eng.nets[n].state_dict().items()}
+            for pk, want in net.state_dict().items():
+                d = np.abs(mine[pk] - want)
+                assert d.max() <= 2 * lrs[n], (shape, k, n, pk, d.max())
+                assert np.mean(d <= 1e-6) >= 0.999, (shape, k, n, pk, np.mean(d <= 1e-6))
+        assert abs(float(eng.alpha_state[0].item()) - st.log_alpha) <= 1e-7
+    eng.check()
