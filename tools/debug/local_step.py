@@ -74,7 +74,11 @@ def f64_pi_update(pre_pi, mo, idx, ea):
                 x = torch.relu(x)
         return x[:, 0]
     alpha = float(alpha_pre)
-    loss = (alpha * lp - torch.minimum(q("q1"), q("q2"))).mean()
+    qa, qb = q("q1"), q("q2")
+    gap = (qa - qb).abs().detach()
+    print(f"      f64 min-Q: smallest |q1 - q2| {gap.min().item():.3e} (row {int(gap.argmin())}),"
+          f" rows under 1e-5: {(gap < 1e-5).sum().item()}", flush=True)
+    loss = (alpha * lp - torch.minimum(qa, qb)).mean()
     loss.backward()
     g = W[0].grad.numpy()
     m0, v0 = mo[0][0].astype(np.float64), mo[1][0].astype(np.float64)
