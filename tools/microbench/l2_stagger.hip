@@ -122,6 +122,95 @@ __global__ void __launch_bounds__(512) layers(const float* __restrict__ W, int n
   if (pfx[0] == 12345.f) sink[0] = pfx[1];
 }
 
+// Twin layers (e.g. Q1t and Q2t at the same depth) on 16 rows: mode 0 runs
+// them one after the other (the engine's row-tile kernels: each wave owns one
+// tile pair per layer); mode 1 runs them as ONE block-diagonal GEMM (each wave
+// owns pair (w, w + 8) of net a and the same pair of net b; net b's loads are
+// issued before net a's MFMAs), one barrier per depth instead of two.
+__global__ void __launch_bounds__(512) twin(const float* __restrict__ W, int nl, int mode, long long* out, float* sink) {
+  __shared__ float lds[4 * 16 * 260];
+  const int ld = 260;
+  float* X[2] = {lds, lds + 16 * ld};
+  float* Y[2] = {lds + 2 * 16 * ld, lds + 3 * 16 * ld};
+  for (int i = threadIdx.x; i < 2 * 16 * ld; i += 512) lds[i] = 0.01f * (i % 7);
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int c = lane & 15, g = lane >> 4;
+  long long t0 = __builtin_amdgcn_s_memrealtime();
+  auto layer = [&](const float* Wn, const float* Xn, float* Yn, f32x4 (&f0)[16], f32x4 (&f1)[16]) {
+    f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
+    const float* arow = Xn + c * ld + g * 4;
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const f32x4 a = *(const f32x4*)(arow + u * 16);
+      mma4(acc0, a, f0[u]);
+      mma4(acc1, a, f1[u]);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      Yn[(g * 4 + i) * ld + wave * 16 + c] = fmaxf(acc0[i] * 1e-3f, 0.f);
+      Yn[(g * 4 + i) * ld + (wave + 8) * 16 + c] = fmaxf(acc1[i] * 1e-3f, 0.f);
+    }
+  };
+  for (int l = 0; l < nl; ++l) {
+    const float* Wa = W + (size_t)(l & 3) * 2 * 65536;
+    const float* Wb = Wa + 65536;
+    auto ld16 = [&](const float* Wn, f32x4 (&f0)[16], f32x4 (&f1)[16]) {
+      const f32x4* p0 = (const f32x4*)(Wn + (size_t)wave * 4096) + lane;
+      const f32x4* p1 = (const f32x4*)(Wn + (size_t)(wave + 8) * 4096) + lane;
+#pragma unroll
+      for (int u = 0; u < 16; ++u) { f0[u] = p0[u * 64]; f1[u] = p1[u * 64]; }
+    };
+    if (mode == 0) {
+      for (int n = 0; n < 2; ++n) {
+        f32x4 f0[16], f1[16];
+        ld16(n ? Wb : Wa, f0, f1);
+        layer(n ? Wb : Wa, X[n], Y[n], f0, f1);
+        __syncthreads();
+      }
+    } else {  // four 8-chunk batches (a lo, a hi, b lo, b hi), each issued one batch ahead
+      f32x4 p0[8], p1[8], q0[8], q1[8];
+      auto ld8 = [&](const float* Wn, int ch0, f32x4 (&f0)[8], f32x4 (&f1)[8]) {
+        const f32x4* r0 = (const f32x4*)(Wn + (size_t)wave * 4096) + lane;
+        const f32x4* r1 = (const f32x4*)(Wn + (size_t)(wave + 8) * 4096) + lane;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) { f0[u] = r0[(ch0 + u) * 64]; f1[u] = r1[(ch0 + u) * 64]; }
+      };
+      auto mm8 = [&](const float* Xn, int ch0, f32x4 (&f0)[8], f32x4 (&f1)[8], f32x4& acc0, f32x4& acc1) {
+        const float* arow = Xn + c * ld + g * 4;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const f32x4 a = *(const f32x4*)(arow + (ch0 + u) * 16);
+          mma4(acc0, a, f0[u]);
+          mma4(acc1, a, f1[u]);
+        }
+      };
+      f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = a0, b0 = a0, b1 = a0;
+      ld8(Wa, 0, p0, p1);
+      ld8(Wa, 8, q0, q1);
+      mm8(X[0], 0, p0, p1, a0, a1);
+      ld8(Wb, 0, p0, p1);
+      mm8(X[0], 8, q0, q1, a0, a1);
+      ld8(Wb, 8, q0, q1);
+      mm8(X[1], 0, p0, p1, b0, b1);
+      mm8(X[1], 8, q0, q1, b0, b1);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        Y[0][(g * 4 + i) * ld + wave * 16 + c] = fmaxf(a0[i] * 1e-3f, 0.f);
+        Y[0][(g * 4 + i) * ld + (wave + 8) * 16 + c] = fmaxf(a1[i] * 1e-3f, 0.f);
+        Y[1][(g * 4 + i) * ld + wave * 16 + c] = fmaxf(b0[i] * 1e-3f, 0.f);
+        Y[1][(g * 4 + i) * ld + (wave + 8) * 16 + c] = fmaxf(b1[i] * 1e-3f, 0.f);
+      }
+      __syncthreads();
+    }
+    float* t = X[0]; X[0] = Y[0]; Y[0] = t;
+    t = X[1]; X[1] = Y[1]; Y[1] = t;
+  }
+  long long t1 = __builtin_amdgcn_s_memrealtime();
+  if (threadIdx.x == 0) out[blockIdx.x] = t1 - t0;
+  if (threadIdx.x < 16) sink[blockIdx.x * 16 + threadIdx.x] = X[0][threadIdx.x] + X[1][threadIdx.x];
+}
+
 int main(int argc, char** argv) {
   const int G = argc > 1 ? atoi(argv[1]) : 256;
   const int nl = 64;
@@ -149,5 +238,16 @@ int main(int argc, char** argv) {
       printf("rows %2d mode %d: per layer median %.2f us, max %.2f us -> %.1f GB/s per CU\n", rt * 16, mode, med, mx,
              262144.0 / (med * 1e3));
     }
+  for (int mode = 0; mode <= 1; ++mode) {
+    const int nlt = 16;
+    for (int rep = 0; rep < 3; ++rep) {
+      twin<<<G, 512>>>(W, nlt, mode, out, sink);
+      CHK(hipDeviceSynchronize());
+    }
+    CHK(hipMemcpy(h.data(), out, G * 8, hipMemcpyDeviceToHost));
+    std::sort(h.begin(), h.end());
+    printf("twin 256x256 layers, 16 rows, %s: per depth (both nets) median %.2f us\n",
+           mode ? "one block-diagonal GEMM" : "one net after the other", h[G / 2] * 10.0 / nlt / 1000.0);
+  }
   return 0;
 }
