@@ -211,6 +211,85 @@ __global__ void __launch_bounds__(512) twin(const float* __restrict__ W, int nl,
   if (threadIdx.x < 16) sink[blockIdx.x * 16 + threadIdx.x] = X[0][threadIdx.x] + X[1][threadIdx.x];
 }
 
+// A whole 3-layer critic forward on 16 rows, as the row-tile kernels run it:
+// layer 0 (K 32 -> 256: one 2-chunk batch per wave), layer 1 (256 -> 256),
+// layer 2 (256 -> N = 1, padded to 2 tiles: waves 0 and 1, two 8-chunk
+// batches each), a barrier after each layer, bias + ReLU epilogues.
+__global__ void __launch_bounds__(512) mlp3(const float* __restrict__ W, int nrep, long long* out, float* sink) {
+  __shared__ float lds[2 * 16 * 260];
+  const int ld = 260;
+  float* X = lds;
+  float* Y = lds + 16 * ld;
+  for (int i = threadIdx.x; i < 16 * ld; i += 512) X[i] = 0.01f * (i % 7);
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int c = lane & 15, g = lane >> 4;
+  long long t0 = __builtin_amdgcn_s_memrealtime();
+  for (int rep = 0; rep < nrep; ++rep) {
+    const float* W0 = W + (size_t)(rep & 3) * 3 * 65536;  // [256][32] packed
+    const float* W1 = W0 + 65536;                          // [256][256]
+    const float* W2 = W1 + 65536;                          // [32][256]
+    {  // layer 0
+      const f32x4* p0 = (const f32x4*)(W0 + (size_t)wave * 512) + lane;
+      const f32x4* p1 = (const f32x4*)(W0 + (size_t)(wave + 8) * 512) + lane;
+      f32x4 f0[2], f1[2], acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
+      for (int u = 0; u < 2; ++u) { f0[u] = p0[u * 64]; f1[u] = p1[u * 64]; }
+      const float* arow = X + c * ld + g * 4;
+      for (int u = 0; u < 2; ++u) {
+        const f32x4 a = *(const f32x4*)(arow + u * 16);
+        mma4(acc0, a, f0[u]);
+        mma4(acc1, a, f1[u]);
+      }
+      for (int i = 0; i < 4; ++i) {
+        Y[(g * 4 + i) * ld + wave * 16 + c] = fmaxf(acc0[i] + 0.01f, 0.f);
+        Y[(g * 4 + i) * ld + (wave + 8) * 16 + c] = fmaxf(acc1[i] + 0.01f, 0.f);
+      }
+      __syncthreads();
+    }
+    {  // layer 1
+      const f32x4* p0 = (const f32x4*)(W1 + (size_t)wave * 4096) + lane;
+      const f32x4* p1 = (const f32x4*)(W1 + (size_t)(wave + 8) * 4096) + lane;
+      f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
+      const float* arow = Y + c * ld + g * 4;
+      for (int bb = 0; bb < 2; ++bb) {
+        f32x4 f0[8], f1[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) { f0[u] = p0[(bb * 8 + u) * 64]; f1[u] = p1[(bb * 8 + u) * 64]; }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const f32x4 a = *(const f32x4*)(arow + (bb * 8 + u) * 16);
+          mma4(acc0, a, f0[u]);
+          mma4(acc1, a, f1[u]);
+        }
+      }
+      for (int i = 0; i < 4; ++i) {
+        X[(g * 4 + i) * ld + wave * 16 + c] = fmaxf(acc0[i] + 0.01f, 0.f);
+        X[(g * 4 + i) * ld + (wave + 8) * 16 + c] = fmaxf(acc1[i] + 0.01f, 0.f);
+      }
+      __syncthreads();
+    }
+    if (wave < 2) {  // layer 2: tile `wave` of 2, 16 chunks
+      const f32x4* p0 = (const f32x4*)(W2 + (size_t)wave * 4096) + lane;
+      f32x4 acc0 = {0.f, 0.f, 0.f, 0.f};
+      const float* arow = X + c * ld + g * 4;
+      for (int bb = 0; bb < 2; ++bb) {
+        f32x4 f0[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) f0[u] = p0[(bb * 8 + u) * 64];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) mma4(acc0, *(const f32x4*)(arow + (bb * 8 + u) * 16), f0[u]);
+      }
+      for (int i = 0; i < 4; ++i) Y[(g * 4 + i) * ld + wave * 16 + c] = acc0[i];
+    }
+    __syncthreads();
+    if (threadIdx.x < 16) X[threadIdx.x] += Y[threadIdx.x * ld] * 1e-6f;  // the head reads q
+    __syncthreads();
+  }
+  long long t1 = __builtin_amdgcn_s_memrealtime();
+  if (threadIdx.x == 0) out[blockIdx.x] = t1 - t0;
+  if (threadIdx.x < 16) sink[blockIdx.x * 16 + threadIdx.x] = X[threadIdx.x];
+}
+
 int main(int argc, char** argv) {
   const int G = argc > 1 ? atoi(argv[1]) : 256;
   const int nl = 64;
@@ -248,6 +327,16 @@ int main(int argc, char** argv) {
     std::sort(h.begin(), h.end());
     printf("twin 256x256 layers, 16 rows, %s: per depth (both nets) median %.2f us\n",
            mode ? "one block-diagonal GEMM" : "one net after the other", h[G / 2] * 10.0 / nlt / 1000.0);
+  }
+  {
+    const int nrep = 16;
+    for (int rep = 0; rep < 3; ++rep) {
+      mlp3<<<G, 512>>>(W, nrep, out, sink);
+      CHK(hipDeviceSynchronize());
+    }
+    CHK(hipMemcpy(h.data(), out, G * 8, hipMemcpyDeviceToHost));
+    std::sort(h.begin(), h.end());
+    printf("3-layer critic forward (24+4 -> 256 -> 256 -> 1), 16 rows: median %.2f us\n", h[G / 2] * 10.0 / nrep / 1000.0);
   }
   return 0;
 }
