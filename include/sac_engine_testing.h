@@ -29,6 +29,10 @@ int sac_engine_uses_split(const sac_engine *e);
  * step in ONE launch, counters between them) when the engine uses it, else 0
  * (four launches per step). */
 int sac_engine_uses_fused_step(const sac_engine *e);
+/* Launches per gradient step of the large-batch stage path (sac_wide.h:
+ * layer-synchronous GEMM stages for phases A and C, used where the per-network
+ * role kernels do not fit), else 0. */
+int sac_engine_uses_wide(const sac_engine *e);
 /* Host evaluation of the device sampler (the same inline code as the sampler
  * inside sac_engine_train and sac_replay_sample_indices): out[b] = b-th element
  * of the Philox-keyed Feistel permutation of [0, size) for RNG (seed, step). */

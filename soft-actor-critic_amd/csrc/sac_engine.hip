@@ -35,6 +35,7 @@
 #include "sac_phases.h"
 #include "sac_split.h"
 #include "sac_persist.h"
+#include "sac_wide.h"
 
 // ============================================================================ params / replay
 template <typename T>
@@ -300,6 +301,18 @@ static int fail(int code, const std::string& msg) {
     if (_e != hipSuccess) return fail(SAC_E_HIP, std::string(#x ": ") + hipGetErrorString(_e));    \
   } while (0)
 
+// Workspace offsets of the large-batch stage path (sac_wide.h), from plan()
+struct WideLay {
+  int on = 0, Brw = 0, hp = 0, hq = 0;
+  size_t o_dev = 0, o_jobs = 0;
+  size_t o_xpi0 = 0, o_xq0 = 0, o_xqt0 = 0, o_xc0 = 0, o_r = 0, o_d = 0, o_lp2 = 0, o_piop = 0;
+  size_t o_outpi = 0, o_outq[2] = {0, 0}, o_outqt[2] = {0, 0}, o_outc[2] = {0, 0}, o_da[2] = {0, 0};
+  size_t o_P[5][SAC_DEV_LAYERS] = {};      // phase A pre-activations (pi on [s'; s], Q1, Q2, Q1t, Q2t)
+  size_t o_Pc[2][SAC_DEV_LAYERS] = {};     // phase C critics
+  size_t o_DYq[2][SAC_DEV_LAYERS] = {}, o_DYc[2][SAC_DEV_LAYERS] = {}, o_DYpi[SAC_DEV_LAYERS] = {};
+};
+#define WIDE_MAX_JOBS 64
+
 struct sac_engine {
   sac_engine_config cfg;
   sac_engine_buffers buf;
@@ -318,6 +331,19 @@ struct sac_engine {
   int ncu = 256;  // compute units of the device (the persistent grid's bound)
   int G = 0;
   std::vector<PTask> hostP;
+  // large-batch stage path (sac_wide.h): layout offsets, stages, jobs
+  WideLay wl;
+  int wide = 0;
+  WideDev wdh;
+  WideDev* wdd = nullptr;
+  WJob* wjobs = nullptr;
+  std::vector<WJob> hostW;
+  struct WStage {
+    int kind;   // 0 gather, 1 GEMM jobs [j0, j1), 2 pi heads, 3 phase B, 4 phase D
+    int j0, j1, grid, phase, last;
+    size_t lds;
+  };
+  std::vector<WStage> wst;
   // graph cache
   hipGraphExec_t gexec = nullptr;
   hipGraph_t graph = nullptr;
@@ -327,6 +353,7 @@ struct sac_engine {
 };
 
 static inline int rup(int x, int m) { return (x + m - 1) / m * m; }
+
 
 struct Layout {
   size_t off = 0;
@@ -363,6 +390,234 @@ static int validate(const sac_engine_config* c) {
 static void xcd_order(std::vector<TileDesc>& tiles);
 static void plan_persist(sac_engine* e, int esz);
 static bool xcd_order_parts(std::vector<TileDesc>& tiles, int P);
+
+
+// The large-batch path's device descriptor, jobs and stage list (sac_wide.h):
+// per step  gather | A forward stages | pi heads | Qt forward stages | critic
+// backward stages | B | C critic forward | critic dX | pi backward | D.
+static void build_wide(sac_engine* e, char* base) {
+  const WideLay& wl = e->wl;
+  const EngineDev& h = e->h;
+  const int esz = e->cfg.precision == SAC_PREC_BF16 ? 2 : 4;
+  auto F = [&](size_t o) { return (float*)(base + o); };
+  WideDev& W = e->wdh;
+  memset(&W, 0, sizeof(W));
+  const int B = h.B, A = h.A, O = h.O, Brw = wl.Brw, hp = wl.hp, hq = wl.hq;
+  const NetDev& np = h.net[NET_PI];
+  const NetDev& nq1 = h.net[NET_Q1];
+  W.B = B;
+  W.Bp = h.Bp;
+  W.Brw = Brw;
+  W.nrt = h.nrt;
+  W.O = O;
+  W.A = A;
+  W.ldpi0 = np.l[0].Kp;
+  W.ldq0 = nq1.l[0].Kp;
+  W.Xpi0 = F(wl.o_xpi0);
+  W.Xq0 = F(wl.o_xq0);
+  W.Xqt0 = F(wl.o_xqt0);
+  W.Xc0 = F(wl.o_xc0);
+  W.R = F(wl.o_r);
+  W.Dn = F(wl.o_d);
+  W.LP2 = F(wl.o_lp2);
+  W.PIOP = F(wl.o_piop);
+  W.ncb_pi = (np.l[hp - 1].Np + 63) / 64;
+  W.ncb_q = (nq1.l[hq - 1].Np + 63) / 64;
+  W.ncb_da = (nq1.l[0].Np + 63) / 64;
+  W.cbs_pi = (long)2 * Brw * 2 * A;
+  W.cbs_q = Brw;
+  W.cbs_da = (long)Brw * A;
+  W.OUTPpi = F(wl.o_outpi);
+  for (int qi = 0; qi < 2; ++qi) {
+    W.OUTPq[qi] = F(wl.o_outq[qi]);
+    W.OUTPqt[qi] = F(wl.o_outqt[qi]);
+    W.OUTPc[qi] = F(wl.o_outc[qi]);
+    W.DA[qi] = F(wl.o_da[qi]);
+    W.GTq_out[qi] = h.net[NET_Q1 + qi].l[hq].GT;
+    W.dbpq_out[qi] = h.net[NET_Q1 + qi].l[hq].dbp;
+  }
+  W.GTpi_out = np.l[hp].GT;
+  W.dbppi_out = np.l[hp].dbp;
+  e->wdd = (WideDev*)(base + wl.o_dev);
+  e->wjobs = (WJob*)(base + wl.o_jobs);
+  std::vector<WJob>& JB = e->hostW;
+  JB.clear();
+  e->wst.clear();
+  const int KC = esz == 4 ? MM<float>::KC : MM<bf16>::KC;
+  const size_t lds_base = (size_t)2 * 64 * WLDA + (size_t)2 * 4 * (WKB / KC) * 256;  // floats
+  auto stage_gemm = [&](std::vector<WJob> js, int phase, int last) {
+    int item = 0;
+    size_t lf = lds_base;
+    for (WJob& j : js) {
+      j.item0 = item;
+      item += j.nrb * j.ncb;
+      if (j.amode == WA_OUTBWD) lf = std::max(lf, lds_base + 64 * WLDD + (size_t)j.J * j.Kp);
+    }
+    sac_engine::WStage st{1, (int)JB.size(), (int)(JB.size() + js.size()), item, phase, last, lf * 4};
+    e->wst.push_back(st);
+    JB.insert(JB.end(), js.begin(), js.end());
+  };
+  auto fwd = [&](int ni, int l, int M, const float* X, float* Pd, void* XT, int xt_row0, long xt_par, float* OUTP) {
+    const NetDev& nd = h.net[ni];
+    const LayerDev& ly = nd.l[l];
+    WJob j;
+    memset(&j, 0, sizeof(j));
+    j.M = M;
+    j.K = ly.K;
+    j.Kp = ly.Kp;
+    j.N = ly.N;
+    j.Np = ly.Np;
+    j.nrb = M / 64;
+    j.ncb = (ly.Np + 63) / 64;
+    j.amode = l == 0 ? WA_PLAIN : WA_ACT;
+    j.aact = nd.hid_act;
+    j.X = X;
+    j.ldx = ly.Kp;
+    j.Wp = ly.Wc;
+    j.tcols = ly.Kp;
+    j.bias = nd.P + ly.b_off;
+    j.emode = WE_FWD;
+    j.P = Pd;
+    j.ldp = ly.Np;
+    j.oact = nd.hid_act;
+    j.XT = XT;
+    j.xt_row0 = xt_row0;
+    j.xt_ld = h.Bp;
+    j.xt_par = xt_par;
+    if (OUTP) {
+      const LayerDev& lo = nd.l[nd.L - 1];
+      j.Wout = nd.P + lo.w_off;
+      j.ldwout = lo.K;
+      j.Nout = lo.N;
+      j.OUTP = OUTP;
+      j.outp_cb = (long)M * lo.N;
+    }
+    j.pact = -1;
+    return j;
+  };
+  // backward GEMM through layer d: dX_d = dY_d W_d -> dY_{d-1} = act'(P_{d-1}) dX_d
+  auto bwd = [&](int ni, int d, int M, const float* X, bool first, int rowpro, int qi, const float* Pprev, float* DY,
+                 void* GT, float* dbp, float* DA) {
+    const NetDev& nd = h.net[ni];
+    const LayerDev& ly = nd.l[d];
+    const LayerDev& lb = nd.l[d - 1];
+    const LayerDev& lo = nd.l[nd.L - 1];
+    WJob j;
+    memset(&j, 0, sizeof(j));
+    j.M = M;
+    j.K = ly.N;
+    j.Kp = ly.Np;
+    j.N = ly.K;
+    j.Np = ly.Kp;
+    j.nrb = M / 64;
+    j.ncb = (ly.Kp + 63) / 64;
+    j.amode = first ? WA_OUTBWD : WA_PLAIN;
+    j.aact = nd.hid_act;
+    j.X = X;
+    j.ldx = ly.Np;
+    if (first) {
+      j.Wo = nd.P + lo.w_off;
+      j.ldwo = lo.K;
+      j.J = lo.N;
+      j.rowpro = rowpro;
+      j.qi = qi;
+      if (GT) {  // phase A / pi: the generated dY of layer d is a dW operand too
+        j.AGT = ly.GT;
+        j.Adbp = ly.dbp;
+        j.adbp_ld = ly.N;
+      }
+    }
+    j.Wp = ly.WTc;
+    j.tcols = ly.Np;
+    j.emode = WE_BWD;
+    j.Pprev = Pprev;
+    j.ldpp = lb.Np;
+    j.pact = nd.hid_act;
+    j.DY = DY;
+    j.lddy = lb.Np;
+    j.GT = GT;
+    j.gt_ld = h.Bp;
+    j.dbp = dbp;
+    j.dbp_ld = lb.N;
+    if (DA) {
+      const LayerDev& l0 = nd.l[0];
+      j.W0a = nd.P + l0.w_off;
+      j.ldw0 = l0.K;
+      j.a_off = O;
+      j.DA = DA;
+      j.da_cb = (long)Brw * A;
+    }
+    return j;
+  };
+  auto add = [&](int kind, int grid, int phase) {
+    sac_engine::WStage st{kind, 0, 0, grid, phase, 0, 0};
+    e->wst.push_back(st);
+  };
+  // ---- phase A
+  add(0, Brw / 64, 0);  // gather
+  for (int d = 0; d < std::max(hp, hq); ++d) {
+    std::vector<WJob> js;
+    if (d < hp)
+      js.push_back(fwd(NET_PI, d, 2 * Brw, d ? F(wl.o_P[0][d - 1]) : W.Xpi0, F(wl.o_P[0][d]), np.l[d + 1].XT, Brw,
+                       np.l[d + 1].xt_par, d == hp - 1 ? W.OUTPpi : nullptr));
+    for (int qi = 0; qi < 2; ++qi)
+      if (d < hq)
+        js.push_back(fwd(NET_Q1 + qi, d, Brw, d ? F(wl.o_P[1 + qi][d - 1]) : W.Xq0, F(wl.o_P[1 + qi][d]),
+                         h.net[NET_Q1 + qi].l[d + 1].XT, 0, 0, d == hq - 1 ? W.OUTPq[qi] : nullptr));
+    stage_gemm(js, 0, 0);
+  }
+  {
+    const int AP = A <= 1 ? 1 : 1 << (32 - __builtin_clz(A - 1));
+    const int rpb = WG_T / AP;
+    add(2, (2 * Brw + rpb - 1) / rpb, 0);  // pi heads
+  }
+  for (int d = 0; d < hq; ++d) {
+    std::vector<WJob> js;
+    for (int qi = 0; qi < 2; ++qi)
+      js.push_back(fwd(NET_Q1T + qi, d, Brw, d ? F(wl.o_P[3 + qi][d - 1]) : W.Xqt0, F(wl.o_P[3 + qi][d]), nullptr, 0, 0,
+                       d == hq - 1 ? W.OUTPqt[qi] : nullptr));
+    stage_gemm(js, 0, 0);
+  }
+  for (int d = hq - 1; d >= 1; --d) {
+    std::vector<WJob> js;
+    for (int qi = 0; qi < 2; ++qi) {
+      const NetDev& nq = h.net[NET_Q1 + qi];
+      const bool first = d == hq - 1;
+      js.push_back(bwd(NET_Q1 + qi, d, Brw, first ? F(wl.o_P[1 + qi][d]) : F(wl.o_DYq[qi][d]), first, WR_YSEED, qi,
+                       F(wl.o_P[1 + qi][d - 1]), d - 1 >= 1 ? F(wl.o_DYq[qi][d - 1]) : nullptr, nq.l[d - 1].GT,
+                       nq.l[d - 1].dbp, nullptr));
+    }
+    stage_gemm(js, 0, 0);
+  }
+  add(3, 0, 1);  // phase B
+  // ---- phase C
+  for (int d = 0; d < hq; ++d) {
+    std::vector<WJob> js;
+    for (int qi = 0; qi < 2; ++qi)
+      js.push_back(fwd(NET_Q1 + qi, d, Brw, d ? F(wl.o_Pc[qi][d - 1]) : W.Xc0, F(wl.o_Pc[qi][d]), nullptr, 0, 0,
+                       d == hq - 1 ? W.OUTPc[qi] : nullptr));
+    stage_gemm(js, 2, 0);
+  }
+  for (int d = hq - 1; d >= 1; --d) {
+    std::vector<WJob> js;
+    for (int qi = 0; qi < 2; ++qi) {
+      const bool first = d == hq - 1;
+      js.push_back(bwd(NET_Q1 + qi, d, Brw, first ? F(wl.o_Pc[qi][d]) : F(wl.o_DYc[qi][d]), first, WR_MINQ, qi,
+                       F(wl.o_Pc[qi][d - 1]), d - 1 >= 1 ? F(wl.o_DYc[qi][d - 1]) : nullptr, nullptr, nullptr,
+                       d == 1 ? W.DA[qi] : nullptr));
+    }
+    stage_gemm(js, 2, 0);
+  }
+  for (int d = hp - 1; d >= 1; --d) {
+    const bool first = d == hp - 1;
+    std::vector<WJob> js;
+    js.push_back(bwd(NET_PI, d, Brw, first ? F(wl.o_P[0][d]) + (size_t)Brw * np.l[d].Np : F(wl.o_DYpi[d]), first,
+                     WR_PIHEAD, 0, F(wl.o_P[0][d - 1]) + (size_t)Brw * np.l[d - 1].Np,
+                     d - 1 >= 1 ? F(wl.o_DYpi[d - 1]) : nullptr, np.l[d - 1].GT, np.l[d - 1].dbp, nullptr));
+    stage_gemm(js, 2, d == 1);
+  }
+  add(4, 0, 3);  // phase D
+}
 
 static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
   const int esz = c->precision == SAC_PREC_BF16 ? 2 : 4;
@@ -500,6 +755,58 @@ static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
       (ni == NET_PI ? nD : nB) += t * parts;
       nhalf += t * (parts - 1);  // producer parts: one granule slot each
     }
+  // Large-batch stage path (sac_wide.h): where the per-network
+  // role kernels do not fit (6 nrt > 256 co-resident workgroups) and both nets
+  // have at least two hidden layers.  SAC_WIDE=0 keeps the row-tile kernels.
+  WideLay wl;
+  {
+    int roles_pre = 6 * nrt0 <= 256 && SAC_ROWS * (A + 1) <= SAC_HAND_STRIDE;
+    if (const char* v = getenv("SAC_ROLES")) roles_pre = roles_pre && atoi(v) != 0;
+    int on = !split && !roles_pre && c->q_layers >= 3 && c->pi_layers >= 3 && 2 * A <= WJMAX;
+    if (const char* v = getenv("SAC_WIDE")) on = on && atoi(v) != 0;
+    wl.on = on;
+  }
+  if (wl.on) {
+    const int Brw = rup(B, 64);
+    const NetDev& np = h.net[NET_PI];
+    const NetDev& nq = h.net[NET_Q1];
+    const int hp = c->pi_layers - 1, hq = c->q_layers - 1;
+    wl.Brw = Brw;
+    wl.hp = hp;
+    wl.hq = hq;
+    wl.o_dev = lay.take(sizeof(WideDev));
+    wl.o_jobs = lay.take(WIDE_MAX_JOBS * sizeof(WJob));
+    wl.o_xpi0 = lay.take((size_t)2 * Brw * np.l[0].Kp * 4);
+    wl.o_xq0 = lay.take((size_t)Brw * nq.l[0].Kp * 4);
+    wl.o_xqt0 = lay.take((size_t)Brw * nq.l[0].Kp * 4);
+    wl.o_xc0 = lay.take((size_t)Brw * nq.l[0].Kp * 4);
+    wl.o_r = lay.take((size_t)Brw * 4);
+    wl.o_d = lay.take((size_t)Brw * 4);
+    wl.o_lp2 = lay.take((size_t)Brw * 4);
+    wl.o_piop = lay.take((size_t)Brw * 2 * A * 4);
+    const int ncb_pi = (np.l[hp - 1].Np + 63) / 64, ncb_q = (nq.l[hq - 1].Np + 63) / 64, ncb_da = (nq.l[0].Np + 63) / 64;
+    wl.o_outpi = lay.take((size_t)ncb_pi * 2 * Brw * 2 * A * 4);
+    for (int qi = 0; qi < 2; ++qi) {
+      wl.o_outq[qi] = lay.take((size_t)ncb_q * Brw * 4);
+      wl.o_outqt[qi] = lay.take((size_t)ncb_q * Brw * 4);
+      wl.o_outc[qi] = lay.take((size_t)ncb_q * Brw * 4);
+      wl.o_da[qi] = lay.take((size_t)ncb_da * Brw * A * 4);
+    }
+    for (int l = 0; l < hp; ++l) wl.o_P[0][l] = lay.take((size_t)2 * Brw * np.l[l].Np * 4);
+    for (int l = 1; l + 1 < hp; ++l) wl.o_DYpi[l] = lay.take((size_t)Brw * np.l[l].Np * 4);
+    for (int qi = 0; qi < 2; ++qi) {
+      for (int l = 0; l < hq; ++l) {
+        const size_t bytes = (size_t)Brw * nq.l[l].Np * 4;
+        wl.o_P[1 + qi][l] = lay.take(bytes);
+        wl.o_P[3 + qi][l] = lay.take(bytes);
+        wl.o_Pc[qi][l] = lay.take(bytes);
+      }
+      for (int l = 1; l + 1 < hq; ++l) {
+        wl.o_DYq[qi][l] = lay.take((size_t)Brw * nq.l[l].Np * 4);
+        wl.o_DYc[qi][l] = lay.take((size_t)Brw * nq.l[l].Np * 4);
+      }
+    }
+  }
   // persistent step: readiness counters (+ the exit word) and the task table
   const size_t o_pctr = lay.take((size_t)(PC_COUNT * PC_SHARDS * PC_STRIDE + PC_STRIDE) * 4);
   const size_t o_ptask = lay.take((size_t)1024 * sizeof(PTask));
@@ -752,6 +1059,9 @@ static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
       e->fused = fuse;
     }
     plan_persist(e, esz);
+    e->wl = wl;
+    e->wide = wl.on;
+    if (wl.on) build_wide(e, base);
   }
   return total + 256;
 }
@@ -918,6 +1228,7 @@ static void set_lds_attrs(size_t bytes) {
   (void)hipFuncSetAttribute((const void*)sac_critic_update<T>, hipFuncAttributeMaxDynamicSharedMemorySize, b);
   (void)hipFuncSetAttribute((const void*)sac_actor_update<T>, hipFuncAttributeMaxDynamicSharedMemorySize, b);
   (void)hipFuncSetAttribute((const void*)sac_persist<T>, hipFuncAttributeMaxDynamicSharedMemorySize, b);
+  (void)hipFuncSetAttribute((const void*)sac_wide_stage<T>, hipFuncAttributeMaxDynamicSharedMemorySize, b);
 }
 
 // empty kernel: the dispatch + event gap of sac_engine_time_phases
@@ -973,6 +1284,36 @@ static void launch_kind(sac_engine* e, int kind, const sac_replay* rb, const int
   }
 }
 
+// One launch of the large-batch stage path (sac_wide.h).
+template <typename T>
+static void launch_wide_stage(sac_engine* e, const sac_engine::WStage& st, const sac_replay* rb, const int32_t* idx,
+                              const float* eps, hipStream_t s) {
+  switch (st.kind) {
+    case 0:
+      sac_wide_gather<T><<<st.grid, WG_T, 0, s>>>(e->d, e->wdd, *rb, idx);
+      break;
+    case 1:
+      sac_wide_stage<T><<<st.grid, WG_T, st.lds, s>>>(e->d, e->wdd, e->wjobs + st.j0, st.j1 - st.j0, st.last);
+      break;
+    case 2:
+      sac_wide_head<T><<<st.grid, WG_T, 0, s>>>(e->d, e->wdd, eps);
+      break;
+    case 3:
+      launch_kind<T>(e, L_B, rb, idx, eps, s);
+      break;
+    case 4:
+      launch_kind<T>(e, L_D, rb, idx, eps, s);
+      break;
+  }
+}
+static void launch_wide(sac_engine* e, const sac_engine::WStage& st, const sac_replay* rb, const int32_t* idx,
+                        const float* eps, hipStream_t s) {
+  if (e->cfg.precision == SAC_PREC_BF16)
+    launch_wide_stage<bf16>(e, st, rb, idx, eps, s);
+  else
+    launch_wide_stage<float>(e, st, rb, idx, eps, s);
+}
+
 // Fused-step launches of n consecutive steps (one step per launch, sac_persist.h).
 static void launch_persist(sac_engine* e, const sac_replay* rb, int n, const int32_t* indices, const float* eps,
                            hipStream_t s) {
@@ -1013,6 +1354,23 @@ static void launch_steps(sac_engine* e, const sac_replay* rb, int n, const int32
       ev->push_back(x);
     }
   };
+  if (e->wide) {  // the stage sequence of sac_wide.h per step
+    for (int i = 0; i < n; ++i) {
+      const int32_t* ix = indices ? indices + (size_t)i * B : nullptr;
+      const float* ep = eps ? eps + (size_t)i * 2 * B * A : nullptr;
+      for (const sac_engine::WStage& st : e->wst) {
+        launch_wide(e, st, rb, ix, ep, s);
+        if (kinds) kinds->push_back(st.phase);
+        if (ev) {
+          hipEvent_t x;
+          (void)hipEventCreate(&x);
+          (void)hipEventRecord(x, s);
+          ev->push_back(x);
+        }
+      }
+    }
+    return;
+  }
   if (!e->fused) {
     for (int i = 0; i < n; ++i)
       for (int k = L_A; k <= L_D; ++k) go(k, i);
@@ -1108,17 +1466,45 @@ int sac_engine_create(const sac_engine_config* cfg, const sac_engine_buffers* bu
     delete e;
     return fail(SAC_E_INVALID, "layer widths need " + std::to_string(lb) + " B of LDS per workgroup (max 163840)");
   }
+  if (e->wide) {
+    size_t mx = 0;
+    for (const sac_engine::WStage& st : e->wst) mx = std::max(mx, st.lds);
+    if (e->hostW.size() > WIDE_MAX_JOBS || mx > 160 * 1024) {
+      const std::string m = "internal: stage path plans " + std::to_string(e->hostW.size()) + " jobs, " +
+                            std::to_string(mx) + " B of LDS";
+      delete e;
+      return fail(SAC_E_INVALID, m);
+    }
+  }
   if ((int)e->hostB.size() != e->nB || (int)e->hostD.size() != e->nD) {  // the grids launch nB / nD tiles
     const std::string m = "internal: update tiles planned " + std::to_string(e->nB) + " / " + std::to_string(e->nD) +
                           ", built " + std::to_string(e->hostB.size()) + " / " + std::to_string(e->hostD.size());
     delete e;
     return fail(SAC_E_INVALID, m);
   }
+  if (cfg->precision == SAC_PREC_BF16)
+    set_lds_attrs<bf16>(e->lds_bytes);
+  else
+    set_lds_attrs<float>(e->lds_bytes);
+  if (e->persist) {
+    // the fused step's G workgroups spin on each other's counters: every one of
+    // them must be resident at once (one per CU at its VGPR count and LDS size)
+    int nb = 0;
+    const size_t lds = (size_t)e->h.o_pflag * 4 + 16;
+    const hipError_t oe =
+        cfg->precision == SAC_PREC_BF16
+            ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, sac_persist<bf16>, SAC_THREADS, lds)
+            : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, sac_persist<float>, SAC_THREADS, lds);
+    if (oe != hipSuccess || nb < 1 || e->G > nb * e->ncu) e->persist = 0;
+  }
   hipStream_t s = (hipStream_t)stream;
   hipError_t err = hipMemsetAsync(buf->workspace, 0, buf->workspace_bytes, s);
   if (err == hipSuccess) err = hipMemcpyAsync(e->d, &e->h, sizeof(EngineDev), hipMemcpyHostToDevice, s);
   if (err == hipSuccess) err = hipMemcpyAsync(e->tilesB, e->hostB.data(), e->hostB.size() * sizeof(TileDesc), hipMemcpyHostToDevice, s);
   if (err == hipSuccess) err = hipMemcpyAsync(e->tilesD, e->hostD.data(), e->hostD.size() * sizeof(TileDesc), hipMemcpyHostToDevice, s);
+  if (err == hipSuccess && e->wide) err = hipMemcpyAsync(e->wdd, &e->wdh, sizeof(WideDev), hipMemcpyHostToDevice, s);
+  if (err == hipSuccess && e->wide)
+    err = hipMemcpyAsync(e->wjobs, e->hostW.data(), e->hostW.size() * sizeof(WJob), hipMemcpyHostToDevice, s);
   if (err == hipSuccess && e->persist)
     err = hipMemcpyAsync((void*)e->h.ptasks, e->hostP.data(), e->hostP.size() * sizeof(PTask), hipMemcpyHostToDevice, s);
   if (err == hipSuccess) err = hipStreamSynchronize(s);
@@ -1126,10 +1512,6 @@ int sac_engine_create(const sac_engine_config* cfg, const sac_engine_buffers* bu
     delete e;
     return fail(SAC_E_HIP, std::string("engine upload: ") + hipGetErrorString(err));
   }
-  if (cfg->precision == SAC_PREC_BF16)
-    set_lds_attrs<bf16>(e->lds_bytes);
-  else
-    set_lds_attrs<float>(e->lds_bytes);
   rc = sac_engine_sync_params(e, stream);
   if (rc) {
     delete e;
@@ -1359,10 +1741,18 @@ int sac_engine_uses_split(const sac_engine* e) { return e && e->h.split ? 1 : 0;
 
 int sac_engine_uses_fused_step(const sac_engine* e) { return e && e->persist ? e->G : 0; }
 
+int sac_engine_uses_wide(const sac_engine* e) { return e && e->wide ? (int)e->wst.size() : 0; }
+
 int sac_engine_phase_layout(const sac_engine* e) { return e ? e->fused : 0; }
 
 int sac_engine_debug_launch(sac_engine* e, const sac_replay* rb, int32_t kind, void* stream) {
   if (!e || !rb || kind < L_A || kind > L_BC) return fail(SAC_E_INVALID, "bad debug_launch arguments");
+  if (e->wide) {  // every launch of that phase
+    for (const sac_engine::WStage& st : e->wst)
+      if (st.phase == kind) launch_wide(e, st, rb, nullptr, nullptr, (hipStream_t)stream);
+    HIPCHK(hipGetLastError());
+    return SAC_OK;
+  }
   if (e->cfg.precision == SAC_PREC_BF16)
     launch_kind<bf16>(e, kind, rb, nullptr, nullptr, (hipStream_t)stream);
   else
@@ -1406,7 +1796,8 @@ int sac_engine_time_phases(sac_engine* e, const sac_replay* rb, int32_t n_steps,
     sum[kinds[i]] += ms;
     ++cnt[kinds[i]];
   }
-  auto avg = [&](int k) { return cnt[k] ? (float)(sum[k] / cnt[k]) : 0.f; };
+  // per phase and step (the stage path has several launches per phase)
+  auto avg = [&](int k) { return cnt[k] ? (float)(sum[k] / (e->wide ? n_steps : cnt[k])) : 0.f; };
   if (e->fused) {
     ms_host[0] = cnt[L_DA] ? avg(L_DA) : avg(L_A);
     ms_host[1] = e->fused == 2 ? 0.f : avg(L_B);

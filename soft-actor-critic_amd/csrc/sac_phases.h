@@ -7,9 +7,6 @@
 #include "sac_device.h"
 
 #define SAC_DEV_LAYERS 6  // Linear layers per network supported by the kernels
-#ifndef SAC_FIX2
-#define SAC_FIX2 0  // gemm_step: 2-chunk steps (fp32 K = 32) on the fixed one-pair path (A/B: libsac_engine_fix2.so)
-#endif
 
 // Coherent (sc1) 16-B accesses: what a workgroup of the SAME launch on any XCD
 // reads after a counter / flag hand-off (MI355X_MICROARCH.md §visibility: every
@@ -531,12 +528,6 @@ __device__ __forceinline__ void gemm_step(const lf* __restrict__ A, int lda, con
     }
     if (nch == 1) {
       gemm_pair_fixed<T, RT, 1, COH, HC>(arow, lda, w, lane, wave, c, epi, held);
-      return;
-    }
-    // fp32 K = 32 (a critic's or pi's layer 0 on a narrow input): the generic
-    // batch of 8 would issue 16 clamped loads for the 4 fragments it needs
-    if (SAC_FIX2 && nch == 2 && (HC == 0 || !held || held->tag != w.p)) {
-      gemm_pair_fixed<T, RT, 2, COH, 0>(arow, lda, w, lane, wave, c, epi, nullptr);
       return;
     }
   }

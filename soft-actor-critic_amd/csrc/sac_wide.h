@@ -1,0 +1,687 @@
+// sac_wide.h — large-batch phases A and C as layer-synchronous GEMM stages.
+// Included by sac_engine.hip only (after sac_phases.h).  Design: DESIGN.md §3.6.
+//
+// At large batches (C3: B = 4096, reference notebooks/configs/bipedal_walker.yaml
+// with train.batch_size 4096) the step is MFMA work, not a hand-off chain, and
+// the per-row-tile kernels are per-CU weight-stream bound (every workgroup
+// streams all five networks' weights for 16 rows).  Here each dense layer of
+// the step (reference sac/agent.py:195-260, models.py:30-92) is one GEMM stage:
+// 64-row x 64-column output tiles over the whole chip, K staged through LDS in
+// 32-deep blocks (double-buffered, one barrier per block), and every
+// elementwise step fused into a stage's prologue or epilogue:
+//   forward      P = X W^T + b  -> pre-activation P (row-major fp32), act(P)^T
+//                into the X^T stash of the update tiles, and for the last
+//                hidden layer the output layer as per-column-block partials
+//                (OUTP[cb][row][j] = sum_{n in cb} Wout[j][n] act(P[row][n]));
+//   backward     dX = dY W -> dY_prev = act'(P_prev) * dX, stored as the dY^T
+//                stash + per-16-row bias partials of the update tiles, and for
+//                the critics' layer 0 the action-column product (d a~ partials);
+//   output layer the first backward stage generates its own A operand from the
+//                last hidden pre-activation: dY[r][n] = act'(P[r][n]) *
+//                sum_j D[r][j] Wout[j][n], with D the row's output-layer seed
+//                (target y + MSE seed, min-Q weights, or the squashed-Gaussian
+//                head backward) computed by the item's row prologue.
+// Stages of one step (two hidden layers; deeper nets add stages):
+//   A: gather | fwd L0 (pi on [s'; s], Q1, Q2) | fwd L1 (+ output partials) |
+//      pi heads | Qt fwd L0 | Qt fwd L1 | critic backward (y, seeds, losses)
+//   B: sac_critic_update (unchanged)
+//   C: critic fwd L0 | fwd L1 | critic dX (min-Q weights, d a~ partials) |
+//      pi backward (head backward) -- the last block advances the step
+//   D: sac_actor_update + alpha (unchanged)
+// The stashes the update tiles read (X^T, dY^T, bias partials per 16-row tile,
+// loss partials, log pi) have exactly the row-tile kernels' layout, so phases B
+// and D are shared.
+#pragma once
+
+#define WG_T 256   // threads per stage workgroup (4 waves)
+#define WBM 64     // rows per output tile
+#define WBN 64     // columns per output tile
+#define WKB 32     // K per LDS block (fp32: two MFMA chunks of 16; bf16: one of 32)
+#define WLDA 36    // LDS row stride of the A block (floats): conflict-free 16-B fragment reads
+#define WLDE 68    // LDS row stride of the epilogue tile
+#define WLDD 17    // LDS row stride of the per-row seeds (J <= 16)
+#define WJMAX 16
+
+enum WAMode { WA_PLAIN = 0, WA_ACT = 1, WA_OUTBWD = 2 };
+enum WEMode { WE_FWD = 0, WE_BWD = 1 };
+enum WRowPro { WR_NONE = 0, WR_YSEED = 1, WR_MINQ = 2, WR_PIHEAD = 3 };
+
+// Buffers of the wide path that the row prologues, the gather and the head
+// kernel need (the GEMM stages get everything else from their job).
+struct WideDev {
+  int B, Bp, Brw, nrt, O, A;
+  int ldpi0, ldq0;   // row strides of the layer-0 inputs (Kp of pi / Q layer 0)
+  float* Xpi0;       // [2 Brw][ldpi0]: s' rows [0, B), s rows [Brw, Brw + B)
+  float* Xq0;        // [Brw][ldq0]: (s, a) of the critics
+  float* Xqt0;       // [Brw][ldq0]: (s', a~') of the target critics (a~' from the head kernel)
+  float* Xc0;        // [Brw][ldq0]: (s, a~) of phase C's critics
+  float* R;          // [Brw] rewards
+  float* Dn;         // [Brw] dones
+  float* LP2;        // [Brw] log pi(a~'|s')
+  float* PIOP;       // [Brw][2A] pi output pre-activation of the actor rows (pi out_act != identity)
+  int ncb_pi, ncb_q;   // column blocks of pi's / Q's last hidden layer
+  long cbs_pi, cbs_q;  // floats between column blocks of the partial outputs
+  float* OUTPpi;       // [ncb_pi][2 Brw][2A]
+  float* OUTPq[2];     // [ncb_q][Brw][1]: critics, phase A
+  float* OUTPqt[2];    // target critics
+  float* OUTPc[2];     // critics on (s, a~), phase C
+  int ncb_da;          // column blocks of the critics' layer 0 outputs
+  long cbs_da;
+  float* DA[2];        // [ncb_da][Brw][A]: phase C critics' seeded d a~ partials
+  // output layers' dY^T / bias partials written by the row prologues
+  void* GTq_out[2];
+  float* dbpq_out[2];
+  void* GTpi_out;
+  float* dbppi_out;
+};
+
+// One GEMM of a stage: output tiles (row block rb, column block cb), items
+// [item0, item0 + nrb * ncb) of the stage's grid.
+struct WJob {
+  int M, K, Kp, N, Np;  // rows (multiple of 64); reduction (valid, padded to 32); outputs (valid, padded)
+  int nrb, ncb, item0;
+  // A operand: X [M][ldx] fp32 (WA_ACT: act(X); WA_OUTBWD: X = P of the layer, see header)
+  int amode, aact;
+  const float* X;
+  int ldx;
+  const float* Wo;  // WA_OUTBWD: output layer weights [J][ldwo] (fp32 master)
+  int ldwo, J;
+  int rowpro, qi;   // row prologue (WA_OUTBWD seeds) and its critic index
+  // B operand: fragment-packed matrix (forward: Wc [Np][Kp]; backward: WTc [Kp][Np])
+  const void* Wp;
+  int tcols;
+  const float* bias;  // forward
+  int emode;
+  // forward epilogue
+  float* P;  // [M][ldp] pre-activation (null: not kept)
+  int ldp;
+  int oact;  // activation of the layer (X^T stash, output partials)
+  void* XT;  // act(P)^T (T) of rows >= xt_row0 at column r - xt_row0; row stride xt_ld
+  int xt_row0;
+  long xt_ld;
+  long xt_par;  // elements between the two step-parity copies (pi: phase D of step k reads one)
+  const float* Wout;  // output layer [Nout][ldwout] (fp32 master) for OUTP
+  int ldwout, Nout;
+  float* OUTP;
+  long outp_cb;
+  // backward epilogue
+  const float* Pprev;  // pre-activation of the layer below (act' of the dX); pact < 0: none
+  int ldpp, pact;
+  float* DY;  // [M][lddy] dY of the layer below (for a following backward stage)
+  int lddy;
+  void* GT;   // dY^T (T), row stride gt_ld = Bp
+  long gt_ld;
+  float* dbp;  // [nrt][dbp_ld] per-16-row bias partials
+  int dbp_ld;
+  const float* W0a;  // critics' layer 0 [N0][ldw0]: d a~ partials through the action columns
+  int ldw0, a_off;
+  float* DA;
+  long da_cb;
+  void* AGT;   // WA_OUTBWD: the generated operand's dY^T and bias partials (cb == 0 items)
+  float* Adbp;
+  int adbp_ld, pad_;
+};
+
+__device__ __forceinline__ bool wrow_ok(const AS_C WideDev& W, int r) { return r % W.Brw < W.B; }
+
+// T-typed 4-element store of 4 consecutive batch columns (16 B fp32 / 8 B bf16)
+template <typename T>
+__device__ __forceinline__ void st4(void* base, size_t off, const f32x4& v) {
+  if constexpr (sizeof(T) == 4) {
+    *(AS_G f32x4*)((AS_G float*)base + off) = v;
+  } else {
+    typedef bf16 bf16x4 __attribute__((ext_vector_type(4)));
+    bf16x4 h;
+    h[0] = (bf16)v[0]; h[1] = (bf16)v[1]; h[2] = (bf16)v[2]; h[3] = (bf16)v[3];
+    *(AS_G bf16x4*)((AS_G bf16*)base + off) = h;
+  }
+}
+
+// ---------------------------------------------------------------------------- row prologues
+// D[r][0..J) of the item's rows into Dl (LDS), plus the side outputs of the
+// output layer (cb == 0 items only: losses, y, the output layer's dY^T / bias).
+template <typename T>
+__device__ __forceinline__ void wide_rowpro(const AS_C EngineDev& E, const AS_C WideDev& W, const AS_C WJob& jb,
+                                            int row0, int cb, int par, lf* Dl) {
+  const int tid = threadIdx.x, B = W.B, A = W.A;
+  const float alpha32 = (float)*GPC(double, E.alpha_state + 1);
+  if (jb.rowpro == WR_YSEED) {
+    // target y (agent.py:195-211) and critic qi's MSE seed 2 (q - y) / B (agent.py:221-234)
+    if (tid < 64) {
+      const int lr = row0 + tid;
+      const bool v = lr < B;
+      const int qi = jb.qi;
+      const AS_C NetDev& qt1 = E.net[NET_Q1T];
+      const AS_C NetDev& qt2 = E.net[NET_Q2T];
+      const AS_C NetDev& q = E.net[NET_Q1 + qi];
+      float seed = 0.f, sq = 0.f, y = 0.f;
+      if (v) {
+        float a1 = 0.f, a2 = 0.f, aq = 0.f;
+        for (int c = 0; c < W.ncb_q; ++c) {
+          a1 += GPC(float, W.OUTPqt[0])[c * W.cbs_q + lr];
+          a2 += GPC(float, W.OUTPqt[1])[c * W.cbs_q + lr];
+          aq += GPC(float, W.OUTPq[qi])[c * W.cbs_q + lr];
+        }
+        const float t1 = act_fwd(qt1.out_act, a1 + GPC(float, qt1.l[qt1.L - 1].bias)[0]);
+        const float t2 = act_fwd(qt2.out_act, a2 + GPC(float, qt2.l[qt2.L - 1].bias)[0]);
+        const float qp = aq + GPC(float, q.l[q.L - 1].bias)[0];
+        y = GPC(float, W.R)[lr] + (E.gamma * (1.f - GPC(float, W.Dn)[lr])) * (fmin_nan(t1, t2) - alpha32 * GPC(float, W.LP2)[lr]);
+        const float d = act_fwd(q.out_act, qp) - y;
+        sq = d * d;
+        seed = (2.0f / (float)B) * d;
+        if (q.out_act != ACT_ID) seed = act_bwd(q.out_act, qp, seed);
+      }
+      Dl[tid * WLDD] = seed;
+      if (cb == 0) {
+        if (qi == 0 && v) GP(float, E.stats)[4 + lr] = y;
+        if (lr < W.Bp) {
+          if constexpr (sizeof(T) == 4) GP(float, W.GTq_out[qi])[lr] = seed;
+          else GP(bf16, W.GTq_out[qi])[lr] = (bf16)seed;
+        }
+        float s = seed;
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) {
+          s += __shfl_xor(s, o, 64);
+          sq += __shfl_xor(sq, o, 64);
+        }
+        const int rt = lr >> 4;
+        if ((tid & 15) == 0 && rt < W.nrt) {
+          GP(float, W.dbpq_out[qi])[rt] = s;
+          GP(float, E.lossp)[(par * E.nrt + rt) * 4 + qi] = sq;
+        }
+      }
+    }
+  } else if (jb.rowpro == WR_MINQ) {
+    // min-Q weights of L_pi = mean(alpha log pi - min Q) (agent.py:244-252), ties split
+    if (tid < 64) {
+      const int lr = row0 + tid;
+      const bool v = lr < B;
+      const AS_C NetDev& q1 = E.net[NET_Q1];
+      const AS_C NetDev& q2 = E.net[NET_Q2];
+      float a1 = 0.f, a2 = 0.f;
+      if (v)
+        for (int c = 0; c < W.ncb_q; ++c) {
+          a1 += GPC(float, W.OUTPc[0])[c * W.cbs_q + lr];
+          a2 += GPC(float, W.OUTPc[1])[c * W.cbs_q + lr];
+        }
+      const float p1 = a1 + GPC(float, q1.l[q1.L - 1].bias)[0], p2 = a2 + GPC(float, q2.l[q2.L - 1].bias)[0];
+      const float o1 = act_fwd(q1.out_act, p1), o2 = act_fwd(q2.out_act, p2);
+      const float m = fmin_nan(o1, o2);
+      const float gm = v ? -1.0f / (float)B : 0.f;
+      float g1 = (o1 == o2) ? gm * 0.5f : (o1 > o2 ? 0.f : gm);
+      float g2 = (o1 == o2) ? gm * 0.5f : (o1 < o2 ? 0.f : gm);
+      if (q1.out_act != ACT_ID) g1 = act_bwd(q1.out_act, p1, g1);
+      if (q2.out_act != ACT_ID) g2 = act_bwd(q2.out_act, p2, g2);
+      Dl[tid * WLDD] = jb.qi ? g2 : g1;
+      if (cb == 0 && jb.qi == 0) {
+        float term = v ? alpha32 * GPC(float, E.lp_st)[par * E.Br + lr] - m : 0.f;
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) term += __shfl_xor(term, o, 64);
+        const int rt = lr >> 4;
+        if ((tid & 15) == 0 && rt < W.nrt) GP(float, E.lossp)[(par * E.nrt + rt) * 4 + 2] = term;
+      }
+    }
+  } else if (jb.rowpro == WR_PIHEAD) {
+    // squashed-Gaussian head backward (models.py:79-87 under agent.py:255-257):
+    // d(mu), d(log_std) of each actor row from d a~ (the critics' seeded partials)
+    const AS_C NetDev& pi = E.net[NET_PI];
+    for (int i = tid; i < 64 * A; i += WG_T) {
+      const int r = i / A, j = i % A, lr = row0 + r;
+      const bool v = lr < B;
+      float gm = 0.f, gs = 0.f;
+      if (v) {
+        float d1 = 0.f, d2 = 0.f;
+        for (int c = 0; c < W.ncb_da; ++c) {
+          d1 += GPC(float, W.DA[0])[c * W.cbs_da + (size_t)lr * A + j];
+          d2 += GPC(float, W.DA[1])[c * W.cbs_da + (size_t)lr * A + j];
+        }
+        const float ga = d1 + d2;
+        const float gl = alpha32 * (1.0f / (float)B);
+        const AS_G float* h = GPC(float, E.head_st) + (size_t)lr * 4 * A;
+        const float lo = E.ls_min, hi = E.ls_max, scale = E.scale;
+        const float mu = h[j], lsr = h[A + j], z = h[2 * A + j], e = h[3 * A + j];
+        const float ls = lsr < lo ? lo : (lsr > hi ? hi : lsr);
+        const float sd = expf(ls);
+        const float t = tanhf(z);
+        const float diff = z - mu, var = sd * sd;
+        float g_z = (ga * scale) * (1.f - t * t);
+        g_z = g_z + (-gl) * 2.f * (-1.f + 2.f * softplus20_grad(-2.f * z));
+        const float two_var = 2.f * var;
+        const float g_sq = -gl / two_var;
+        const float g_twovar = gl * (diff * diff) / (two_var * two_var);
+        const float g_var = 2.f * g_twovar;
+        float g_std = 2.f * sd * g_var - gl / sd;
+        const float g_diff = 2.f * diff * g_sq;
+        g_z = g_z + g_diff;
+        const float g_mu = -g_diff + g_z;
+        g_std = g_std + g_z * e;
+        const float g_ls = g_std * sd;
+        const bool in_range = (lsr >= lo) && (lsr <= hi);
+        gm = g_mu;
+        gs = in_range ? g_ls : 0.f;
+        if (pi.out_act != ACT_ID) {
+          gm = act_bwd(pi.out_act, GPC(float, W.PIOP)[(size_t)lr * 2 * A + j], gm);
+          gs = act_bwd(pi.out_act, GPC(float, W.PIOP)[(size_t)lr * 2 * A + A + j], gs);
+        }
+      }
+      Dl[r * WLDD + j] = gm;
+      Dl[r * WLDD + A + j] = gs;
+      if (cb == 0 && lr < W.Bp) {
+        if constexpr (sizeof(T) == 4) {
+          GP(float, W.GTpi_out)[(size_t)j * W.Bp + lr] = gm;
+          GP(float, W.GTpi_out)[(size_t)(A + j) * W.Bp + lr] = gs;
+        } else {
+          GP(bf16, W.GTpi_out)[(size_t)j * W.Bp + lr] = (bf16)gm;
+          GP(bf16, W.GTpi_out)[(size_t)(A + j) * W.Bp + lr] = (bf16)gs;
+        }
+      }
+    }
+    if (cb == 0) {  // bias partials of the output layer: per 16-row tile, column j < 2A
+      __syncthreads();
+      for (int i = tid; i < 4 * 2 * A; i += WG_T) {
+        const int rt = i / (2 * A), j = i % (2 * A);
+        const int grt = row0 / 16 + rt;
+        float s = 0.f;
+        for (int r = 0; r < 16; ++r) s += Dl[(rt * 16 + r) * WLDD + j];
+        if (grt < W.nrt) GP(float, W.dbppi_out)[(size_t)grt * 2 * A + j] = s;
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------- one GEMM item
+template <typename T>
+__device__ __forceinline__ void wide_item(const AS_C EngineDev& E, const AS_C WideDev& W, const AS_C WJob& jb, int it,
+                                          lf* lds, int par) {
+  constexpr int KC = MM<T>::KC, KL = MM<T>::KL, NCH = WKB / KC;
+  typedef typename MM<T>::Frag F;
+  const int tid = threadIdx.x, lane = tid & 63, wave = wave_id();
+  const int c = lane & 15, g = lane >> 4;
+  const int wr = wave >> 1, wc = wave & 1;
+  const int rb = it / jb.ncb, cb = it % jb.ncb;
+  const int row0 = rb * WBM, col0 = cb * WBN;
+  const int NT = jb.Np >> 4, t0 = col0 >> 4, nchT = jb.tcols / KC;
+  const int Kp = jb.Kp, nkb = Kp / WKB;
+  lf* Ab = lds;                       // [2][64][WLDA] fp32 A blocks
+  lf* Bb = lds + 2 * 64 * WLDA;       // [2][4 tiles][NCH][64 lanes x 16 B] packed B fragments
+  constexpr int BBUF = 4 * NCH * 256;  // floats per B buffer
+  lf* Dl = Bb + 2 * BBUF;             // [64][WLDD] row seeds (WA_OUTBWD)
+  lf* Wol = Dl + 64 * WLDD;           // [J][Kp] output layer weights (WA_OUTBWD)
+  const bool outbwd = jb.amode == WA_OUTBWD;
+  const int J = jb.J;
+
+  if (outbwd) {
+    wide_rowpro<T>(E, W, jb, row0, cb, par, Dl);
+    for (int i = tid; i < J * Kp; i += WG_T) {
+      const int j = i / Kp, k = i % Kp;
+      Wol[i] = k < jb.ldwo ? GPC(float, jb.Wo)[(size_t)j * jb.ldwo + k] : 0.f;
+    }
+    __syncthreads();
+  }
+
+  f32x4 ra[2];
+  u32x4 rbv[NCH];
+  auto load = [&](int kb) __attribute__((always_inline)) {
+    const int k0 = kb * WKB;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int p = tid + WG_T * u, row = p >> 3, kq = p & 7;
+      ra[u] = *(const AS_G f32x4*)(GPC(float, jb.X) + (size_t)(row0 + row) * jb.ldx + k0 + 4 * kq);
+    }
+#pragma unroll
+    for (int v = 0; v < NCH; ++v) {
+      const int pb = tid + WG_T * v, ct = pb / (64 * NCH), rest = pb % (64 * NCH), ch = rest >> 6, ln = rest & 63;
+      const int t = t0 + ct;
+      rbv[v] = t < NT ? *(const AS_G u32x4*)(GPC(T, jb.Wp) + ((size_t)(t * nchT + kb * NCH + ch) * 64 + ln) * KL)
+                      : u32x4{0u, 0u, 0u, 0u};
+    }
+  };
+  auto store = [&](int kb, int buf) __attribute__((always_inline)) {
+    const int k0 = kb * WKB;
+    lf* Aq = Ab + buf * 64 * WLDA;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int p = tid + WG_T * u, row = p >> 3, kq = p & 7;
+      f32x4 v = ra[u];
+      if (jb.amode == WA_ACT) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = act_fwd(jb.aact, v[e]);
+      } else if (outbwd) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int k = k0 + 4 * kq + e;
+          float s = 0.f;
+          for (int j = 0; j < J; ++j) s += Dl[row * WLDD + j] * Wol[j * Kp + k];
+          v[e] = act_bwd(jb.aact, v[e], s);
+        }
+      }
+      *(AS_L f32x4*)(Aq + row * WLDA + 4 * kq) = v;
+    }
+    lf* Bq = Bb + buf * BBUF;
+#pragma unroll
+    for (int v = 0; v < NCH; ++v) *(AS_L u32x4*)(Bq + (tid + WG_T * v) * 4) = rbv[v];
+  };
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto comp = [&](int buf) __attribute__((always_inline)) {
+    const lf* Aq = Ab + buf * 64 * WLDA;
+    const lf* Bq = Bb + buf * BBUF;
+#pragma unroll
+    for (int ch = 0; ch < NCH; ++ch) {
+      const F a0 = MM<T>::from_lds(Aq + (wr * 32 + c) * WLDA + ch * KC + g * KL);
+      const F a1 = MM<T>::from_lds(Aq + (wr * 32 + 16 + c) * WLDA + ch * KC + g * KL);
+      const F b0 = *(const AS_L F*)(Bq + ((wc * 2 + 0) * NCH + ch) * 256 + lane * 4);
+      const F b1 = *(const AS_L F*)(Bq + ((wc * 2 + 1) * NCH + ch) * 256 + lane * 4);
+      MM<T>::mma(acc[0][0], a0, b0);
+      MM<T>::mma(acc[0][1], a0, b1);
+      MM<T>::mma(acc[1][0], a1, b0);
+      MM<T>::mma(acc[1][1], a1, b1);
+    }
+  };
+  // the generated operand's dY^T + bias partials (WA_OUTBWD, cb == 0): block kb from LDS
+  const bool agt = outbwd && jb.AGT && cb == 0;
+  auto agt_store = [&](int kb, int buf) __attribute__((always_inline)) {
+    const int k0 = kb * WKB;
+    const lf* Aq = Ab + buf * 64 * WLDA;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int p = tid + WG_T * u, k = p >> 4, q = p & 15;  // column k0 + k, rows 4q..4q+3
+      const int b0 = row0 + 4 * q;
+      if (b0 < W.Bp) {
+        f32x4 v;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = Aq[(4 * q + e) * WLDA + k];
+        st4<T>(jb.AGT, (size_t)(k0 + k) * W.Bp + b0, v);
+      }
+    }
+    if (tid < 4 * WKB) {
+      const int rt = tid / WKB, k = tid % WKB, grt = row0 / 16 + rt;
+      float s = 0.f;
+      for (int r = 0; r < 16; ++r) s += Aq[(rt * 16 + r) * WLDA + k];
+      if (grt < W.nrt && k0 + k < jb.adbp_ld) GP(float, jb.Adbp)[(size_t)grt * jb.adbp_ld + k0 + k] = s;
+    }
+  };
+
+  load(0);
+  store(0, 0);
+  __syncthreads();
+  for (int kb = 0; kb < nkb; ++kb) {
+    const int cur = kb & 1;
+    if (kb + 1 < nkb) load(kb + 1);
+    if (agt) agt_store(kb, cur);
+    comp(cur);
+    if (kb + 1 < nkb) store(kb + 1, cur ^ 1);
+    __syncthreads();
+  }
+
+  // ---- epilogue through an LDS tile [64][WLDE] (aliases the K-loop buffers)
+  lf* Et = lds;
+  const bool fwd = jb.emode == WE_FWD;
+#pragma unroll
+  for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+    for (int ct = 0; ct < 2; ++ct) {
+      const int cl = wc * 32 + ct * 16 + c, n = col0 + cl;
+      const float bn = (fwd && n < jb.N) ? GPC(float, jb.bias)[n] : 0.f;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int r = wr * 32 + rt * 16 + 4 * g + i;
+        const bool ok = n < jb.N && row0 + r < jb.M && wrow_ok(W, row0 + r);
+        Et[r * WLDE + cl] = ok ? acc[rt][ct][i] + bn : 0.f;
+      }
+    }
+  __syncthreads();
+  if (!fwd) {  // dY of the layer below = act'(P_prev) * dX, in place (row pieces)
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int p = tid + WG_T * u, r = p >> 4, q = p & 15, k = col0 + 4 * q;
+      if (k < jb.Np) {
+        f32x4 v = *(AS_L f32x4*)(Et + r * WLDE + 4 * q);
+        if (jb.pact >= 0) {
+          const f32x4 pp = *(const AS_G f32x4*)(GPC(float, jb.Pprev) + (size_t)(row0 + r) * jb.ldpp + k);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = act_bwd(jb.pact, pp[e], v[e]);
+          *(AS_L f32x4*)(Et + r * WLDE + 4 * q) = v;
+        }
+        if (jb.DY) *(AS_G f32x4*)(GP(float, jb.DY) + (size_t)(row0 + r) * jb.lddy + k) = v;
+      }
+    }
+    __syncthreads();
+    // dY^T stash + per-16-row bias partials
+    if (jb.GT) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int p = tid + WG_T * u, k = p >> 4, q = p & 15, b0 = row0 + 4 * q;
+        if (col0 + k < jb.Np && b0 < W.Bp) {
+          f32x4 v;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = Et[(4 * q + e) * WLDE + k];
+          st4<T>(jb.GT, (size_t)(col0 + k) * jb.gt_ld + b0, v);
+        }
+      }
+    }
+    if (jb.dbp) {
+      const int rt = tid >> 6, k = tid & 63, grt = row0 / 16 + rt;
+      float s = 0.f;
+      for (int r = 0; r < 16; ++r) s += Et[(rt * 16 + r) * WLDE + k];
+      if (grt < W.nrt && col0 + k < jb.N) GP(float, jb.dbp)[(size_t)grt * jb.dbp_ld + col0 + k] = s;
+    }
+    if (jb.DA) {  // d a~ partials: sum over this block's hidden units of dY0[r][n] W0[n][O + j]
+      for (int i = tid; i < 64 * W.A; i += WG_T) {
+        const int r = i / W.A, j = i % W.A;
+        float s = 0.f;
+        for (int k = 0; k < WBN && col0 + k < jb.N; ++k)
+          s += Et[r * WLDE + k] * GPC(float, jb.W0a)[(size_t)(col0 + k) * jb.ldw0 + jb.a_off + j];
+        GP(float, jb.DA)[cb * jb.da_cb + (size_t)(row0 + r) * W.A + j] = s;
+      }
+    }
+    return;
+  }
+  // forward: pre-activation rows, act(P)^T stash, output-layer partials
+  if (jb.P) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int p = tid + WG_T * u, r = p >> 4, q = p & 15;
+      if (col0 + 4 * q < jb.Np)
+        *(AS_G f32x4*)(GP(float, jb.P) + (size_t)(row0 + r) * jb.ldp + col0 + 4 * q) = *(AS_L f32x4*)(Et + r * WLDE + 4 * q);
+    }
+  }
+  if (jb.XT && row0 >= jb.xt_row0) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int p = tid + WG_T * u, n = p >> 4, q = p & 15, b0 = row0 - jb.xt_row0 + 4 * q;
+      if (col0 + n < jb.Np && b0 < W.Bp) {
+        f32x4 v;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = act_fwd(jb.oact, Et[(4 * q + e) * WLDE + n]);
+        st4<T>(jb.XT, (size_t)par * jb.xt_par + (size_t)(col0 + n) * jb.xt_ld + b0, v);
+      }
+    }
+  }
+  if (jb.OUTP) {
+    const int No = jb.Nout;
+    for (int i = tid; i < 64 * No; i += WG_T) {
+      const int r = i / No, j = i % No;
+      float s = 0.f;
+      for (int k = 0; k < WBN && col0 + k < jb.N; ++k)
+        s += GPC(float, jb.Wout)[(size_t)j * jb.ldwout + col0 + k] * act_fwd(jb.oact, Et[r * WLDE + k]);
+      GP(float, jb.OUTP)[cb * jb.outp_cb + (size_t)(row0 + r) * No + j] = s;
+    }
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(WG_T) sac_wide_stage(const EngineDev* __restrict__ Ep, const WideDev* __restrict__ Wd,
+                                                       const WJob* __restrict__ jobs, int njobs, int last) {
+  const AS_C EngineDev& E = *(const AS_C EngineDev*)Ep;
+  const AS_C WideDev& W = *(const AS_C WideDev*)Wd;
+  extern __shared__ float lds_raw[];
+  int j = 0;
+  while (j + 1 < njobs && (int)blockIdx.x >= ((const AS_C WJob*)jobs)[j + 1].item0) ++j;
+  const AS_C WJob& jb = ((const AS_C WJob*)jobs)[j];
+  const int par = (int)(*GPC(uint64_t, E.rng_step) & 1);
+  wide_item<T>(E, W, jb, (int)blockIdx.x - jb.item0, (lf*)lds_raw, par);
+  if (last) phase_c_done(E);  // the step's last launch before phase D advances the step
+}
+
+// ---------------------------------------------------------------------------- gather (phase A, first)
+// The step's batch (replay_buffer.py:32-39, agent.py:166-193) into the row-major
+// layer-0 inputs and the layer-0 X^T stashes; block 0 also derives the step's
+// Adam bias corrections (torch adam.py) as phase A of the row-tile path does.
+template <typename T>
+__global__ void __launch_bounds__(WG_T) sac_wide_gather(const EngineDev* __restrict__ Ep, const WideDev* __restrict__ Wd,
+                                                        sac_replay rb, const int32_t* __restrict__ inj_idx_) {
+  const AS_C EngineDev& E = *(const AS_C EngineDev*)Ep;
+  const AS_C WideDev& W = *(const AS_C WideDev*)Wd;
+  __shared__ int64_t slot[64];
+  const int tid = threadIdx.x, O = W.O, A = W.A, B = W.B;
+  const int row0 = blockIdx.x * 64;
+  const uint64_t step = *GPC(uint64_t, E.rng_step);
+  const int par = (int)(step & 1);
+  if (blockIdx.x == 0 && tid < 4 && (tid < 3 || (E.auto_entropy && E.alpha_update))) {
+    const double t = GP(double, E.opt_steps)[tid] + 1.0;
+    GP(double, E.opt_steps)[tid] = t;
+    if (tid < 3) {
+      const double lr = tid == 0 ? E.actor_lr : E.critic_lr;
+      GP(float, E.adam_sc)[par * 6 + tid * 2] = (float)(-(lr / (1.0 - pow((double)E.beta1, t))));
+      GP(float, E.adam_sc)[par * 6 + tid * 2 + 1] = (float)sqrt(1.0 - pow((double)E.beta2, t));
+    } else {
+      GP(double, E.alpha_sc)[par * 2] = 1.0 - pow((double)E.beta1, t);
+      GP(double, E.alpha_sc)[par * 2 + 1] = 1.0 - pow((double)E.beta2, t);
+    }
+  }
+  const int64_t size = GPC(int64_t, rb.state)[0], pos = GPC(int64_t, rb.state)[1];
+  if (tid < 64) {
+    const int b = row0 + tid;
+    int64_t s = -1;
+    if (b < B) {
+      int64_t li;
+      if (inj_idx_) {
+        li = GPC(int32_t, inj_idx_)[b];
+      } else {
+        const Feistel f = feistel_make(E.seed, step, size);
+        li = feistel_sample(f, b, size);
+      }
+      s = size < rb.capacity ? li : (pos + li) % rb.capacity;
+    }
+    slot[tid] = s;
+  }
+  __syncthreads();
+  const RowStrides rs = row_strides(rb.row_stride, O, A);
+  const int Wf = 2 * O + A + 2;
+  for (int i = tid; i < 64 * Wf; i += WG_T) {
+    const int r = i / Wf, f = i % Wf, b = row0 + r;
+    const int64_t sl = slot[r];
+    if (sl < 0) continue;
+    if (f < O) {
+      const float v = GPC(float, rb.obs)[sl * rs.obs + f];
+      GP(float, W.Xpi0)[(size_t)(W.Brw + b) * W.ldpi0 + f] = v;
+      GP(float, W.Xq0)[(size_t)b * W.ldq0 + f] = v;
+      GP(float, W.Xc0)[(size_t)b * W.ldq0 + f] = v;
+    } else if (f < 2 * O) {
+      const float v = GPC(float, rb.next_obs)[sl * rs.obs + (f - O)];
+      GP(float, W.Xpi0)[(size_t)b * W.ldpi0 + (f - O)] = v;
+      GP(float, W.Xqt0)[(size_t)b * W.ldq0 + (f - O)] = v;
+    } else if (f < 2 * O + A) {
+      const float v = GPC(float, rb.act)[sl * rs.act + (f - 2 * O)];
+      GP(float, W.Xq0)[(size_t)b * W.ldq0 + O + (f - 2 * O)] = v;
+    } else if (f == 2 * O + A) {
+      GP(float, W.R)[b] = GPC(float, rb.rew)[sl * rs.one];
+    } else {
+      GP(float, W.Dn)[b] = GPC(float, rb.done)[sl * rs.one];
+    }
+  }
+  __syncthreads();
+  // X^T stashes of layer 0: the critics' (s, a) and the actor rows' s (this step's parity copy)
+  const AS_C LayerDev& q0 = E.net[NET_Q1].l[0];
+  const AS_C LayerDev& p0 = E.net[NET_PI].l[0];
+  T* xq = (T*)q0.XT;
+  T* xp = (T*)p0.XT + par * p0.xt_par;
+  for (int i = tid; i < (O + A) * 64; i += WG_T) {  // k-major: 64 consecutive batch columns per k
+    const int k = i / 64, r = i % 64, b = row0 + r;
+    const int64_t sl = slot[r];
+    if (b >= B || sl < 0) continue;
+    const float v = k < O ? GPC(float, rb.obs)[sl * rs.obs + k] : GPC(float, rb.act)[sl * rs.act + (k - O)];
+    xq[(size_t)k * W.Bp + b] = MM<T>::cvt(v);
+    if (k < O) xp[(size_t)k * W.Bp + b] = MM<T>::cvt(v);
+  }
+}
+
+// ---------------------------------------------------------------------------- pi heads (phase A)
+// Squashed-Gaussian sample (models.py:79-87) of every pi row: target rows
+// (s', draw 0) -> a~' into the target critics' input and log pi' (LP2); actor
+// rows (s, draw 1) -> a~ into phase C's critic input, the head stash, log pi.
+template <typename T>
+__global__ void __launch_bounds__(WG_T) sac_wide_head(const EngineDev* __restrict__ Ep, const WideDev* __restrict__ Wd,
+                                                      const float* __restrict__ inj_eps_) {
+  const AS_C EngineDev& E = *(const AS_C EngineDev*)Ep;
+  const AS_C WideDev& W = *(const AS_C WideDev*)Wd;
+  const AS_C NetDev& pi = E.net[NET_PI];
+  const int tid = threadIdx.x, A = W.A, B = W.B;
+  const uint64_t step = *GPC(uint64_t, E.rng_step);
+  const int par = (int)(step & 1);
+  const int AP = A <= 1 ? 1 : 1 << (32 - __builtin_clz(A - 1));
+  const int rows_per_block = WG_T / AP;
+  const int r = blockIdx.x * rows_per_block + tid / AP, j = tid % AP;  // r in [0, 2 Brw)
+  const int which = r >= W.Brw ? 1 : 0, b = r - which * W.Brw;
+  const bool live = r < 2 * W.Brw && b < B && j < A;
+  float lp = 0.f, corr = 0.f;
+  if (live) {
+    float am = 0.f, as = 0.f;
+    for (int c = 0; c < W.ncb_pi; ++c) {
+      am += GPC(float, W.OUTPpi)[c * W.cbs_pi + (size_t)r * 2 * A + j];
+      as += GPC(float, W.OUTPpi)[c * W.cbs_pi + (size_t)r * 2 * A + A + j];
+    }
+    const AS_G float* bo = GPC(float, pi.l[pi.L - 1].bias);
+    const float pm = am + bo[j], ps = as + bo[A + j];
+    const float mu = act_fwd(pi.out_act, pm), lsr = act_fwd(pi.out_act, ps);
+    float e;
+    if (inj_eps_) {
+      e = GPC(float, inj_eps_)[((size_t)which * B + b) * A + j];
+    } else {
+      float n0, n1;
+      philox_normal2(E.seed, step, (uint32_t)b, (uint32_t)which, (uint32_t)(j >> 1), n0, n1);
+      e = (j & 1) ? n1 : n0;
+    }
+    const float lo = E.ls_min, hi = E.ls_max;
+    const float ls = lsr < lo ? lo : (lsr > hi ? hi : lsr);
+    const float sd = expf(ls);
+    const float z = mu + e * sd;
+    const float act_v = tanhf(z) * E.scale;
+    const float diff = z - mu;
+    const float var = sd * sd;
+    lp = -(diff * diff) / (2.f * var) - logf(sd) - HALF_LOG_2PI;
+    corr = 2.f * ((LOG2F - z) - softplus20(-2.f * z));
+    if (which) {
+      AS_G float* h = GP(float, E.head_st) + (size_t)b * 4 * A;
+      h[j] = mu;
+      h[A + j] = lsr;
+      h[2 * A + j] = z;
+      h[3 * A + j] = e;
+      GP(float, E.a_st)[(size_t)b * A + j] = act_v;
+      GP(float, W.Xc0)[(size_t)b * W.ldq0 + W.O + j] = act_v;
+      if (pi.out_act != ACT_ID) {
+        GP(float, W.PIOP)[(size_t)b * 2 * A + j] = pm;
+        GP(float, W.PIOP)[(size_t)b * 2 * A + A + j] = ps;
+      }
+    } else {
+      GP(float, W.Xqt0)[(size_t)b * W.ldq0 + W.O + j] = act_v;
+    }
+  }
+  for (int o = 1; o < AP; o <<= 1) {
+    lp += __shfl_xor(lp, o, 64);
+    corr += __shfl_xor(corr, o, 64);
+  }
+  if (live && j == 0) {
+    const float v = lp - corr;
+    if (which) {
+      GP(float, E.lp_st)[par * E.Br + b] = v;
+      GP(float, E.stats)[4 + B + b] = v;
+    } else {
+      GP(float, W.LP2)[b] = v;
+    }
+  }
+}

@@ -40,7 +40,7 @@ import time
 import warnings
 from collections import deque
 from copy import deepcopy
-from typing import Any, Dict, Optional
+from typing import Callable, Any, Dict, Optional
 
 import numpy as np
 import torch
@@ -191,6 +191,9 @@ class QValueLog:
         n = host.shape[0]
         if self.fill + n > self.cap:
             self._flush()
+        if n > self.cap:  # one call larger than the ring (num_envs > 2 * every): grow it
+            self.cap = n
+            self.dev = torch.empty(self.cap, 2, dtype=torch.float32, device=a.device)
         x = torch.from_numpy(np.ascontiguousarray(host))
         if a.device.type == "cuda":
             x = x.pin_memory().to(a.device, non_blocking=True)
@@ -595,7 +598,8 @@ class SAC:
 
     def run_vectorized_training_loop(self, total_env_steps: int, vec_env: Any = None, logger=None,
                                      tqdm_disable: bool = True, print_rewards: bool = False,
-                                     seed: Optional[int] = None) -> Dict[str, float]:
+                                     seed: Optional[int] = None,
+                                     callback: Optional[Callable[[Dict[str, float]], None]] = None) -> Dict[str, float]:
         """Batched form of ``run_training_loop`` (agent.py:329-418) over a
         ``SyncVectorEnv`` of N envs.
 
@@ -610,7 +614,13 @@ class SAC:
 
         ``vec_env`` defaults to ``self.env`` (pass a ``SyncVectorEnv`` as the
         agent's env so ``_set_seed`` seeds env i with seed + i).  Stops after the
-        first vector step that reaches ``total_env_steps``."""
+        first vector step that reaches ``total_env_steps``.
+
+        ``callback`` (optional) is called after every vector step with the
+        loop's host counters (``env_steps``, ``gradient_steps``, ``episodes``,
+        ``avg_return`` over the last 100 episodes): the hook of
+        ``sac.replicas.ReplicaAggregator`` (independent-seed replicas, one per
+        GPU, sac/train_replicas.py).  It must not synchronise the device."""
         env = vec_env if vec_env is not None else self.env
         if not hasattr(env, "num_envs"):
             raise TypeError("run_vectorized_training_loop needs a vectorised env (sac.vector_env.SyncVectorEnv)")
@@ -663,6 +673,9 @@ class SAC:
                 ep_ret[i] = 0.0
                 ep_len[i] = 0
             obs = next_obs
+            if callback is not None:
+                callback({"env_steps": total_steps, "gradient_steps": grad_steps, "episodes": total_episodes,
+                          "avg_return": avg_return})
         if self.engine is not None:
             self.engine.check()  # a timed-out hand-off invalidates the run: raise, do not report it
         if loss_log is not None:

@@ -143,6 +143,9 @@ class SacEngine:
         self.lib.sac_engine_uses_roles.argtypes = [ctypes.c_void_p]
         self.roles = bool(self.lib.sac_engine_uses_roles(h))
         self.fused = int(self.lib.sac_engine_phase_layout(h))  # 1: D in the next A's launch, 2: + B in C's
+        # large-batch stage path (csrc/sac_wide.h): launches per step, 0 when the phase kernels run
+        self.lib.sac_engine_uses_wide.argtypes = [ctypes.c_void_p]
+        self.wide = int(self.lib.sac_engine_uses_wide(h))
 
     # ------------------------------------------------------------------ plumbing
     def _stream(self):

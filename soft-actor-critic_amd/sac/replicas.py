@@ -13,15 +13,16 @@ host, only (on the device) for the tens-of-bytes all-reduce.
 """
 from __future__ import annotations
 
+import math
 import time
 from typing import List, Optional, Sequence, Tuple
 
 import torch
 
-# order of the aggregated metric vector of aggregate_metrics
+# order of the replica metric vector, host (aggregate_metrics) and
+# device (metric_vector / replica_train / ReplicaAggregator) forms alike
 METRICS = ("steps", "wall_s", "q1_loss", "q2_loss", "policy_loss", "alpha_loss", "alpha", "mean_return")
-# order of the per-block device vector of replica_train (no host values: no sync)
-REPLICA_METRICS = ("steps", "q1_loss", "q2_loss", "policy_loss", "alpha_loss", "alpha")
+REPLICA_METRICS = METRICS
 
 
 def replica_seed(base_seed: int, rank: int) -> int:
@@ -51,10 +52,15 @@ def aggregate_metrics(values: Sequence[float], group=None, device: Optional[torc
     return {"sum": s.tolist(), "mean": (s / world).tolist(), "max": m.tolist(), "world": world}
 
 
-def metric_vector(engine) -> torch.Tensor:
-    """REPLICA_METRICS of the engine's last step as a float64 device tensor,
-    built by device ops from the engine's own buffers (no host read)."""
-    return torch.cat([engine.rng_step.double(), engine.stats[:4].double(), engine.alpha_state[1:2].double()])
+def metric_vector(engine, wall_s: float = 0.0, mean_return: float = float("nan")) -> torch.Tensor:
+    """METRICS of the engine's last step as a float64 device tensor: the step
+    counter, losses and alpha come from the engine's own buffers by device ops
+    (no host read); the host scalars wall_s and mean_return enter as fill
+    kernels (torch.full: a kernel argument, not a copy), so nothing waits."""
+    dev = engine.stats.device
+    host = lambda x: torch.full((1,), float(x), dtype=torch.float64, device=dev)  # noqa: E731
+    return torch.cat([engine.rng_step.double().reshape(1), host(wall_s), engine.stats[:4].double(),
+                      engine.alpha_state[1:2].double(), host(mean_return)])
 
 
 def aggregate_device(v: torch.Tensor, group=None) -> Tuple[torch.Tensor, torch.Tensor]:
@@ -80,13 +86,51 @@ def replica_train(engine, replay, n_steps: int, chunk: int, every: int = 1024, g
     out = []
     done = 0
     every = max(1, int(every))
+    t0 = time.perf_counter()
     while done < n_steps:
         k = min(every, n_steps - done)
         engine.train_graph(replay, k, chunk)
         done += k
-        if on:
-            out.append(aggregate_device(metric_vector(engine), group))
+        if on:  # wall_s: host time of the enqueues so far; mean_return: no episodes in a bench
+            out.append(aggregate_device(metric_vector(engine, time.perf_counter() - t0), group))
     return out
+
+
+class ReplicaAggregator:
+    """``callback`` of ``SAC.run_vectorized_training_loop`` for replica
+    training (sac/train_replicas.py): every ``every`` gradient steps of this
+    rank's learner (and once more at ``finish``) the replica metric vector
+    METRICS -- the engine's step counter, losses and alpha, this rank's wall
+    time and the mean return of its last 100 episodes -- is all-reduced
+    (sum and max) over the process group, on the device, without a host sync
+    (RCCL orders the collectives after the training stream's work).  Without an
+    initialised process group the rank's own vector is kept."""
+
+    def __init__(self, engine, every: int = 1024, group=None):
+        self.engine, self.group = engine, group
+        self.every = max(1, int(every))
+        self.next = self.every
+        self.t0 = time.perf_counter()
+        self.aggs: List[Tuple] = []
+        self.last: dict = {}
+
+    def _aggregate(self, st: dict) -> None:
+        v = metric_vector(self.engine, time.perf_counter() - self.t0, st.get("avg_return", float("nan")))
+        self.aggs.append(aggregate_device(v, self.group) if _initialised() else (v, v))
+
+    def __call__(self, st: dict) -> None:
+        self.last = st
+        if st["gradient_steps"] >= self.next:
+            self.next = (st["gradient_steps"] // self.every + 1) * self.every
+            self._aggregate(st)
+
+    def finish(self) -> dict:
+        """The final aggregation (after the loop's last step) and its host view."""
+        self._aggregate(self.last)
+        import torch.distributed as dist
+
+        world = dist.get_world_size(self.group) if _initialised() else 1
+        return summarise_aggregates(self.aggs, world, self.every)
 
 
 def summarise_aggregates(aggs, world: int, every: int) -> dict:
@@ -95,8 +139,9 @@ def summarise_aggregates(aggs, world: int, every: int) -> dict:
         return {"every": every, "aggregations": 0}
     s, m = aggs[-1]
     s, m = s.tolist(), m.tolist()
+    fin = lambda xs: [x if math.isfinite(x) else None for x in xs]  # noqa: E731  (JSON: no NaN)
     return {"every": every, "aggregations": len(aggs), "world": world, "fields": list(REPLICA_METRICS),
-            "last_sum": s, "last_mean": [x / world for x in s], "last_max": m}
+            "last_sum": fin(s), "last_mean": fin([x / world for x in s]), "last_max": fin(m)}
 
 
 def timed_region(run, sync, device: Optional[torch.device] = None, group=None) -> float:

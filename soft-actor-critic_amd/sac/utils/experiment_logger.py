@@ -7,7 +7,7 @@ Same run directory, writers, tags and hparams record as the reference:
 floats and bools kept, everything else ``str()``-ed) and whose metrics are
 the given names as floats, ``{"placeholder_metric": 0.0}`` when empty
 (reference :104-112, :129-148).  Pinned against the reference's own calls by
-tests/test_ref_pins.py (tests/golden/ref_logger.json).
+tests/test_logger_pins.py (tests/golden/ref_logger.json).
 
 TensorBoard is optional: without ``torch.utils.tensorboard`` the writers keep
 every call in memory (``_NullWriter.calls``), and the .npy dumps still work.

@@ -45,7 +45,10 @@ def test_bench_spawns_its_ranks_and_reports_replicas():
     assert rm["fields"][0] == "steps"
     assert rm["last_sum"][0] == 2 * (4 + 40)  # each replica's step counter: warm-up + timed
     assert rm["last_max"][0] == 4 + 40
-    assert rm["last_mean"][1] == pytest.approx(1.0)  # the stub's L_Q1 on both ranks
+    assert rm["fields"][2] == "q1_loss" and rm["fields"][7] == "mean_return"
+    assert rm["last_mean"][2] == pytest.approx(1.0)  # the stub's L_Q1 on both ranks
+    assert rm["last_max"][1] > 0  # wall_s: the slower rank's time so far
+    assert rm["last_sum"][7] is None  # mean_return: no episodes in a bench (NaN -> null)
 
 
 def test_bench_single_gpu_runs_in_process():

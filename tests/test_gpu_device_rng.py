@@ -14,9 +14,9 @@ restated in oracle/sampler_oracle.py.  These tests pin that path:
   * device-RNG steps (eager and graph-replayed, staged next-step batches
     included) equal the oracle fed the restated indices AND eps, at the fp32
     tolerances of tests/test_gpu_parity.py;
-  * a 200-step C2 fp32 run with injected inputs stays on the oracle: every
-    step's losses within 1e-4 rel, and the final parameters within the drift
-    bound written in the test.
+  * a 200-step C2 fp32 run with injected inputs stays on the oracle: the
+    losses within 1e-5 rel over the first 50 steps and 1e-3 rel over all 200,
+    and the parameters within the drift bounds written in the test.
 """
 import ctypes
 

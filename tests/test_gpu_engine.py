@@ -247,10 +247,12 @@ def test_role_split_equals_fused(precision, monkeypatch):
         assert torch.equal(out["1"][k], out["0"][k]), k
 
 
-def test_large_batch_uses_fused_kernels_and_runs():
-    """C3 (B=4096): 256 row tiles do not fit the role split; the fused kernels run."""
+def test_large_batch_uses_fused_kernels_and_runs(monkeypatch):
+    """C3 (B=4096): 256 row tiles do not fit the role split; the one-block-per-
+    row-tile kernels run (SAC_WIDE=0; the default is the stage path)."""
+    monkeypatch.setenv("SAC_WIDE", "0")
     eng, rb, c = _engine("c3", "bf16", capacity=20_000)
-    assert not eng.roles
+    assert not eng.roles and not eng.wide
     eng.train_graph(rb, 20, chunk=10)
     eng.check()
     assert all(np.isfinite(eng.losses()))
@@ -267,6 +269,8 @@ def test_staged_batch_equals_in_step_gather(cfg, precision, fuse, monkeypatch):
     from sac import _engine as E
 
     monkeypatch.setenv("SAC_FUSE", fuse)
+    if cfg == "c3":
+        monkeypatch.setenv("SAC_WIDE", "0")  # batch staging is a feature of the row-tile kernels
     if fuse != "0":
         monkeypatch.setenv("SAC_SPLIT", "0")  # fused layouts run the one-workgroup-per-role kernels
     out = {}

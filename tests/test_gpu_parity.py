@@ -156,7 +156,9 @@ def test_edge_shapes_match_oracle(shape, precision):
     tolerances as the BASELINE configs (parity unpinned by the reference at
     these shapes; the oracle is pinned by the 8 reference fixtures)."""
     c = dict(EDGE_SHAPES[shape], name=shape)
-    _check_config_against_oracle(c, precision, 2 if c["batch"] > 1024 else 3)
+    # y / log pi against the oracle's trajectory after step 1: 2e-3 at these
+    # shapes (measured 6.1e-4 at obs 256, step 3: Adam sign flips of ~0 gradients)
+    _check_config_against_oracle(c, precision, 2 if c["batch"] > 1024 else 3, traj_tol=2e-3)
 
 
 @pytest.mark.parametrize("precision", ["fp32", "bf16"])
@@ -181,7 +183,7 @@ def _engine_mlp(eng, key):
                                  "relu")
 
 
-def _check_config_against_oracle(c, precision, steps, roles=None):
+def _check_config_against_oracle(c, precision, steps, roles=None, traj_tol=1e-4):
     import bench
 
     ckey = "_parity_" + c.get("name", "cfg")
@@ -233,8 +235,9 @@ def _check_config_against_oracle(c, precision, steps, roles=None):
             # against the oracle's own trajectory: from step 2 on, an Adam update
             # whose gradient is ~0 may take the other sign under another
             # summation order (that element moves +-lr instead of -+lr, inside
-            # the parameter bounds below); measured 6.1e-4 in log pi at obs 256, step 3
-            tol = 1e-4 if k == 1 else 2e-3
+            # the parameter bounds below): traj_tol (1e-4 for the BASELINE
+            # configs; the edge shapes pass their measured bound)
+            tol = 1e-4 if k == 1 else traj_tol
             np.testing.assert_allclose(y, ref["y"], rtol=tol, atol=tol)
             np.testing.assert_allclose(lp, ref["log_pi"], rtol=tol, atol=tol)
         else:

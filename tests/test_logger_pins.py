@@ -159,3 +159,17 @@ def test_q_value_log_equals_eager_values_on_cpu(monkeypatch):
         ql1.record(s[0], a[0], k)
     ql1.finish()
     assert got == want1
+    # one record() larger than the ring (2 * every rows: a vector env with
+    # num_envs > 2 * q_values_flush_every) grows it instead of failing
+    got.clear()
+    ql2 = QValueLog(agent, L(), every=1)
+    s = g.standard_normal((5, 3)).astype(np.float32)
+    a = g.uniform(-1, 1, (5, 2)).astype(np.float32)
+    with torch.no_grad():
+        st, ac = torch.from_numpy(s), torch.from_numpy(a)
+        q1, q2 = agent.q_net1(st, ac).reshape(-1), agent.q_net2(st, ac).reshape(-1)
+    ql2.record(s, a, 1)
+    ql2.record(s[:2], a[:2], 6)
+    ql2.finish()
+    assert [x[2] for x in got] == [1, 2, 3, 4, 5, 6, 7]
+    np.testing.assert_allclose(np.array([x[:2] for x in got[:5]]), torch.stack([q1, q2], 1).numpy(), rtol=1e-6)
