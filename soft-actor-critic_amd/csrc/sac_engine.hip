@@ -438,13 +438,17 @@ static void build_wide(sac_engine* e, char* base) {
   }
   W.GTpi_out = np.l[hp].GT;
   W.dbppi_out = np.l[hp].dbp;
+  W.rng_step = e->buf.rng_step;
+  W.stamp_stage = -1;
+  if (const char* v = getenv("SAC_WIDE_STAMP_STAGE")) W.stamp_stage = atoi(v);
   e->wdd = (WideDev*)(base + wl.o_dev);
   e->wjobs = (WJob*)(base + wl.o_jobs);
   std::vector<WJob>& JB = e->hostW;
   JB.clear();
   e->wst.clear();
   const int KC = esz == 4 ? MM<float>::KC : MM<bf16>::KC;
-  const size_t lds_base = (size_t)2 * 64 * WLDA + (size_t)2 * 4 * (WKB / KC) * 256;  // floats
+  // A/B double buffers + the row-seed area (also the epilogue's weight slices, <= WWS floats)
+  const size_t lds_base = (size_t)2 * 64 * WLDA + (size_t)2 * 4 * (WKB / KC) * 256 + WWS;  // floats
   auto stage_gemm = [&](std::vector<WJob> js, int phase, int last) {
     int item = 0;
     size_t lf = lds_base;
@@ -452,6 +456,7 @@ static void build_wide(sac_engine* e, char* base) {
       j.item0 = item;
       item += j.nrb * j.ncb;
       if (j.amode == WA_OUTBWD) lf = std::max(lf, lds_base + 64 * WLDD + (size_t)j.J * j.Kp);
+      if ((j.OUTP && (size_t)j.Nout * WBN > WWS) || (j.DA && (size_t)WBN * A > WWS)) lf = ~(size_t)0 / 8;  // refused
     }
     sac_engine::WStage st{1, (int)JB.size(), (int)(JB.size() + js.size()), item, phase, last, lf * 4};
     e->wst.push_back(st);
@@ -554,7 +559,7 @@ static void build_wide(sac_engine* e, char* base) {
     e->wst.push_back(st);
   };
   // ---- phase A
-  add(0, Brw / 64, 0);  // gather
+  add(0, (B + WGR - 1) / WGR, 0);  // gather
   for (int d = 0; d < std::max(hp, hq); ++d) {
     std::vector<WJob> js;
     if (d < hp)
@@ -631,9 +636,77 @@ static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
   int maxKp = 32, maxNo = 32;
   size_t xt_q0 = 0;
   const int nrt0 = (B + SAC_ROWS - 1) / SAC_ROWS;
+  // dims-only pre-pass: the padded widths the phase kernels' LDS layout needs
+  EngineDev probe;
+  memset(&probe, 0, sizeof(probe));
+  for (int ni = 0; ni < 5; ++ni) {
+    const bool is_pi = ni == NET_PI;
+    const int L = is_pi ? c->pi_layers : c->q_layers;
+    const int* dims = is_pi ? c->pi_dims : c->q_dims;
+    for (int l = 0; l < L; ++l) {
+      probe.net[ni].l[l].Kp = rup(dims[l], SAC_PAD);
+      probe.net[ni].l[l].Np = rup(dims[l + 1], SAC_PAD);
+      maxKp = std::max(maxKp, probe.net[ni].l[l].Kp);
+      if (l < L - 1) maxKp = std::max(maxKp, probe.net[ni].l[l].Np);
+      else maxNo = std::max(maxNo, probe.net[ni].l[l].Np);
+    }
+  }
+  int split = 0;  // decided below; the layout lambda reads it
+  auto lds_layout = [&](EngineDev& hh, int xrows, bool full) -> int {
+    const int R = SAC_ROWS;
+    hh.ld = maxKp + 4;
+    hh.ldo = maxNo + 4;
+    int lo = 0;
+    auto lt = [&](int floats) {
+      lo = (lo + 3) & ~3;  // 16-B alignment
+      const int o = lo;
+      lo += floats;
+      return o;
+    };
+    hh.o_X = lt(xrows * hh.ld);
+    hh.o_Y = lt(xrows * hh.ld);
+    const int Lhq = c->q_layers - 1, Lhp = c->pi_layers - 1;
+    for (int l = 0; full && l < std::max(Lhq, Lhp); ++l) {
+      int np = 0;
+      if (l < Lhq) np = std::max(np, hh.net[NET_Q1].l[l].Np);
+      if (l < Lhp) np = std::max(np, hh.net[NET_PI].l[l].Np);
+      hh.ldp1[l] = np + 4;
+      hh.o_P1[l] = lt(R * hh.ldp1[l]);
+    }
+    for (int l = 0; full && l < Lhq; ++l) {
+      hh.ldp2[l] = hh.net[NET_Q2].l[l].Np + 4;
+      hh.o_P2[l] = lt(R * hh.ldp2[l]);
+    }
+    hh.o_s = lt(R * O);
+    hh.o_s2 = lt(R * O);
+    hh.o_a = lt(R * A);
+    hh.o_a2 = lt(R * A);
+    hh.o_r = lt(R);
+    hh.o_d = lt(R);
+    hh.o_et = lt(R * A);
+    hh.o_ea = lt(R * A);
+    hh.o_out = lt(xrows * hh.ldo);
+    hh.o_outp = lt(xrows * hh.ldo);
+    hh.o_out2 = lt(R * hh.ldo);
+    hh.o_outp2 = lt(R * hh.ldo);
+    hh.o_lp = lt(R);
+    hh.o_qt = lt(2 * R);
+    hh.o_y = lt(R);
+    hh.o_g = lt(R * hh.ldo);
+    hh.o_g2 = lt(R * hh.ldo);
+    hh.o_ga = lt(R * A);
+    hh.o_gout = lt(R * hh.ldo);
+    hh.o_slot = lt(2 * R);  // int64[R]
+    hh.o_red = split ? lt(SAC_NW * 256) : 0;
+    return lo;
+  };
+  // does the phase kernels' layout fit a CU?  (per-network roles: R rows; one
+  // block per row tile: pi on [s'; s], 2R rows)
+  const bool lds_fits_roles = (size_t)lds_layout(probe, SAC_ROWS, true) * 4 <= 160 * 1024;
+  const bool lds_fits_rows = (size_t)lds_layout(probe, 2 * SAC_ROWS, true) * 4 <= 160 * 1024;
   // hidden-split role kernels (sac_split.h): two hidden layers of width 256 in
   // both nets, identity pi output, 2 act <= 32, and 12 * nrt co-resident blocks
-  int split = c->q_layers == 3 && c->pi_layers == 3 && c->q_dims[1] == SPLIT_H && c->q_dims[2] == SPLIT_H &&
+  split = lds_fits_roles && c->q_layers == 3 && c->pi_layers == 3 && c->q_dims[1] == SPLIT_H && c->q_dims[2] == SPLIT_H &&
               c->pi_dims[1] == SPLIT_H && c->pi_dims[2] == SPLIT_H && c->pi_out_act == SAC_ACT_IDENTITY &&
               2 * A <= 32 && (10 + split_wpi(esz)) * nrt0 <= 256 && (3 * split_wc(esz) + 1) * nrt0 <= 256 &&
               SAC_ROWS * (A + 1) <= SAC_HAND_STRIDE;
@@ -762,7 +835,10 @@ static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
   {
     int roles_pre = 6 * nrt0 <= 256 && SAC_ROWS * (A + 1) <= SAC_HAND_STRIDE;
     if (const char* v = getenv("SAC_ROLES")) roles_pre = roles_pre && atoi(v) != 0;
-    int on = !split && !roles_pre && c->q_layers >= 3 && c->pi_layers >= 3 && 2 * A <= WJMAX;
+    // ... or where the phase kernels' LDS layout does not fit a CU (hidden
+    // layers wider than 256, wide inputs): the stage path takes any width
+    const bool too_big = !(roles_pre ? lds_fits_roles : lds_fits_rows);
+    int on = !split && (!roles_pre || too_big) && c->q_layers >= 3 && c->pi_layers >= 3 && 2 * A <= WJMAX;
     if (const char* v = getenv("SAC_WIDE")) on = on && atoi(v) != 0;
     wl.on = on;
   }
@@ -815,58 +891,16 @@ static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
   const size_t o_part = lay.take((size_t)nhalf * SAC_PART_STRIDE * 8);  // batch-half partial dW granules of split tiles
   const size_t total = lay.take(0);
 
-  // LDS layout (floats)
-  const int R = SAC_ROWS;
-  h.ld = maxKp + 4;
-  h.ldo = maxNo + 4;
-  int lo = 0;
-  auto lt = [&](int floats) {
-    lo = (lo + 3) & ~3;  // 16-B alignment
-    const int o = lo;
-    lo += floats;
-    return o;
-  };
+  // LDS layout (floats) of the row-tile / role kernels (policy_act included).
   // role split of phases A/C (decided here: it sizes the LDS): 6 * nrt
   // workgroups must be co-resident (one per CU).  Only the one-block-per-row-
   // tile kernels run pi on [s'; s] (2R rows); with roles every MLP pass is R rows.
+  // The stage path (wl.on) launches none of them but policy_act: R rows, no
+  // pre-activation buffers.
   int roles = 6 * nrt <= 256 && SAC_ROWS * (A + 1) <= SAC_HAND_STRIDE;
   if (const char* v = getenv("SAC_ROLES")) roles = roles && atoi(v) != 0;
-  const int xrows = roles ? R : 2 * R;
-  h.o_X = lt(xrows * h.ld);
-  h.o_Y = lt(xrows * h.ld);
-  const int Lhq = c->q_layers - 1, Lhp = c->pi_layers - 1;
-  for (int l = 0; l < std::max(Lhq, Lhp); ++l) {
-    int np = 0;
-    if (l < Lhq) np = std::max(np, h.net[NET_Q1].l[l].Np);
-    if (l < Lhp) np = std::max(np, h.net[NET_PI].l[l].Np);
-    h.ldp1[l] = np + 4;
-    h.o_P1[l] = lt(R * h.ldp1[l]);
-  }
-  for (int l = 0; l < Lhq; ++l) {
-    h.ldp2[l] = h.net[NET_Q2].l[l].Np + 4;
-    h.o_P2[l] = lt(R * h.ldp2[l]);
-  }
-  h.o_s = lt(R * O);
-  h.o_s2 = lt(R * O);
-  h.o_a = lt(R * A);
-  h.o_a2 = lt(R * A);
-  h.o_r = lt(R);
-  h.o_d = lt(R);
-  h.o_et = lt(R * A);
-  h.o_ea = lt(R * A);
-  h.o_out = lt(xrows * h.ldo);
-  h.o_outp = lt(xrows * h.ldo);
-  h.o_out2 = lt(R * h.ldo);
-  h.o_outp2 = lt(R * h.ldo);
-  h.o_lp = lt(R);
-  h.o_qt = lt(2 * R);
-  h.o_y = lt(R);
-  h.o_g = lt(R * h.ldo);
-  h.o_g2 = lt(R * h.ldo);
-  h.o_ga = lt(R * A);
-  h.o_gout = lt(R * h.ldo);
-  h.o_slot = lt(2 * R);  // int64[R]
-  h.o_red = split ? lt(SAC_NW * 256) : 0;
+  roles = roles && !wl.on;
+  const int lo = lds_layout(h, wl.on || roles ? SAC_ROWS : 2 * SAC_ROWS, !wl.on);
 
   if (e) {
     h.B = B;
@@ -1287,14 +1321,20 @@ static void launch_kind(sac_engine* e, int kind, const sac_replay* rb, const int
 // One launch of the large-batch stage path (sac_wide.h).
 template <typename T>
 static void launch_wide_stage(sac_engine* e, const sac_engine::WStage& st, const sac_replay* rb, const int32_t* idx,
-                              const float* eps, hipStream_t s) {
+                              const float* eps, hipStream_t s, bool stage_next, const int32_t* next_idx) {
+  const size_t glds = (size_t)((WGR * (e->cfg.obs_dim + e->cfg.act_dim) + 1) & ~1) * 4 + WGR * 8;
   switch (st.kind) {
     case 0:
-      sac_wide_gather<T><<<st.grid, WG_T, 0, s>>>(e->d, e->wdd, *rb, idx);
+      sac_wide_gather<T><<<st.grid, WG_T, glds, s>>>(e->d, e->wdd, *rb, idx);
       break;
-    case 1:
-      sac_wide_stage<T><<<st.grid, WG_T, st.lds, s>>>(e->d, e->wdd, e->wjobs + st.j0, st.j1 - st.j0, st.last);
+    case 1: {
+      // the last phase-C stage also gathers the next step's batch (when there is one in this call)
+      const int ng = st.last && stage_next ? (e->cfg.batch + WGR - 1) / WGR : 0;
+      const int flags = st.last | (&st == &e->wst[1] ? 2 : 0) | (ng ? 4 : 0) | (int)((&st - e->wst.data()) << 8);
+      sac_wide_stage<T><<<st.grid + ng, WG_T, std::max(st.lds, ng ? glds : 0), s>>>(
+          e->d, e->wdd, e->wjobs + st.j0, st.j1 - st.j0, flags, st.grid, *rb, next_idx);
       break;
+    }
     case 2:
       sac_wide_head<T><<<st.grid, WG_T, 0, s>>>(e->d, e->wdd, eps);
       break;
@@ -1307,11 +1347,11 @@ static void launch_wide_stage(sac_engine* e, const sac_engine::WStage& st, const
   }
 }
 static void launch_wide(sac_engine* e, const sac_engine::WStage& st, const sac_replay* rb, const int32_t* idx,
-                        const float* eps, hipStream_t s) {
+                        const float* eps, hipStream_t s, bool stage_next = false, const int32_t* next_idx = nullptr) {
   if (e->cfg.precision == SAC_PREC_BF16)
-    launch_wide_stage<bf16>(e, st, rb, idx, eps, s);
+    launch_wide_stage<bf16>(e, st, rb, idx, eps, s, stage_next, next_idx);
   else
-    launch_wide_stage<float>(e, st, rb, idx, eps, s);
+    launch_wide_stage<float>(e, st, rb, idx, eps, s, stage_next, next_idx);
 }
 
 // Fused-step launches of n consecutive steps (one step per launch, sac_persist.h).
@@ -1358,8 +1398,12 @@ static void launch_steps(sac_engine* e, const sac_replay* rb, int n, const int32
     for (int i = 0; i < n; ++i) {
       const int32_t* ix = indices ? indices + (size_t)i * B : nullptr;
       const float* ep = eps ? eps + (size_t)i * 2 * B * A : nullptr;
+      // step i > 0 of the call uses the batch step i - 1 gathered in its last phase-C stage
+      const bool next = i + 1 < n;
+      const int32_t* nix = indices && next ? indices + (size_t)(i + 1) * B : nullptr;
       for (const sac_engine::WStage& st : e->wst) {
-        launch_wide(e, st, rb, ix, ep, s);
+        if (st.kind == 0 && i > 0) continue;
+        launch_wide(e, st, rb, ix, ep, s, next, nix);
         if (kinds) kinds->push_back(st.phase);
         if (ev) {
           hipEvent_t x;

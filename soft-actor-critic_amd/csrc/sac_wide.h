@@ -41,6 +41,7 @@
 #define WLDE 68    // LDS row stride of the epilogue tile
 #define WLDD 17    // LDS row stride of the per-row seeds (J <= 16)
 #define WJMAX 16
+#define WWS 1088   // floats of the epilogue weight slices (OUTP: Nout x 64; DA: 64 x A)
 
 enum WAMode { WA_PLAIN = 0, WA_ACT = 1, WA_OUTBWD = 2 };
 enum WEMode { WE_FWD = 0, WE_BWD = 1 };
@@ -73,6 +74,8 @@ struct WideDev {
   float* dbpq_out[2];
   void* GTpi_out;
   float* dbppi_out;
+  int stamp_stage;  // stamps builds: the stage index that writes stamps (SAC_WIDE_STAMP_STAGE)
+  const uint64_t* rng_step;  // = EngineDev::rng_step (read through the prefetched WideDev lines)
 };
 
 // One GEMM of a stage: output tiles (row block rb, column block cb), items
@@ -122,6 +125,34 @@ struct WJob {
   int adbp_ld, pad_;
 };
 
+static_assert(sizeof(WJob) <= 448, "extend wide_prefetch");
+static_assert(sizeof(WideDev) <= 384, "extend wide_prefetch");
+
+// Every 64-B line of the stage's job descriptor and of WideDev touched once at
+// entry with back-to-back scalar loads (one latency instead of one per line
+// at first use; see prefetch_engine).
+__device__ __forceinline__ void wide_prefetch(const void* job, const void* wd) {
+  const uint64_t a = (uint64_t)(uintptr_t)job, b = (uint64_t)(uintptr_t)wd;
+  asm volatile("s_load_dword s95, %0, 0\n\t" "s_load_dword s95, %0, 64\n\t" "s_load_dword s95, %0, 128\n\t"
+               "s_load_dword s95, %0, 192\n\t" "s_load_dword s95, %0, 256\n\t" "s_load_dword s95, %0, 320\n\t"
+               "s_load_dword s95, %0, 384\n\t" "s_load_dword s95, %1, 0\n\t" "s_load_dword s95, %1, 64\n\t"
+               "s_load_dword s95, %1, 128\n\t" "s_load_dword s95, %1, 192\n\t" "s_load_dword s95, %1, 256\n\t"
+               "s_load_dword s95, %1, 320\n\t" "s_waitcnt lgkmcnt(0)" :: "s"(a), "s"(b) : "s95", "memory");
+}
+
+// In-kernel stamps of one stage (stamps builds: the stage whose index is
+// WideDev::stamp_stage writes s_memrealtime at slot i of its block's row)
+#ifdef SAC_STAMPS
+#define WSTAMP(i)                                                                                          \
+  do {                                                                                                     \
+    if (wst && threadIdx.x == 0) GP(long long, E.stamps)[blockIdx.x * 64 + (i)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+#else
+#define WSTAMP(i) \
+  do {            \
+  } while (0)
+#endif
+
 __device__ __forceinline__ bool wrow_ok(const AS_C WideDev& W, int r) { return r % W.Brw < W.B; }
 
 // T-typed 4-element store of 4 consecutive batch columns (16 B fp32 / 8 B bf16)
@@ -157,10 +188,22 @@ __device__ __forceinline__ void wide_rowpro(const AS_C EngineDev& E, const AS_C 
       float seed = 0.f, sq = 0.f, y = 0.f;
       if (v) {
         float a1 = 0.f, a2 = 0.f, aq = 0.f;
-        for (int c = 0; c < W.ncb_q; ++c) {
-          a1 += GPC(float, W.OUTPqt[0])[c * W.cbs_q + lr];
-          a2 += GPC(float, W.OUTPqt[1])[c * W.cbs_q + lr];
-          aq += GPC(float, W.OUTPq[qi])[c * W.cbs_q + lr];
+        for (int c0 = 0; c0 < W.ncb_q; c0 += 4) {  // every load of a batch of 4 blocks in flight together
+          float x1[4], x2[4], xq[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const int c = c0 + u < W.ncb_q ? c0 + u : W.ncb_q - 1;
+            x1[u] = GPC(float, W.OUTPqt[0])[c * W.cbs_q + lr];
+            x2[u] = GPC(float, W.OUTPqt[1])[c * W.cbs_q + lr];
+            xq[u] = GPC(float, W.OUTPq[qi])[c * W.cbs_q + lr];
+          }
+#pragma unroll
+          for (int u = 0; u < 4; ++u)
+            if (c0 + u < W.ncb_q) {
+              a1 += x1[u];
+              a2 += x2[u];
+              aq += xq[u];
+            }
         }
         const float t1 = act_fwd(qt1.out_act, a1 + GPC(float, qt1.l[qt1.L - 1].bias)[0]);
         const float t2 = act_fwd(qt2.out_act, a2 + GPC(float, qt2.l[qt2.L - 1].bias)[0]);
@@ -200,9 +243,20 @@ __device__ __forceinline__ void wide_rowpro(const AS_C EngineDev& E, const AS_C 
       const AS_C NetDev& q2 = E.net[NET_Q2];
       float a1 = 0.f, a2 = 0.f;
       if (v)
-        for (int c = 0; c < W.ncb_q; ++c) {
-          a1 += GPC(float, W.OUTPc[0])[c * W.cbs_q + lr];
-          a2 += GPC(float, W.OUTPc[1])[c * W.cbs_q + lr];
+        for (int c0 = 0; c0 < W.ncb_q; c0 += 4) {  // every load of a batch of 4 blocks in flight together
+          float x1[4], x2[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const int c = c0 + u < W.ncb_q ? c0 + u : W.ncb_q - 1;
+            x1[u] = GPC(float, W.OUTPc[0])[c * W.cbs_q + lr];
+            x2[u] = GPC(float, W.OUTPc[1])[c * W.cbs_q + lr];
+          }
+#pragma unroll
+          for (int u = 0; u < 4; ++u)
+            if (c0 + u < W.ncb_q) {
+              a1 += x1[u];
+              a2 += x2[u];
+            }
         }
       const float p1 = a1 + GPC(float, q1.l[q1.L - 1].bias)[0], p2 = a2 + GPC(float, q2.l[q2.L - 1].bias)[0];
       const float o1 = act_fwd(q1.out_act, p1), o2 = act_fwd(q2.out_act, p2);
@@ -231,9 +285,20 @@ __device__ __forceinline__ void wide_rowpro(const AS_C EngineDev& E, const AS_C 
       float gm = 0.f, gs = 0.f;
       if (v) {
         float d1 = 0.f, d2 = 0.f;
-        for (int c = 0; c < W.ncb_da; ++c) {
-          d1 += GPC(float, W.DA[0])[c * W.cbs_da + (size_t)lr * A + j];
-          d2 += GPC(float, W.DA[1])[c * W.cbs_da + (size_t)lr * A + j];
+        for (int c0 = 0; c0 < W.ncb_da; c0 += 4) {  // every load of a batch of 4 blocks in flight together
+          float x1[4], x2[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const int c = c0 + u < W.ncb_da ? c0 + u : W.ncb_da - 1;
+            x1[u] = GPC(float, W.DA[0])[c * W.cbs_da + (size_t)lr * A + j];
+            x2[u] = GPC(float, W.DA[1])[c * W.cbs_da + (size_t)lr * A + j];
+          }
+#pragma unroll
+          for (int u = 0; u < 4; ++u)
+            if (c0 + u < W.ncb_da) {
+              d1 += x1[u];
+              d2 += x2[u];
+            }
         }
         const float ga = d1 + d2;
         const float gl = alpha32 * (1.0f / (float)B);
@@ -292,13 +357,24 @@ __device__ __forceinline__ void wide_rowpro(const AS_C EngineDev& E, const AS_C 
 // ---------------------------------------------------------------------------- one GEMM item
 template <typename T>
 __device__ __forceinline__ void wide_item(const AS_C EngineDev& E, const AS_C WideDev& W, const AS_C WJob& jb, int it,
-                                          lf* lds, int par) {
+                                          lf* lds, int par, bool wst) {
   constexpr int KC = MM<T>::KC, KL = MM<T>::KL, NCH = WKB / KC;
   typedef typename MM<T>::Frag F;
   const int tid = threadIdx.x, lane = tid & 63, wave = wave_id();
   const int c = lane & 15, g = lane >> 4;
   const int wr = wave >> 1, wc = wave & 1;
-  const int rb = it / jb.ncb, cb = it % jb.ncb;
+  // item -> (row block, column block): the column blocks of one row block 8
+  // items apart, i.e. on one XCD under round-robin placement (speed only), so
+  // the row block's A operand is fetched into one L2 and re-read from there
+  int rb, cb;
+  if ((jb.nrb & 7) == 0 && (jb.item0 & 7) == 0) {
+    const int grp = it / (8 * jb.ncb), rem = it % (8 * jb.ncb);
+    cb = rem >> 3;
+    rb = grp * 8 + (rem & 7);
+  } else {
+    rb = it / jb.ncb;
+    cb = it % jb.ncb;
+  }
   const int row0 = rb * WBM, col0 = cb * WBN;
   const int NT = jb.Np >> 4, t0 = col0 >> 4, nchT = jb.tcols / KC;
   const int Kp = jb.Kp, nkb = Kp / WKB;
@@ -309,6 +385,21 @@ __device__ __forceinline__ void wide_item(const AS_C EngineDev& E, const AS_C Wi
   lf* Wol = Dl + 64 * WLDD;           // [J][Kp] output layer weights (WA_OUTBWD)
   const bool outbwd = jb.amode == WA_OUTBWD;
   const int J = jb.J;
+  // the epilogue's weight slices (WWS floats): output layer columns of this block
+  // [Nout][64] (OUTP) or layer-0 action columns [64][A] (DA), staged here so the
+  // epilogue's dot products read LDS, not one dependent global load per term
+  lf* Ws = outbwd ? Wol + J * Kp : Dl;
+  if (jb.OUTP) {
+    for (int i = tid; i < jb.Nout * WBN; i += WG_T) {
+      const int j = i / WBN, k = i % WBN;
+      Ws[i] = col0 + k < jb.N ? GPC(float, jb.Wout)[(size_t)j * jb.ldwout + col0 + k] : 0.f;
+    }
+  } else if (jb.DA) {
+    for (int i = tid; i < WBN * W.A; i += WG_T) {
+      const int k = i / W.A, j = i % W.A;
+      Ws[i] = col0 + k < jb.N ? GPC(float, jb.W0a)[(size_t)(col0 + k) * jb.ldw0 + jb.a_off + j] : 0.f;
+    }
+  }
 
   if (outbwd) {
     wide_rowpro<T>(E, W, jb, row0, cb, par, Dl);
@@ -319,30 +410,34 @@ __device__ __forceinline__ void wide_item(const AS_C EngineDev& E, const AS_C Wi
     __syncthreads();
   }
 
-  f32x4 ra[2];
-  u32x4 rbv[NCH];
-  auto load = [&](int kb) __attribute__((always_inline)) {
+  // K blocks staged two ahead: two register sets, R0 for even blocks, R1 for odd
+  struct Regs {
+    f32x4 a[2];
+    u32x4 b[NCH];
+  };
+  Regs R0, R1;
+  auto load = [&](int kb, Regs& R) __attribute__((always_inline)) {
     const int k0 = kb * WKB;
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const int p = tid + WG_T * u, row = p >> 3, kq = p & 7;
-      ra[u] = *(const AS_G f32x4*)(GPC(float, jb.X) + (size_t)(row0 + row) * jb.ldx + k0 + 4 * kq);
+      R.a[u] = *(const AS_G f32x4*)(GPC(float, jb.X) + (size_t)(row0 + row) * jb.ldx + k0 + 4 * kq);
     }
 #pragma unroll
     for (int v = 0; v < NCH; ++v) {
       const int pb = tid + WG_T * v, ct = pb / (64 * NCH), rest = pb % (64 * NCH), ch = rest >> 6, ln = rest & 63;
       const int t = t0 + ct;
-      rbv[v] = t < NT ? *(const AS_G u32x4*)(GPC(T, jb.Wp) + ((size_t)(t * nchT + kb * NCH + ch) * 64 + ln) * KL)
+      R.b[v] = t < NT ? *(const AS_G u32x4*)(GPC(T, jb.Wp) + ((size_t)(t * nchT + kb * NCH + ch) * 64 + ln) * KL)
                       : u32x4{0u, 0u, 0u, 0u};
     }
   };
-  auto store = [&](int kb, int buf) __attribute__((always_inline)) {
+  auto store = [&](int kb, int buf, const Regs& R) __attribute__((always_inline)) {
     const int k0 = kb * WKB;
     lf* Aq = Ab + buf * 64 * WLDA;
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const int p = tid + WG_T * u, row = p >> 3, kq = p & 7;
-      f32x4 v = ra[u];
+      f32x4 v = R.a[u];
       if (jb.amode == WA_ACT) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) v[e] = act_fwd(jb.aact, v[e]);
@@ -359,7 +454,7 @@ __device__ __forceinline__ void wide_item(const AS_C EngineDev& E, const AS_C Wi
     }
     lf* Bq = Bb + buf * BBUF;
 #pragma unroll
-    for (int v = 0; v < NCH; ++v) *(AS_L u32x4*)(Bq + (tid + WG_T * v) * 4) = rbv[v];
+    for (int v = 0; v < NCH; ++v) *(AS_L u32x4*)(Bq + (tid + WG_T * v) * 4) = R.b[v];
   };
   f32x4 acc[2][2];
 #pragma unroll
@@ -405,27 +500,46 @@ __device__ __forceinline__ void wide_item(const AS_C EngineDev& E, const AS_C Wi
     }
   };
 
-  load(0);
-  store(0, 0);
+  // the epilogue's biases, loaded before the K loop (their latency hides under it)
+  const bool fwd = jb.emode == WE_FWD;
+  float bias_r[2];
+#pragma unroll
+  for (int ct = 0; ct < 2; ++ct) {
+    const int n = col0 + wc * 32 + ct * 16 + c;
+    bias_r[ct] = (fwd && n < jb.N) ? GPC(float, jb.bias)[n] : 0.f;
+  }
+  WSTAMP(1);
+  // block kb is loaded into registers two iterations before it is stored to
+  // LDS (its loads have two blocks of MFMAs to land), stored one iteration
+  // before it is computed (one barrier per block)
+  load(0, R0);
+  if (nkb > 1) load(1, R1);
+  store(0, 0, R0);
   __syncthreads();
-  for (int kb = 0; kb < nkb; ++kb) {
+  WSTAMP(2);
+  auto iter = [&](int kb, Regs& Rnext2, const Regs& Rnext1) __attribute__((always_inline)) {
     const int cur = kb & 1;
-    if (kb + 1 < nkb) load(kb + 1);
+    if (kb + 2 < nkb) load(kb + 2, Rnext2);
     if (agt) agt_store(kb, cur);
     comp(cur);
-    if (kb + 1 < nkb) store(kb + 1, cur ^ 1);
+    if (kb + 1 < nkb) store(kb + 1, cur ^ 1, Rnext1);
     __syncthreads();
+    if (kb < 8) WSTAMP(3 + kb);
+  };
+  for (int kb = 0; kb < nkb; kb += 2) {  // unrolled by two: the register sets stay static
+    iter(kb, R0, R1);
+    if (kb + 1 < nkb) iter(kb + 1, R1, R0);
   }
+  WSTAMP(11);
 
   // ---- epilogue through an LDS tile [64][WLDE] (aliases the K-loop buffers)
   lf* Et = lds;
-  const bool fwd = jb.emode == WE_FWD;
 #pragma unroll
   for (int rt = 0; rt < 2; ++rt)
 #pragma unroll
     for (int ct = 0; ct < 2; ++ct) {
       const int cl = wc * 32 + ct * 16 + c, n = col0 + cl;
-      const float bn = (fwd && n < jb.N) ? GPC(float, jb.bias)[n] : 0.f;
+      const float bn = bias_r[ct];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int r = wr * 32 + rt * 16 + 4 * g + i;
@@ -434,6 +548,7 @@ __device__ __forceinline__ void wide_item(const AS_C EngineDev& E, const AS_C Wi
       }
     }
   __syncthreads();
+  WSTAMP(12);
   if (!fwd) {  // dY of the layer below = act'(P_prev) * dX, in place (row pieces)
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
@@ -473,8 +588,7 @@ __device__ __forceinline__ void wide_item(const AS_C EngineDev& E, const AS_C Wi
       for (int i = tid; i < 64 * W.A; i += WG_T) {
         const int r = i / W.A, j = i % W.A;
         float s = 0.f;
-        for (int k = 0; k < WBN && col0 + k < jb.N; ++k)
-          s += Et[r * WLDE + k] * GPC(float, jb.W0a)[(size_t)(col0 + k) * jb.ldw0 + jb.a_off + j];
+        for (int k = 0; k < WBN; ++k) s += Et[r * WLDE + k] * Ws[k * W.A + j];
         GP(float, jb.DA)[cb * jb.da_cb + (size_t)(row0 + r) * W.A + j] = s;
       }
     }
@@ -506,42 +620,115 @@ __device__ __forceinline__ void wide_item(const AS_C EngineDev& E, const AS_C Wi
     for (int i = tid; i < 64 * No; i += WG_T) {
       const int r = i / No, j = i % No;
       float s = 0.f;
-      for (int k = 0; k < WBN && col0 + k < jb.N; ++k)
-        s += GPC(float, jb.Wout)[(size_t)j * jb.ldwout + col0 + k] * act_fwd(jb.oact, Et[r * WLDE + k]);
+      for (int k = 0; k < WBN; ++k) s += Ws[j * WBN + k] * act_fwd(jb.oact, Et[r * WLDE + k]);
       GP(float, jb.OUTP)[cb * jb.outp_cb + (size_t)(row0 + r) * No + j] = s;
     }
   }
 }
 
+// ---------------------------------------------------------------------------- gather
+// One step's batch (replay_buffer.py:32-39, agent.py:166-193) into the row-major
+// layer-0 inputs and the layer-0 X^T stashes, WGR rows per workgroup: each
+// thread issues up to 8 independent replay loads before storing any (sampled
+// rows are random lines: one memory latency per batch of loads, not per load),
+// the (s, a) columns go through LDS to the k-major X^T stores.  Runs as its own
+// launch for the first step of a call, and inside the last phase-C stage of
+// step t for step t + 1 (every buffer it writes is past its last reader of
+// step t: the layer-0 inputs and rewards are read in phase A and by phase C's
+// first stage, the critics' X^T by phase B, and pi's X^T is the other step
+// parity's copy from the one phase D of step t reads).
+#define WGR 16
 template <typename T>
-__global__ void __launch_bounds__(WG_T) sac_wide_stage(const EngineDev* __restrict__ Ep, const WideDev* __restrict__ Wd,
-                                                       const WJob* __restrict__ jobs, int njobs, int last) {
-  const AS_C EngineDev& E = *(const AS_C EngineDev*)Ep;
-  const AS_C WideDev& W = *(const AS_C WideDev*)Wd;
-  extern __shared__ float lds_raw[];
-  int j = 0;
-  while (j + 1 < njobs && (int)blockIdx.x >= ((const AS_C WJob*)jobs)[j + 1].item0) ++j;
-  const AS_C WJob& jb = ((const AS_C WJob*)jobs)[j];
-  const int par = (int)(*GPC(uint64_t, E.rng_step) & 1);
-  wide_item<T>(E, W, jb, (int)blockIdx.x - jb.item0, (lf*)lds_raw, par);
-  if (last) phase_c_done(E);  // the step's last launch before phase D advances the step
+__device__ __forceinline__ void wide_gather_rows(const AS_C EngineDev& E, const AS_C WideDev& W, const sac_replay& rb,
+                                                 const int32_t* __restrict__ inj_idx_, uint64_t step, int blk,
+                                                 lf* gl) {
+  // LDS: [WGR][O + A] (s, a) of the block's rows, then the rows' replay slots
+  // (all dynamic: a static array would push the stage kernel past the 160 KiB
+  // dynamic-LDS attribute)
+  const int tid = threadIdx.x, O = W.O, A = W.A, B = W.B, OA = O + A;
+  AS_L int64_t* slot = (AS_L int64_t*)(gl + ((WGR * OA + 1) & ~1));
+  const int row0 = blk * WGR;
+  const int par = (int)(step & 1);
+  if (tid < WGR) {
+    const int64_t size = GPC(int64_t, rb.state)[0], pos = GPC(int64_t, rb.state)[1];
+    const int b = row0 + tid;
+    int64_t sl = -1;
+    if (b < B) {
+      int64_t li;
+      if (inj_idx_) {
+        li = GPC(int32_t, inj_idx_)[b];
+      } else {
+        const Feistel f = feistel_make(E.seed, step, size);
+        li = feistel_sample(f, b, size);
+      }
+      sl = size < rb.capacity ? li : (pos + li) % rb.capacity;
+    }
+    slot[tid] = sl;
+  }
+  __syncthreads();
+  const RowStrides rs = row_strides(rb.row_stride, O, A);
+  const int Wf = 2 * O + A + 2, total = WGR * Wf;
+  constexpr int U = 8;
+  for (int base = 0; base < total; base += U * WG_T) {
+    float v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {  // every load of the batch first
+      const int i = base + u * WG_T + tid;
+      const int r = i / Wf, f = i % Wf;
+      const int64_t sl = i < total ? slot[r] : -1;
+      const int64_t src = sl < 0 ? 0 : sl;
+      const AS_G float* p = f < O ? GPC(float, rb.obs) + src * rs.obs + f
+                          : f < 2 * O ? GPC(float, rb.next_obs) + src * rs.obs + (f - O)
+                          : f < 2 * O + A ? GPC(float, rb.act) + src * rs.act + (f - 2 * O)
+                          : f == 2 * O + A ? GPC(float, rb.rew) + src * rs.one : GPC(float, rb.done) + src * rs.one;
+      v[u] = *p;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = base + u * WG_T + tid;
+      if (i >= total) continue;
+      const int r = i / Wf, f = i % Wf, b = row0 + r;
+      if (slot[r] < 0) continue;
+      const float x = v[u];
+      if (f < O) {
+        GP(float, W.Xpi0)[(size_t)(W.Brw + b) * W.ldpi0 + f] = x;
+        GP(float, W.Xq0)[(size_t)b * W.ldq0 + f] = x;
+        GP(float, W.Xc0)[(size_t)b * W.ldq0 + f] = x;
+        gl[r * OA + f] = x;
+      } else if (f < 2 * O) {
+        GP(float, W.Xpi0)[(size_t)b * W.ldpi0 + (f - O)] = x;
+        GP(float, W.Xqt0)[(size_t)b * W.ldq0 + (f - O)] = x;
+      } else if (f < 2 * O + A) {
+        GP(float, W.Xq0)[(size_t)b * W.ldq0 + O + (f - 2 * O)] = x;
+        gl[r * OA + O + (f - 2 * O)] = x;
+      } else if (f == 2 * O + A) {
+        GP(float, W.R)[b] = x;
+      } else {
+        GP(float, W.Dn)[b] = x;
+      }
+    }
+  }
+  __syncthreads();
+  // X^T stashes of layer 0: the critics' (s, a) and the actor rows' s (the step's parity copy)
+  const AS_C LayerDev& q0 = E.net[NET_Q1].l[0];
+  const AS_C LayerDev& p0 = E.net[NET_PI].l[0];
+  T* xq = (T*)q0.XT;
+  T* xp = (T*)p0.XT + par * p0.xt_par;
+  for (int i = tid; i < OA * WGR; i += WG_T) {  // k-major: WGR consecutive batch columns per k
+    const int k = i / WGR, r = i % WGR, b = row0 + r;
+    if (b >= B) continue;
+    const float x = gl[r * OA + k];
+    xq[(size_t)k * W.Bp + b] = MM<T>::cvt(x);
+    if (k < O) xp[(size_t)k * W.Bp + b] = MM<T>::cvt(x);
+  }
 }
 
-// ---------------------------------------------------------------------------- gather (phase A, first)
-// The step's batch (replay_buffer.py:32-39, agent.py:166-193) into the row-major
-// layer-0 inputs and the layer-0 X^T stashes; block 0 also derives the step's
-// Adam bias corrections (torch adam.py) as phase A of the row-tile path does.
-template <typename T>
-__global__ void __launch_bounds__(WG_T) sac_wide_gather(const EngineDev* __restrict__ Ep, const WideDev* __restrict__ Wd,
-                                                        sac_replay rb, const int32_t* __restrict__ inj_idx_) {
-  const AS_C EngineDev& E = *(const AS_C EngineDev*)Ep;
-  const AS_C WideDev& W = *(const AS_C WideDev*)Wd;
-  __shared__ int64_t slot[64];
-  const int tid = threadIdx.x, O = W.O, A = W.A, B = W.B;
-  const int row0 = blockIdx.x * 64;
-  const uint64_t step = *GPC(uint64_t, E.rng_step);
-  const int par = (int)(step & 1);
-  if (blockIdx.x == 0 && tid < 4 && (tid < 3 || (E.auto_entropy && E.alpha_update))) {
+// The step's optimizer step counts and Adam bias corrections (torch adam.py:
+// step_size = lr / (1 - beta1^t), sqrt(1 - beta2^t)), once per step by block 0
+// of the step's first GEMM stage (the row-tile path does it in phase A).
+__device__ __forceinline__ void wide_step_scalars(const AS_C EngineDev& E, int par) {
+  const int tid = threadIdx.x;
+  if (tid < 4 && (tid < 3 || (E.auto_entropy && E.alpha_update))) {
     const double t = GP(double, E.opt_steps)[tid] + 1.0;
     GP(double, E.opt_steps)[tid] = t;
     if (tid < 3) {
@@ -553,61 +740,15 @@ __global__ void __launch_bounds__(WG_T) sac_wide_gather(const EngineDev* __restr
       GP(double, E.alpha_sc)[par * 2 + 1] = 1.0 - pow((double)E.beta2, t);
     }
   }
-  const int64_t size = GPC(int64_t, rb.state)[0], pos = GPC(int64_t, rb.state)[1];
-  if (tid < 64) {
-    const int b = row0 + tid;
-    int64_t s = -1;
-    if (b < B) {
-      int64_t li;
-      if (inj_idx_) {
-        li = GPC(int32_t, inj_idx_)[b];
-      } else {
-        const Feistel f = feistel_make(E.seed, step, size);
-        li = feistel_sample(f, b, size);
-      }
-      s = size < rb.capacity ? li : (pos + li) % rb.capacity;
-    }
-    slot[tid] = s;
-  }
-  __syncthreads();
-  const RowStrides rs = row_strides(rb.row_stride, O, A);
-  const int Wf = 2 * O + A + 2;
-  for (int i = tid; i < 64 * Wf; i += WG_T) {
-    const int r = i / Wf, f = i % Wf, b = row0 + r;
-    const int64_t sl = slot[r];
-    if (sl < 0) continue;
-    if (f < O) {
-      const float v = GPC(float, rb.obs)[sl * rs.obs + f];
-      GP(float, W.Xpi0)[(size_t)(W.Brw + b) * W.ldpi0 + f] = v;
-      GP(float, W.Xq0)[(size_t)b * W.ldq0 + f] = v;
-      GP(float, W.Xc0)[(size_t)b * W.ldq0 + f] = v;
-    } else if (f < 2 * O) {
-      const float v = GPC(float, rb.next_obs)[sl * rs.obs + (f - O)];
-      GP(float, W.Xpi0)[(size_t)b * W.ldpi0 + (f - O)] = v;
-      GP(float, W.Xqt0)[(size_t)b * W.ldq0 + (f - O)] = v;
-    } else if (f < 2 * O + A) {
-      const float v = GPC(float, rb.act)[sl * rs.act + (f - 2 * O)];
-      GP(float, W.Xq0)[(size_t)b * W.ldq0 + O + (f - 2 * O)] = v;
-    } else if (f == 2 * O + A) {
-      GP(float, W.R)[b] = GPC(float, rb.rew)[sl * rs.one];
-    } else {
-      GP(float, W.Dn)[b] = GPC(float, rb.done)[sl * rs.one];
-    }
-  }
-  __syncthreads();
-  // X^T stashes of layer 0: the critics' (s, a) and the actor rows' s (this step's parity copy)
-  const AS_C LayerDev& q0 = E.net[NET_Q1].l[0];
-  const AS_C LayerDev& p0 = E.net[NET_PI].l[0];
-  T* xq = (T*)q0.XT;
-  T* xp = (T*)p0.XT + par * p0.xt_par;
-  for (int i = tid; i < (O + A) * 64; i += WG_T) {  // k-major: 64 consecutive batch columns per k
-    const int k = i / 64, r = i % 64, b = row0 + r;
-    const int64_t sl = slot[r];
-    if (b >= B || sl < 0) continue;
-    const float v = k < O ? GPC(float, rb.obs)[sl * rs.obs + k] : GPC(float, rb.act)[sl * rs.act + (k - O)];
-    xq[(size_t)k * W.Bp + b] = MM<T>::cvt(v);
-    if (k < O) xp[(size_t)k * W.Bp + b] = MM<T>::cvt(v);
-  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(WG_T) sac_wide_gather(const EngineDev* __restrict__ Ep, const WideDev* __restrict__ Wd,
+                                                        sac_replay rb, const int32_t* __restrict__ inj_idx_) {
+  const AS_C EngineDev& E = *(const AS_C EngineDev*)Ep;
+  const AS_C WideDev& W = *(const AS_C WideDev*)Wd;
+  extern __shared__ float lds_raw[];
+  wide_gather_rows<T>(E, W, rb, inj_idx_, *GPC(uint64_t, E.rng_step), blockIdx.x, (lf*)lds_raw);
 }
 
 // ---------------------------------------------------------------------------- pi heads (phase A)
@@ -631,9 +772,20 @@ __global__ void __launch_bounds__(WG_T) sac_wide_head(const EngineDev* __restric
   float lp = 0.f, corr = 0.f;
   if (live) {
     float am = 0.f, as = 0.f;
-    for (int c = 0; c < W.ncb_pi; ++c) {
-      am += GPC(float, W.OUTPpi)[c * W.cbs_pi + (size_t)r * 2 * A + j];
-      as += GPC(float, W.OUTPpi)[c * W.cbs_pi + (size_t)r * 2 * A + A + j];
+    for (int c0 = 0; c0 < W.ncb_pi; c0 += 8) {  // every load of a batch of 8 blocks in flight together
+      float xm[8], xs[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int c = c0 + u < W.ncb_pi ? c0 + u : W.ncb_pi - 1;
+        xm[u] = GPC(float, W.OUTPpi)[c * W.cbs_pi + (size_t)r * 2 * A + j];
+        xs[u] = GPC(float, W.OUTPpi)[c * W.cbs_pi + (size_t)r * 2 * A + A + j];
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (c0 + u < W.ncb_pi) {
+          am += xm[u];
+          as += xs[u];
+        }
     }
     const AS_G float* bo = GPC(float, pi.l[pi.L - 1].bias);
     const float pm = am + bo[j], ps = as + bo[A + j];
@@ -685,3 +837,44 @@ __global__ void __launch_bounds__(WG_T) sac_wide_head(const EngineDev* __restric
     }
   }
 }
+
+// ---------------------------------------------------------------------------- the stage kernel
+// flags: bit 0 = the step's last launch before phase D (advances the step),
+// bit 1 = the step's first GEMM stage (block 0 derives the step's Adam scalars),
+// bit 2 = blocks [nitems, grid) gather the next step's batch; bits 8.. = the
+// stage's index in the step (stamps builds)
+template <typename T>
+__global__ void __launch_bounds__(WG_T, 4) sac_wide_stage(const EngineDev* __restrict__ Ep, const WideDev* __restrict__ Wd,
+                                                       const WJob* __restrict__ jobs, int njobs, int flags, int nitems,
+                                                       sac_replay rb, const int32_t* __restrict__ next_idx) {
+  const AS_C EngineDev& E = *(const AS_C EngineDev*)Ep;
+  const AS_C WideDev& W = *(const AS_C WideDev*)Wd;
+  extern __shared__ float lds_raw[];
+  if ((int)blockIdx.x >= nitems) {  // flags & 4: the next step's batch (see wide_gather_rows)
+    wide_gather_rows<T>(E, W, rb, next_idx, *GPC(uint64_t, E.rng_step) + 1, (int)blockIdx.x - nitems, (lf*)lds_raw);
+    if (flags & 1) phase_c_done(E);
+    return;
+  }
+  if ((flags & 2) && blockIdx.x == 0) wide_step_scalars(E, (int)(*GPC(uint64_t, E.rng_step) & 1));
+#ifdef SAC_STAMPS
+  const bool wst = E.stamps && (flags >> 8) == W.stamp_stage;
+#else
+  const bool wst = false;
+#endif
+  WSTAMP(0);
+  int j = 0;
+  while (j + 1 < njobs && (int)blockIdx.x >= ((const AS_C WJob*)jobs)[j + 1].item0) ++j;
+  const AS_C WJob& jb = ((const AS_C WJob*)jobs)[j];
+  wide_prefetch(jobs + j, Wd);
+  const int par = (int)(*GPC(uint64_t, W.rng_step) & 1);
+  wide_item<T>(E, W, jb, (int)blockIdx.x - jb.item0, (lf*)lds_raw, par, wst);
+#ifdef SAC_STAMPS
+  if (wst) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    WSTAMP(13);
+  }
+#endif
+  if (flags & 1) phase_c_done(E);  // the step's last launch before phase D advances the step
+}
+

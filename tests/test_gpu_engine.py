@@ -555,3 +555,36 @@ def test_fused_step_equals_four_launches(lib, cfg, precision, monkeypatch):
         out[fused]["stats"] = eng.stats.clone()
     for k in out["1"]:
         assert torch.equal(out["1"][k], out["0"][k]), (k, (out["1"][k].double() - out["0"][k].double()).abs().max())
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_stage_path_staged_batches_equal_fresh_gathers(precision):
+    """The stage path (csrc/sac_wide.h) gathers step t+1's batch inside step t's
+    last phase-C launch; the first step of every call gathers its own.  So one
+    call of 5 steps (device RNG) must equal 5 calls of one step, bit for bit,
+    and the same with injected indices; graph replay equals eager launches."""
+    out = {}
+    for mode in ("one_call", "per_step", "graph"):
+        eng, rb, c = _engine("c3", precision, capacity=12_000)
+        assert eng.wide > 0
+        if mode == "one_call":
+            eng.train(rb, 5)
+        elif mode == "per_step":
+            for _ in range(5):
+                eng.train(rb, 1)
+        else:
+            eng.train_graph(rb, 5, chunk=5)
+        r9 = np.random.default_rng(9)
+        idx = torch.from_numpy(np.stack([r9.choice(len(rb), size=c["batch"], replace=False) for _ in range(3)])
+                               .astype(np.int32))
+        if mode == "per_step":
+            for i in range(3):
+                eng.train(rb, 1, indices=idx[i:i + 1])
+        else:
+            eng.train(rb, 3, indices=idx)
+        eng.check()
+        out[mode] = {k: v.clone() for k, v in eng.state_tensors().items()}
+        out[mode]["stats"] = eng.stats.clone()
+    for mode in ("per_step", "graph"):
+        for k in out["one_call"]:
+            assert torch.equal(out["one_call"][k], out[mode][k]), (mode, k)

@@ -146,6 +146,12 @@ EDGE_SHAPES = {
     "rowtile_b4001": dict(obs=24, act=4, hidden=[256, 256], batch=4001, capacity=8192),
     "obs256": dict(obs=256, act=6, hidden=[256, 256], batch=64, capacity=1024),
     "deep4": dict(obs=11, act=3, hidden=[128, 96, 64], batch=80, capacity=1024),
+    # past the phase kernels' LDS layout: the stage path (csrc/sac_wide.h) at small batches
+    "obs300": dict(obs=300, act=6, hidden=[256, 256], batch=64, capacity=1024),
+    "wide400_300": dict(obs=17, act=6, hidden=[400, 300], batch=256, capacity=2048),
+    "wide512_b384": dict(obs=24, act=4, hidden=[512, 512], batch=384, capacity=2048),
+    # the stage path at a large batch with ragged column blocks and three hidden layers
+    "wide_deep_b1100": dict(obs=5, act=3, hidden=[96, 160, 64], batch=1100, capacity=4096),
 }
 
 
@@ -161,20 +167,55 @@ def test_edge_shapes_match_oracle(shape, precision):
     _check_config_against_oracle(c, precision, 2 if c["batch"] > 1024 else 3, traj_tol=2e-3)
 
 
-@pytest.mark.parametrize("precision", ["fp32", "bf16"])
-def test_too_wide_input_is_refused_cleanly(precision):
-    """An input the LDS layout cannot hold (obs 300 with [256, 256] nets: the
-    workgroup would need > 160 KiB) fails in engine creation with the size in
-    the message -- no launch, no fallback."""
+@pytest.mark.parametrize("shape", ["obs300", "wide400_300", "wide512_b384", "wide_deep_b1100", "rowtile_b4001"])
+def test_stage_path_is_used_where_the_phase_kernels_do_not_fit(shape):
+    """Shapes past the phase kernels' LDS layout, and batches past the role
+    split, run the layer-synchronous stage path (no fallback, no refusal)."""
     import bench
-    from sac._engine import EngineError
 
-    bench.CONFIGS["_parity_obs300"] = dict(obs=300, act=6, hidden=[256, 256], batch=64, capacity=256)
+    bench.CONFIGS["_stage"] = dict(EDGE_SHAPES[shape])
     try:
-        with pytest.raises(EngineError, match="B of LDS per workgroup"):
-            bench.build_engine("_parity_obs300", precision, 3, torch.device("cuda", 0))
+        eng, rb, cc = bench.build_engine("_stage", "fp32", 3, torch.device("cuda", 0))
     finally:
-        del bench.CONFIGS["_parity_obs300"]
+        del bench.CONFIGS["_stage"]
+    assert eng.wide > 0 and not eng.roles
+    eng.train(rb, 2)
+    eng.check()
+    assert all(np.isfinite(eng.losses()))
+
+
+def _relu_ties(mlp, x, rel=1e-7):
+    """Does a hidden ReLU pre-activation of this forward sit within fp32
+    summation-order noise of 0?  |p| <= rel * (|W| |x| + |b|): its sign -- and
+    so the unit's whole backward for that row -- then depends on the order of
+    the fp32 sum, and a correct fp32 engine may decide it the other way from
+    the numpy oracle.  tools/debug/pi0_grad.py found one at [512, 512], B = 384,
+    step 2 (profiles/r04_debug_wide512_relu_tie.txt): pi layer 1, one row,
+    pre-activation 5.8e-8; the engine's pi layer-0 gradient differed from
+    float64 by exactly that row's rank-one term (singular values 3.7e-4 vs
+    1e-8).  The stage path and round 3's role variant both decided it the same way."""
+    h = np.asarray(x, np.float64)
+    for i in range(len(mlp.W) - 1):
+        W, b = mlp.W[i].astype(np.float64), mlp.b[i].astype(np.float64)
+        p = h @ W.T + b
+        if np.any(np.abs(p) <= rel * (np.abs(h) @ np.abs(W).T + np.abs(b))):
+            return True
+        h = np.maximum(p, 0.0)
+    return False
+
+
+def _tied_nets(st, bt):
+    """Networks whose element-fraction check a ReLU tie of this step voids (the
+    max-error bound still applies): pi on the actor rows s, each critic (and its
+    target) on the batch (s, a)."""
+    tied = set()
+    if _relu_ties(st.pi, bt.s):
+        tied.add("policy")
+    sa = np.concatenate([bt.s, bt.a], 1)
+    for k, net in (("q1", st.q1), ("q2", st.q2)):
+        if _relu_ties(net, sa):
+            tied |= {k, k + "t"}
+    return tied
 
 
 def _engine_mlp(eng, key):
@@ -206,6 +247,7 @@ def _check_config_against_oracle(c, precision, steps, roles=None, traj_tol=1e-4)
     rtol = 1e-4 if precision == "fp32" else 2e-3 * max(1.0, (256 / B) ** 0.5)
     lrs = {"policy": hp.actor_lr, "q1": hp.critic_lr, "q2": hp.critic_lr, "q1t": hp.critic_lr * hp.tau,
            "q2t": hp.critic_lr * hp.tau}
+    tied = set()
     for k in range(1, steps + 1):
         idx = g.choice(len(rb), size=B, replace=False).astype(np.int32)
         et = g.standard_normal((B, A)).astype(np.float32)
@@ -214,6 +256,7 @@ def _check_config_against_oracle(c, precision, steps, roles=None, traj_tol=1e-4)
         # the engine's own pre-step state, for the one-step (local) check of y and log pi
         pre = {n: _engine_mlp(eng, n) for n in ("pi", "q1t", "q2t")}
         alpha_pre = np.float32(eng.alpha_state[1].item())
+        tied |= _tied_nets(st, bt)  # once the trajectories split at a tie they stay split
         ref = O.training_step(st, hp, bt, et, ea)
         eng.train(rb, 1, indices=torch.from_numpy(idx).reshape(1, B),
                   eps=torch.from_numpy(np.stack([et, ea])).reshape(1, 2, B, A))
@@ -251,7 +294,7 @@ def _check_config_against_oracle(c, precision, steps, roles=None, traj_tol=1e-4)
             for pk, want in _oracle_net(st, key).state_dict().items():
                 d = np.abs(mine[pk] - want)
                 assert d.max() <= 2 * lr + 1e-5, (c.get('name'), precision, k, key, pk, d.max())
-                if precision == "fp32":
+                if precision == "fp32" and key not in tied:
                     assert np.mean(d <= 1e-6) >= 0.995, (c.get('name'), k, key, pk, np.mean(d <= 1e-6))
                 ds.append(d.ravel())
             if precision == "bf16":
@@ -278,7 +321,8 @@ def _oracle_state_from_engine(eng, act):
                       opt_alpha_v=float(al[3]), opt_alpha_step=float(steps[3]))
 
 
-@pytest.mark.parametrize("shape", ["c2_split", "c4", "roles_b384", "rowtile_b2000"])
+@pytest.mark.parametrize("shape", ["c2_split", "c4", "roles_b384", "rowtile_b2000", "rowtile_b2000_wide0",
+                                   "wide512_b384", "wide400_300"])
 def test_one_step_from_the_engine_state(shape, monkeypatch):
     """Per-step parity without trajectory drift (fp32): before every step the
     oracle is loaded with the engine's FULL state (parameters, Adam moments and
@@ -286,15 +330,21 @@ def test_one_step_from_the_engine_state(shape, monkeypatch):
     the five networks must match the engine's to 1e-6 for >= 99.9% of the
     elements (a handful may sit where Adam divides a ~0 gradient by ~eps) and
     to 2 lr everywhere; losses to 1e-5 rel (L_pi against the scale of its terms).  Four steps per shape, covering the
-    hidden-split, role and row-tile kernel layouts."""
+    hidden-split, role and row-tile kernel layouts and the stage path (B = 2000 with
+    [128, 128], and [512, 512] / [400, 300] hidden layers at small batches)."""
     import bench
 
     c = {"c2_split": dict(obs=24, act=4, hidden=[256, 256], batch=256, capacity=2048),
          "c4": dict(obs=32, act=2, hidden=[256, 256], batch=256, capacity=2048),
          "roles_b384": dict(obs=24, act=4, hidden=[256, 256], batch=384, capacity=2048),
-         "rowtile_b2000": dict(obs=17, act=6, hidden=[128, 128], batch=2000, capacity=4096)}[shape]
+         "rowtile_b2000": dict(obs=17, act=6, hidden=[128, 128], batch=2000, capacity=4096),
+         "rowtile_b2000_wide0": dict(obs=17, act=6, hidden=[128, 128], batch=2000, capacity=4096),
+         "wide512_b384": dict(obs=24, act=4, hidden=[512, 512], batch=384, capacity=2048),
+         "wide400_300": dict(obs=17, act=6, hidden=[400, 300], batch=256, capacity=2048)}[shape]
     if shape == "roles_b384":
         monkeypatch.setenv("SAC_SPLIT", "0")
+    if shape == "rowtile_b2000_wide0":
+        monkeypatch.setenv("SAC_WIDE", "0")  # the one-block-per-row-tile kernels
     bench.CONFIGS["_local"] = c
     try:
         eng, rb, cc = bench.build_engine("_local", "fp32", 3, torch.device("cuda", 0))
@@ -310,8 +360,9 @@ def test_one_step_from_the_engine_state(shape, monkeypatch):
         et = g.standard_normal((B, A)).astype(np.float32)
         ea = g.standard_normal((B, A)).astype(np.float32)
         st = _oracle_state_from_engine(eng, A)
-        ref = O.training_step(st, hp, O.Batch(rows["obs"][idx], rows["act"][idx], rows["rew"][idx],
-                                              rows["next_obs"][idx], rows["done"][idx]), et, ea)
+        bt = O.Batch(rows["obs"][idx], rows["act"][idx], rows["rew"][idx], rows["next_obs"][idx], rows["done"][idx])
+        tied = {{"policy": "pi"}.get(n, n) for n in _tied_nets(st, bt)}  # this step only: the state is reloaded
+        ref = O.training_step(st, hp, bt, et, ea)
         eng.train(rb, 1, indices=torch.from_numpy(idx).reshape(1, B),
                   eps=torch.from_numpy(np.stack([et, ea])).reshape(1, 2, B, A))
         torch.cuda.synchronize()
@@ -324,6 +375,7 @@ def test_one_step_from_the_engine_state(shape, monkeypatch):
             for pk, want in net.state_dict().items():
                 d = np.abs(mine[pk] - want)
                 assert d.max() <= 2 * lrs[n], (shape, k, n, pk, d.max())
-                assert np.mean(d <= 1e-6) >= 0.999, (shape, k, n, pk, np.mean(d <= 1e-6))
+                if n not in tied:
+                    assert np.mean(d <= 1e-6) >= 0.999, (shape, k, n, pk, np.mean(d <= 1e-6))
         assert abs(float(eng.alpha_state[0].item()) - st.log_alpha) <= 1e-7
     eng.check()
