@@ -446,23 +446,37 @@ static void build_wide(sac_engine* e, char* base) {
   std::vector<WJob>& JB = e->hostW;
   JB.clear();
   e->wst.clear();
-  const int KC = esz == 4 ? MM<float>::KC : MM<bf16>::KC;
-  // A/B double buffers + the row-seed area (also the epilogue's weight slices, <= WWS floats)
-  const size_t lds_base = (size_t)2 * 64 * WLDA + (size_t)2 * 4 * (WKB / KC) * 256 + WWS;  // floats
+  // the two K-block buffers + the epilogue's weight slices (WWS floats); WA_OUTBWD
+  // adds the row seeds and the output layer's weights
+  // K-block buffers: as many (2..4) as keep the stage's workgroups co-resident
+  // in one round (items / CUs per CU) in 160 KiB of LDS per CU
+  const size_t kbuf = esz == 4 ? WK<float>::BUF : WK<bf16>::BUF;  // floats
+  const int ncu = e->ncu > 0 ? e->ncu : 256;
   auto stage_gemm = [&](std::vector<WJob> js, int phase, int last) {
     int item = 0;
-    size_t lf = lds_base;
+    size_t extra = WWS;  // floats past the K buffers
     for (WJob& j : js) {
+      if (j.amode != js[0].amode) fprintf(stderr, "sac_engine: internal: mixed A modes in one stage\n"), abort();
       j.item0 = item;
       item += j.nrb * j.ncb;
-      if (j.amode == WA_OUTBWD) lf = std::max(lf, lds_base + 64 * WLDD + (size_t)j.J * j.Kp);
-      if ((j.OUTP && (size_t)j.Nout * WBN > WWS) || (j.DA && (size_t)WBN * A > WWS)) lf = ~(size_t)0 / 8;  // refused
+      if (j.amode == WA_OUTBWD) extra = std::max(extra, (size_t)WWS + 64 * WLDD + (size_t)j.J * j.Kp);
+      if ((j.OUTP && (size_t)j.Nout * WBN > WWS) || (j.DA && (size_t)WBN * A > WWS)) extra = ~(size_t)0 / 64;  // refused
     }
+    const int per_cu = std::max(1, (item + ncu - 1) / ncu);
+    int nb = 2;
+    for (int b = 4; b > 2; --b)
+      if ((size_t)per_cu * (b * kbuf + extra) * 4 <= 160 * 1024) {
+        nb = b;
+        break;
+      }
+    for (WJob& j : js) j.nbuf = nb;
+    const size_t lf = nb * kbuf + extra;
     sac_engine::WStage st{1, (int)JB.size(), (int)(JB.size() + js.size()), item, phase, last, lf * 4};
     e->wst.push_back(st);
     JB.insert(JB.end(), js.begin(), js.end());
   };
-  auto fwd = [&](int ni, int l, int M, const float* X, float* Pd, void* XT, int xt_row0, long xt_par, float* OUTP) {
+  auto fwd = [&](int ni, int l, int M, const float* X, float* Pd, void* XT, int xt_row0, long xt_par, float* OUTP,
+                 int p_row0 = 0) {
     const NetDev& nd = h.net[ni];
     const LayerDev& ly = nd.l[l];
     WJob j;
@@ -483,6 +497,7 @@ static void build_wide(sac_engine* e, char* base) {
     j.bias = nd.P + ly.b_off;
     j.emode = WE_FWD;
     j.P = Pd;
+    j.p_row0 = p_row0;
     j.ldp = ly.Np;
     j.oact = nd.hid_act;
     j.XT = XT;
@@ -563,8 +578,9 @@ static void build_wide(sac_engine* e, char* base) {
   for (int d = 0; d < std::max(hp, hq); ++d) {
     std::vector<WJob> js;
     if (d < hp)
+      // the last hidden layer's P is read by pi's backward only: actor rows [Brw, 2 Brw)
       js.push_back(fwd(NET_PI, d, 2 * Brw, d ? F(wl.o_P[0][d - 1]) : W.Xpi0, F(wl.o_P[0][d]), np.l[d + 1].XT, Brw,
-                       np.l[d + 1].xt_par, d == hp - 1 ? W.OUTPpi : nullptr));
+                       np.l[d + 1].xt_par, d == hp - 1 ? W.OUTPpi : nullptr, d == hp - 1 ? Brw : 0));
     for (int qi = 0; qi < 2; ++qi)
       if (d < hq)
         js.push_back(fwd(NET_Q1 + qi, d, Brw, d ? F(wl.o_P[1 + qi][d - 1]) : W.Xq0, F(wl.o_P[1 + qi][d]),
@@ -579,7 +595,8 @@ static void build_wide(sac_engine* e, char* base) {
   for (int d = 0; d < hq; ++d) {
     std::vector<WJob> js;
     for (int qi = 0; qi < 2; ++qi)
-      js.push_back(fwd(NET_Q1T + qi, d, Brw, d ? F(wl.o_P[3 + qi][d - 1]) : W.Xqt0, F(wl.o_P[3 + qi][d]), nullptr, 0, 0,
+      js.push_back(fwd(NET_Q1T + qi, d, Brw, d ? F(wl.o_P[3 + qi][d - 1]) : W.Xqt0,
+                       d < hq - 1 ? F(wl.o_P[3 + qi][d]) : nullptr, nullptr, 0, 0,  // no backward: last P unread
                        d == hq - 1 ? W.OUTPqt[qi] : nullptr));
     stage_gemm(js, 0, 0);
   }
@@ -828,18 +845,20 @@ static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
       (ni == NET_PI ? nD : nB) += t * parts;
       nhalf += t * (parts - 1);  // producer parts: one granule slot each
     }
-  // Large-batch stage path (sac_wide.h): where the per-network
-  // role kernels do not fit (6 nrt > 256 co-resident workgroups) and both nets
-  // have at least two hidden layers.  SAC_WIDE=0 keeps the row-tile kernels.
+  // Layer-synchronous stage path (sac_wide.h): where the phase
+  // kernels' LDS layout does not fit a CU (hidden layers wider than 256, wide
+  // inputs: the stage path takes any width), for nets with at least two hidden
+  // layers.  At C3 the row-tile kernels are faster (profiles/r04_ab_c3_paths.txt),
+  // so they keep the batches they fit; SAC_WIDE=1 forces the stage path on any
+  // batch past the hidden split, SAC_WIDE=0 refuses it.
   WideLay wl;
   {
     int roles_pre = 6 * nrt0 <= 256 && SAC_ROWS * (A + 1) <= SAC_HAND_STRIDE;
     if (const char* v = getenv("SAC_ROLES")) roles_pre = roles_pre && atoi(v) != 0;
-    // ... or where the phase kernels' LDS layout does not fit a CU (hidden
-    // layers wider than 256, wide inputs): the stage path takes any width
     const bool too_big = !(roles_pre ? lds_fits_roles : lds_fits_rows);
-    int on = !split && (!roles_pre || too_big) && c->q_layers >= 3 && c->pi_layers >= 3 && 2 * A <= WJMAX;
-    if (const char* v = getenv("SAC_WIDE")) on = on && atoi(v) != 0;
+    const bool able = !split && c->q_layers >= 3 && c->pi_layers >= 3 && 2 * A <= WJMAX;
+    int on = able && too_big;
+    if (const char* v = getenv("SAC_WIDE")) on = atoi(v) != 0 ? able : 0;
     wl.on = on;
   }
   if (wl.on) {
@@ -1262,7 +1281,12 @@ static void set_lds_attrs(size_t bytes) {
   (void)hipFuncSetAttribute((const void*)sac_critic_update<T>, hipFuncAttributeMaxDynamicSharedMemorySize, b);
   (void)hipFuncSetAttribute((const void*)sac_actor_update<T>, hipFuncAttributeMaxDynamicSharedMemorySize, b);
   (void)hipFuncSetAttribute((const void*)sac_persist<T>, hipFuncAttributeMaxDynamicSharedMemorySize, b);
-  (void)hipFuncSetAttribute((const void*)sac_wide_stage<T>, hipFuncAttributeMaxDynamicSharedMemorySize, b);
+  (void)hipFuncSetAttribute((const void*)sac_wide_stage<T, WA_PLAIN, false>, hipFuncAttributeMaxDynamicSharedMemorySize, b);
+  (void)hipFuncSetAttribute((const void*)sac_wide_stage<T, WA_ACT, false>, hipFuncAttributeMaxDynamicSharedMemorySize, b);
+  (void)hipFuncSetAttribute((const void*)sac_wide_stage<T, WA_OUTBWD, false>, hipFuncAttributeMaxDynamicSharedMemorySize, b);
+  (void)hipFuncSetAttribute((const void*)sac_wide_stage<T, WA_PLAIN, true>, hipFuncAttributeMaxDynamicSharedMemorySize, b);
+  (void)hipFuncSetAttribute((const void*)sac_wide_stage<T, WA_ACT, true>, hipFuncAttributeMaxDynamicSharedMemorySize, b);
+  (void)hipFuncSetAttribute((const void*)sac_wide_stage<T, WA_OUTBWD, true>, hipFuncAttributeMaxDynamicSharedMemorySize, b);
 }
 
 // empty kernel: the dispatch + event gap of sac_engine_time_phases
@@ -1331,8 +1355,14 @@ static void launch_wide_stage(sac_engine* e, const sac_engine::WStage& st, const
       // the last phase-C stage also gathers the next step's batch (when there is one in this call)
       const int ng = st.last && stage_next ? (e->cfg.batch + WGR - 1) / WGR : 0;
       const int flags = st.last | (&st == &e->wst[1] ? 2 : 0) | (ng ? 4 : 0) | (int)((&st - e->wst.data()) << 8);
-      sac_wide_stage<T><<<st.grid + ng, WG_T, std::max(st.lds, ng ? glds : 0), s>>>(
-          e->d, e->wdd, e->wjobs + st.j0, st.j1 - st.j0, flags, st.grid, *rb, next_idx);
+      const bool relu = e->cfg.q_hidden_act == ACT_RELU && e->cfg.pi_hidden_act == ACT_RELU;
+      const int am = e->hostW[st.j0].amode;  // one A-operand mode per stage (build_wide)
+      auto k = relu ? (am == WA_PLAIN ? sac_wide_stage<T, WA_PLAIN, true>
+                       : am == WA_ACT ? sac_wide_stage<T, WA_ACT, true> : sac_wide_stage<T, WA_OUTBWD, true>)
+                    : (am == WA_PLAIN ? sac_wide_stage<T, WA_PLAIN, false>
+                       : am == WA_ACT ? sac_wide_stage<T, WA_ACT, false> : sac_wide_stage<T, WA_OUTBWD, false>);
+      k<<<st.grid + ng, WG_T, std::max(st.lds, ng ? glds : 0), s>>>(e->d, e->wdd, e->wjobs + st.j0, st.j1 - st.j0,
+                                                                    flags, st.grid, *rb, next_idx);
       break;
     }
     case 2:

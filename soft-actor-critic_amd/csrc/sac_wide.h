@@ -36,12 +36,10 @@
 #define WG_T 256   // threads per stage workgroup (4 waves)
 #define WBM 64     // rows per output tile
 #define WBN 64     // columns per output tile
-#define WKB 32     // K per LDS block (fp32: two MFMA chunks of 16; bf16: one of 32)
-#define WLDA 36    // LDS row stride of the A block (floats): conflict-free 16-B fragment reads
 #define WLDE 68    // LDS row stride of the epilogue tile
 #define WLDD 17    // LDS row stride of the per-row seeds (J <= 16)
 #define WJMAX 16
-#define WWS 1088   // floats of the epilogue weight slices (OUTP: Nout x 64; DA: 64 x A)
+#define WWS 1088   // floats of the epilogue weight slices (OUTP: Nout x 64; DA: A x 64)
 
 enum WAMode { WA_PLAIN = 0, WA_ACT = 1, WA_OUTBWD = 2 };
 enum WEMode { WE_FWD = 0, WE_BWD = 1 };
@@ -122,7 +120,9 @@ struct WJob {
   long da_cb;
   void* AGT;   // WA_OUTBWD: the generated operand's dY^T and bias partials (cb == 0 items)
   float* Adbp;
-  int adbp_ld, pad_;
+  int adbp_ld;
+  int p_row0;  // forward: P is stored for rows >= p_row0 only
+  int nbuf;    // K-block buffers in LDS (2..4): nbuf - 1 blocks in flight ahead of the MFMAs
 };
 
 static_assert(sizeof(WJob) <= 448, "extend wide_prefetch");
@@ -355,10 +355,93 @@ __device__ __forceinline__ void wide_rowpro(const AS_C EngineDev& E, const AS_C 
 }
 
 // ---------------------------------------------------------------------------- one GEMM item
+// K is staged through LDS in blocks of WK<T>::KB by LDS-DMA (global_load_lds,
+// 16 B per lane, no register staging): the A block as fragment pieces (16 rows
+// x 4 k per lane group, lane-linear in exactly the order a wave reads one MFMA
+// operand), the B block as the packed weight fragments themselves.  Two
+// buffers, one barrier per block; block kb + 1 lands while block kb is
+// multiplied.  Every wave issues the same number of DMAs per block (a piece
+// past Kp or a column tile past Np re-loads a valid address and is never
+// multiplied), so blocks in flight are counted with vmcnt.
 template <typename T>
+struct WK {
+  static constexpr int KC = MM<T>::KC, KL = MM<T>::KL;
+  static constexpr int KB = sizeof(T) == 4 ? 32 : 64;  // K per block
+  static constexpr int NCH = KB / KC;                   // MFMA chunks per block
+  static constexpr int PR = KB / 16;                    // A pieces per 16-row tile
+  static constexpr int APC = 4 * PR, BPC = 4 * NCH;     // A / B pieces per block
+  static constexpr int ABUF = APC * 256, BUF = ABUF + BPC * 256;  // floats
+  // in-block k of lane group gg's 4 elements in A piece h (fp32: piece = chunk;
+  // bf16: chunk h / 2, elements 4 (h & 1).. of the lane's 8)
+  static __device__ __forceinline__ int koff(int h, int gg) {
+    if constexpr (sizeof(T) == 4) return h * 16 + gg * 4;
+    else return (h >> 1) * 32 + gg * 8 + (h & 1) * 4;
+  }
+  static __device__ __forceinline__ int chunk(int h) { return sizeof(T) == 4 ? h : h >> 1; }
+  // LDS float index of A element (row r, in-block k) in a block image
+  static __device__ __forceinline__ int aloc(int r, int k) {
+    int h, gg;
+    if constexpr (sizeof(T) == 4) {
+      h = k >> 4;
+      gg = (k & 15) >> 2;
+    } else {
+      h = (k >> 5) * 2 + ((k >> 2) & 1);
+      gg = (k & 31) >> 3;
+    }
+    return ((r >> 4) * PR + h) * 256 + (gg * 16 + (r & 15)) * 4 + (k & 3);
+  }
+};
+static_assert(64 * WLDE <= 2 * WK<float>::BUF && 64 * WLDE <= 2 * WK<bf16>::BUF, "epilogue tile aliases the K buffers");
+
+__device__ __forceinline__ void glds16(const AS_G void* g, lf* l) {
+  __builtin_amdgcn_global_load_lds(g, (AS_L void*)l, 16, 0, 0);
+}
+// hidden activation and its derivative; HR: every hidden layer of the stage is ReLU
+template <bool HR>
+__device__ __forceinline__ float hact(int a, float p) {
+  if constexpr (HR) return p > 0.f ? p : 0.f;
+  else return act_fwd(a, p);
+}
+template <bool HR>
+__device__ __forceinline__ float hactb(int a, float p, float g) {
+  if constexpr (HR) return p > 0.f ? g : 0.f;
+  else return act_bwd(a, p, g);
+}
+
+// 64 rows x 64 columns of Et dotted with No weight rows Ws[j][0..64): four
+// threads per row, 16 columns each, reduced by two shuffles; act: apply the
+// hidden activation to Et first (output-layer partials of a forward stage)
+template <bool HR, bool ACTX>
+__device__ __forceinline__ void wide_rowdot(const lf* Et, const lf* Ws, int No, int aact, AS_G float* dst) {
+  const int tid = threadIdx.x, r = tid >> 2, kq = tid & 3;
+  float x[16];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const f32x4 v = *(const AS_L f32x4*)(Et + r * WLDE + kq * 16 + q * 4);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) x[q * 4 + e] = ACTX ? hact<HR>(aact, v[e]) : v[e];
+  }
+  for (int j = 0; j < No; ++j) {
+    float s = 0.f;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const f32x4 w = *(const AS_L f32x4*)(Ws + j * WBN + kq * 16 + q * 4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) s += x[q * 4 + e] * w[e];
+    }
+    s += __shfl_xor(s, 1, 64);
+    s += __shfl_xor(s, 2, 64);
+    if (kq == (j & 3)) dst[(size_t)r * No + j] = s;
+  }
+}
+
+template <typename T, int AM, bool HR>
 __device__ __forceinline__ void wide_item(const AS_C EngineDev& E, const AS_C WideDev& W, const AS_C WJob& jb, int it,
                                           lf* lds, int par, bool wst) {
-  constexpr int KC = MM<T>::KC, KL = MM<T>::KL, NCH = WKB / KC;
+  typedef WK<T> K_;
+  constexpr int KC = K_::KC, KL = K_::KL, KB = K_::KB, NCH = K_::NCH, PR = K_::PR;
+  static_assert(3 * (PR + NCH) < 64, "vmcnt counts blocks in flight");
+  constexpr bool XF = AM == WA_OUTBWD || (AM == WA_ACT && !HR);  // A transformed in place after landing
   typedef typename MM<T>::Frag F;
   const int tid = threadIdx.x, lane = tid & 63, wave = wave_id();
   const int c = lane & 15, g = lane >> 4;
@@ -376,98 +459,177 @@ __device__ __forceinline__ void wide_item(const AS_C EngineDev& E, const AS_C Wi
     cb = it % jb.ncb;
   }
   const int row0 = rb * WBM, col0 = cb * WBN;
+  const int rbase = row0 % W.Brw;  // row r of the block is a batch row iff rbase + r < B
   const int NT = jb.Np >> 4, t0 = col0 >> 4, nchT = jb.tcols / KC;
-  const int Kp = jb.Kp, nkb = Kp / WKB;
-  lf* Ab = lds;                       // [2][64][WLDA] fp32 A blocks
-  lf* Bb = lds + 2 * 64 * WLDA;       // [2][4 tiles][NCH][64 lanes x 16 B] packed B fragments
-  constexpr int BBUF = 4 * NCH * 256;  // floats per B buffer
-  lf* Dl = Bb + 2 * BBUF;             // [64][WLDD] row seeds (WA_OUTBWD)
-  lf* Wol = Dl + 64 * WLDD;           // [J][Kp] output layer weights (WA_OUTBWD)
-  const bool outbwd = jb.amode == WA_OUTBWD;
-  const int J = jb.J;
-  // the epilogue's weight slices (WWS floats): output layer columns of this block
-  // [Nout][64] (OUTP) or layer-0 action columns [64][A] (DA), staged here so the
-  // epilogue's dot products read LDS, not one dependent global load per term
-  lf* Ws = outbwd ? Wol + J * Kp : Dl;
-  if (jb.OUTP) {
+  const int Kp = jb.Kp, nkb = (Kp + KB - 1) / KB;
+  const int NB = jb.nbuf;
+  lf* Ws = lds + NB * K_::BUF;  // the epilogue's weight slices (WWS floats)
+  lf* Dl = Ws + WWS;           // [64][WLDD] row seeds (WA_OUTBWD)
+  lf* Wol = Dl + 64 * WLDD;    // [J][Kp] output layer weights (WA_OUTBWD)
+
+  // ---- LDS-DMA sources: this wave's A pieces wave + 4 i, B pieces wave + 4 i
+  const AS_G float* xa[PR];
+#pragma unroll
+  for (int i = 0; i < PR; ++i) {
+    const int pa = wave + 4 * i, rt = pa / PR, h = pa % PR;
+    xa[i] = GPC(float, jb.X) + (size_t)(row0 + rt * 16 + c) * jb.ldx + K_::koff(h, g);
+  }
+  const AS_G T* wb[NCH];
+  bool bv[NCH];
+#pragma unroll
+  for (int i = 0; i < NCH; ++i) {
+    const int pb = wave + 4 * i, ct = pb / NCH, ch = pb % NCH, t = t0 + ct;
+    bv[i] = t < NT;
+    wb[i] = GPC(T, jb.Wp) + ((size_t)((bv[i] ? t : 0) * nchT + ch) * 64 + lane) * KL;
+  }
+  auto issue = [&](int kb, int buf) __attribute__((always_inline)) {
+    lf* Aq = lds + buf * K_::BUF;
+    lf* Bq = Aq + K_::ABUF;
+    const int k0 = kb * KB;
+#pragma unroll
+    for (int i = 0; i < PR; ++i) {
+      const int pa = wave + 4 * i, h = pa % PR;
+      const bool v = k0 + K_::chunk(h) * KC < Kp;
+      glds16(xa[i] + (v ? k0 : -K_::koff(h, g)), Aq + pa * 256);  // past Kp: the row's first 4 k
+    }
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) {
+      const int pb = wave + 4 * i;
+      const bool v = k0 + (pb % NCH) * KC < Kp;
+      glds16(wb[i] + (v ? (size_t)kb * NCH * 64 * KL : 0), Bq + pb * 256);
+    }
+  };
+  constexpr int CNT = PR + NCH;  // DMAs per wave per block
+  // wait until this wave's DMAs of the block `ahead` blocks older than the
+  // newest issued one have landed (vmcnt retires in issue order)
+  auto wait_ahead = [&](int ahead) __attribute__((always_inline)) {
+    if (ahead <= 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else if (ahead == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(CNT) : "memory");
+    else if (ahead == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * CNT) : "memory");
+    else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * CNT) : "memory");
+  };
+  // a workgroup barrier that does not drain the DMAs in flight (__syncthreads
+  // would wait vmcnt(0)): LDS traffic retired, then s_barrier
+  auto bar = [&]() __attribute__((always_inline)) { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
+  // the output layer's weight slice [Nout][64] by DMA when the block's 64
+  // columns are all inside the rows (issued first: retired by the first wait)
+  const bool ws_dma = jb.OUTP && col0 + WBN <= jb.N && (jb.ldwout & 3) == 0 && ((uintptr_t)jb.Wout & 15) == 0;
+  if (ws_dma) {
+    const int j = 4 * wave + (lane >> 4);  // wave w: rows q0 + 4w..4w+3, 16 lanes x 16 B per row
+    for (int q0 = 0; q0 < jb.Nout; q0 += 16)
+      if (q0 + j < jb.Nout)
+        glds16(GPC(float, jb.Wout) + (size_t)(q0 + j) * jb.ldwout + col0 + (lane & 15) * 4, Ws + (q0 + 4 * wave) * WBN);
+  }
+  for (int b = 0; b < NB && b < nkb; ++b) issue(b, b);
+
+  // ---- prologue (under the first two blocks' DMA)
+  const bool fwd = jb.emode == WE_FWD;
+  float bias_r[2];
+#pragma unroll
+  for (int ct = 0; ct < 2; ++ct) {
+    const int n = col0 + wc * 32 + ct * 16 + c;
+    bias_r[ct] = (fwd && n < jb.N) ? GPC(float, jb.bias)[n] : 0.f;
+  }
+  // the epilogue's weight slices, row-major [j][64 columns of this block]:
+  // output layer columns (OUTP) or the critics' layer-0 action columns (DA)
+  if (jb.OUTP && !ws_dma) {
     for (int i = tid; i < jb.Nout * WBN; i += WG_T) {
       const int j = i / WBN, k = i % WBN;
       Ws[i] = col0 + k < jb.N ? GPC(float, jb.Wout)[(size_t)j * jb.ldwout + col0 + k] : 0.f;
     }
   } else if (jb.DA) {
-    for (int i = tid; i < WBN * W.A; i += WG_T) {
-      const int k = i / W.A, j = i % W.A;
+    for (int i = tid; i < W.A * WBN; i += WG_T) {
+      const int j = i / WBN, k = i % WBN;
       Ws[i] = col0 + k < jb.N ? GPC(float, jb.W0a)[(size_t)(col0 + k) * jb.ldw0 + jb.a_off + j] : 0.f;
     }
   }
-
-  if (outbwd) {
+  // XF pass mapping: a thread transforms lanes pL, pL + 1 of the pieces of
+  // row tile prt with h = (tid >> 7) + 2 i (its two rows are fixed)
+  const int prt = (tid >> 5) & 3, pL = (tid & 31) * 2, pg = pL >> 4;
+  const int J = jb.J;
+  const int rA = prt * 16 + (pL & 15);  // the pass's two rows rA, rA + 1
+  if constexpr (AM == WA_OUTBWD) {
     wide_rowpro<T>(E, W, jb, row0, cb, par, Dl);
     for (int i = tid; i < J * Kp; i += WG_T) {
       const int j = i / Kp, k = i % Kp;
       Wol[i] = k < jb.ldwo ? GPC(float, jb.Wo)[(size_t)j * jb.ldwo + k] : 0.f;
     }
-    __syncthreads();
+    // (the loop's first barrier orders Dl / Wol before the first pass)
   }
-
-  // K blocks staged two ahead: two register sets, R0 for even blocks, R1 for odd
-  struct Regs {
-    f32x4 a[2];
-    u32x4 b[NCH];
-  };
-  Regs R0, R1;
-  auto load = [&](int kb, Regs& R) __attribute__((always_inline)) {
-    const int k0 = kb * WKB;
+  auto xform = [&](int kb, int buf) __attribute__((always_inline)) {
+    lf* Aq = lds + buf * K_::BUF;
+    const int k0 = kb * KB;
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int p = tid + WG_T * u, row = p >> 3, kq = p & 7;
-      R.a[u] = *(const AS_G f32x4*)(GPC(float, jb.X) + (size_t)(row0 + row) * jb.ldx + k0 + 4 * kq);
-    }
-#pragma unroll
-    for (int v = 0; v < NCH; ++v) {
-      const int pb = tid + WG_T * v, ct = pb / (64 * NCH), rest = pb % (64 * NCH), ch = rest >> 6, ln = rest & 63;
-      const int t = t0 + ct;
-      R.b[v] = t < NT ? *(const AS_G u32x4*)(GPC(T, jb.Wp) + ((size_t)(t * nchT + kb * NCH + ch) * 64 + ln) * KL)
-                      : u32x4{0u, 0u, 0u, 0u};
-    }
-  };
-  auto store = [&](int kb, int buf, const Regs& R) __attribute__((always_inline)) {
-    const int k0 = kb * WKB;
-    lf* Aq = Ab + buf * 64 * WLDA;
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int p = tid + WG_T * u, row = p >> 3, kq = p & 7;
-      f32x4 v = R.a[u];
-      if (jb.amode == WA_ACT) {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = act_fwd(jb.aact, v[e]);
-      } else if (outbwd) {
+    for (int i = 0; i < PR / 2; ++i) {
+      const int h = (tid >> 7) + 2 * i;
+      if (k0 + K_::chunk(h) * KC >= Kp) continue;
+      AS_L f32x4* q = (AS_L f32x4*)(Aq + (prt * PR + h) * 256 + pL * 4);
+      f32x4 a = q[0], b = q[1];
+      if constexpr (AM == WA_OUTBWD) {
+        // dY[r][k] = act'(P[r][k]) * sum_j D[r][j] Wout[j][k]
+        const int k = k0 + K_::koff(h, pg);
+        f32x4 sa = {0.f, 0.f, 0.f, 0.f}, sb = {0.f, 0.f, 0.f, 0.f};
+        for (int j = 0; j < J; ++j) {
+          const f32x4 w = *(const AS_L f32x4*)(Wol + j * Kp + k);
+          sa += Dl[rA * WLDD + j] * w;
+          sb += Dl[(rA + 1) * WLDD + j] * w;
+        }
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          const int k = k0 + 4 * kq + e;
-          float s = 0.f;
-          for (int j = 0; j < J; ++j) s += Dl[row * WLDD + j] * Wol[j * Kp + k];
-          v[e] = act_bwd(jb.aact, v[e], s);
+          a[e] = hactb<HR>(jb.aact, a[e], sa[e]);
+          b[e] = hactb<HR>(jb.aact, b[e], sb[e]);
+        }
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          a[e] = act_fwd(jb.aact, a[e]);
+          b[e] = act_fwd(jb.aact, b[e]);
         }
       }
-      *(AS_L f32x4*)(Aq + row * WLDA + 4 * kq) = v;
+      q[0] = a;
+      q[1] = b;
     }
-    lf* Bq = Bb + buf * BBUF;
-#pragma unroll
-    for (int v = 0; v < NCH; ++v) *(AS_L u32x4*)(Bq + (tid + WG_T * v) * 4) = R.b[v];
   };
+
   f32x4 acc[2][2];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  auto comp = [&](int buf) __attribute__((always_inline)) {
-    const lf* Aq = Ab + buf * 64 * WLDA;
-    const lf* Bq = Bb + buf * BBUF;
+  auto afrag = [&](const lf* Aq, int rt, int ch) __attribute__((always_inline)) -> F {
+    constexpr bool RL = AM == WA_ACT && HR;  // ReLU applied as the fragment is read
+    if constexpr (sizeof(T) == 4) {
+      f32x4 v = *(const AS_L f32x4*)(Aq + (rt * PR + ch) * 256 + lane * 4);
+      if constexpr (RL)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = v[e] > 0.f ? v[e] : 0.f;
+      return v;
+    } else {
+      f32x4 u = *(const AS_L f32x4*)(Aq + (rt * PR + ch * 2) * 256 + lane * 4);
+      f32x4 v = *(const AS_L f32x4*)(Aq + (rt * PR + ch * 2 + 1) * 256 + lane * 4);
+      if constexpr (RL)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          u[e] = u[e] > 0.f ? u[e] : 0.f;
+          v[e] = v[e] > 0.f ? v[e] : 0.f;
+        }
+      F f;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        f[e] = (bf16)u[e];
+        f[4 + e] = (bf16)v[e];
+      }
+      return f;
+    }
+  };
+  auto comp = [&](int buf, int nc) __attribute__((always_inline)) {
+    const lf* Aq = lds + buf * K_::BUF;
+    const lf* Bq = Aq + K_::ABUF;
 #pragma unroll
     for (int ch = 0; ch < NCH; ++ch) {
-      const F a0 = MM<T>::from_lds(Aq + (wr * 32 + c) * WLDA + ch * KC + g * KL);
-      const F a1 = MM<T>::from_lds(Aq + (wr * 32 + 16 + c) * WLDA + ch * KC + g * KL);
+      if (ch >= nc) break;
+      const F a0 = afrag(Aq, wr * 2, ch);
+      const F a1 = afrag(Aq, wr * 2 + 1, ch);
       const F b0 = *(const AS_L F*)(Bq + ((wc * 2 + 0) * NCH + ch) * 256 + lane * 4);
       const F b1 = *(const AS_L F*)(Bq + ((wc * 2 + 1) * NCH + ch) * 256 + lane * 4);
       MM<T>::mma(acc[0][0], a0, b0);
@@ -476,63 +638,53 @@ __device__ __forceinline__ void wide_item(const AS_C EngineDev& E, const AS_C Wi
       MM<T>::mma(acc[1][1], a1, b1);
     }
   };
-  // the generated operand's dY^T + bias partials (WA_OUTBWD, cb == 0): block kb from LDS
-  const bool agt = outbwd && jb.AGT && cb == 0;
-  auto agt_store = [&](int kb, int buf) __attribute__((always_inline)) {
-    const int k0 = kb * WKB;
-    const lf* Aq = Ab + buf * 64 * WLDA;
+  // the generated operand's dY^T + bias partials (WA_OUTBWD, cb == 0 items): from the transformed block
+  // (spread over the row block's items: item cb stores the K blocks kb = cb mod ncb)
+  const bool agt = AM == WA_OUTBWD && jb.AGT;
+  auto agt_store = [&](int kb, int buf, int nk) __attribute__((always_inline)) {
+    const int k0 = kb * KB;
+    const lf* Aq = lds + buf * K_::BUF;
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
+    for (int u = 0; u < KB / 16; ++u) {
       const int p = tid + WG_T * u, k = p >> 4, q = p & 15;  // column k0 + k, rows 4q..4q+3
       const int b0 = row0 + 4 * q;
-      if (b0 < W.Bp) {
+      if (b0 < W.Bp && k < nk) {
         f32x4 v;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = Aq[(4 * q + e) * WLDA + k];
+        for (int e = 0; e < 4; ++e) v[e] = Aq[K_::aloc(4 * q + e, k)];
         st4<T>(jb.AGT, (size_t)(k0 + k) * W.Bp + b0, v);
       }
     }
-    if (tid < 4 * WKB) {
-      const int rt = tid / WKB, k = tid % WKB, grt = row0 / 16 + rt;
+    if (tid < 4 * KB) {
+      const int rt = tid / KB, k = tid % KB, grt = row0 / 16 + rt;
       float s = 0.f;
-      for (int r = 0; r < 16; ++r) s += Aq[(rt * 16 + r) * WLDA + k];
-      if (grt < W.nrt && k0 + k < jb.adbp_ld) GP(float, jb.Adbp)[(size_t)grt * jb.adbp_ld + k0 + k] = s;
+      for (int r = 0; r < 16; ++r) s += Aq[K_::aloc(rt * 16 + r, k)];
+      if (grt < W.nrt && k < nk && k0 + k < jb.adbp_ld) GP(float, jb.Adbp)[(size_t)grt * jb.adbp_ld + k0 + k] = s;
     }
   };
 
-  // the epilogue's biases, loaded before the K loop (their latency hides under it)
-  const bool fwd = jb.emode == WE_FWD;
-  float bias_r[2];
-#pragma unroll
-  for (int ct = 0; ct < 2; ++ct) {
-    const int n = col0 + wc * 32 + ct * 16 + c;
-    bias_r[ct] = (fwd && n < jb.N) ? GPC(float, jb.bias)[n] : 0.f;
-  }
   WSTAMP(1);
-  // block kb is loaded into registers two iterations before it is stored to
-  // LDS (its loads have two blocks of MFMAs to land), stored one iteration
-  // before it is computed (one barrier per block)
-  load(0, R0);
-  if (nkb > 1) load(1, R1);
-  store(0, 0, R0);
-  __syncthreads();
-  WSTAMP(2);
-  auto iter = [&](int kb, Regs& Rnext2, const Regs& Rnext1) __attribute__((always_inline)) {
-    const int cur = kb & 1;
-    if (kb + 2 < nkb) load(kb + 2, Rnext2);
-    if (agt) agt_store(kb, cur);
-    comp(cur);
-    if (kb + 1 < nkb) store(kb + 1, cur ^ 1, Rnext1);
-    __syncthreads();
-    if (kb < 8) WSTAMP(3 + kb);
-  };
-  for (int kb = 0; kb < nkb; kb += 2) {  // unrolled by two: the register sets stay static
-    iter(kb, R0, R1);
-    if (kb + 1 < nkb) iter(kb + 1, R1, R0);
+  int cur = 0;
+  for (int kb = 0; kb < nkb; ++kb) {
+    const int nc = min(NCH, (Kp - kb * KB) / KC);
+    // newest block issued so far: NB - 1 at kb = 0, then kb + NB - 2
+    const int last = min(nkb - 1, kb == 0 ? NB - 1 : kb + NB - 2);
+    wait_ahead(last - kb);  // this wave's pieces of block kb have landed
+    bar();                  // ... and every wave's; block kb - 1 is consumed
+    if constexpr (XF) {
+      xform(kb, cur);
+      bar();
+    }
+    if (kb >= 1 && kb + NB - 1 < nkb) issue(kb + NB - 1, cur == 0 ? NB - 1 : cur - 1);  // block kb - 1's buffer
+    if (kb < 8) WSTAMP(2 + kb);
+    if (agt && kb % jb.ncb == cb) agt_store(kb, cur, nc * KC);
+    comp(cur, nc);
+    cur = cur + 1 == NB ? 0 : cur + 1;
   }
   WSTAMP(11);
+  __syncthreads();  // the epilogue tile aliases the K buffers (no DMA in flight)
 
-  // ---- epilogue through an LDS tile [64][WLDE] (aliases the K-loop buffers)
+  // ---- epilogue through an LDS tile [64][WLDE]
   lf* Et = lds;
 #pragma unroll
   for (int rt = 0; rt < 2; ++rt)
@@ -543,7 +695,7 @@ __device__ __forceinline__ void wide_item(const AS_C EngineDev& E, const AS_C Wi
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int r = wr * 32 + rt * 16 + 4 * g + i;
-        const bool ok = n < jb.N && row0 + r < jb.M && wrow_ok(W, row0 + r);
+        const bool ok = n < jb.N && rbase + r < W.B;
         Et[r * WLDE + cl] = ok ? acc[rt][ct][i] + bn : 0.f;
       }
     }
@@ -558,7 +710,7 @@ __device__ __forceinline__ void wide_item(const AS_C EngineDev& E, const AS_C Wi
         if (jb.pact >= 0) {
           const f32x4 pp = *(const AS_G f32x4*)(GPC(float, jb.Pprev) + (size_t)(row0 + r) * jb.ldpp + k);
 #pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] = act_bwd(jb.pact, pp[e], v[e]);
+          for (int e = 0; e < 4; ++e) v[e] = hactb<HR>(jb.pact, pp[e], v[e]);
           *(AS_L f32x4*)(Et + r * WLDE + 4 * q) = v;
         }
         if (jb.DY) *(AS_G f32x4*)(GP(float, jb.DY) + (size_t)(row0 + r) * jb.lddy + k) = v;
@@ -584,18 +736,12 @@ __device__ __forceinline__ void wide_item(const AS_C EngineDev& E, const AS_C Wi
       for (int r = 0; r < 16; ++r) s += Et[(rt * 16 + r) * WLDE + k];
       if (grt < W.nrt && col0 + k < jb.N) GP(float, jb.dbp)[(size_t)grt * jb.dbp_ld + col0 + k] = s;
     }
-    if (jb.DA) {  // d a~ partials: sum over this block's hidden units of dY0[r][n] W0[n][O + j]
-      for (int i = tid; i < 64 * W.A; i += WG_T) {
-        const int r = i / W.A, j = i % W.A;
-        float s = 0.f;
-        for (int k = 0; k < WBN; ++k) s += Et[r * WLDE + k] * Ws[k * W.A + j];
-        GP(float, jb.DA)[cb * jb.da_cb + (size_t)(row0 + r) * W.A + j] = s;
-      }
-    }
+    // d a~ partials: sum over this block's hidden units of dY0[r][n] W0[n][O + j]
+    if (jb.DA) wide_rowdot<HR, false>(Et, Ws, W.A, 0, GP(float, jb.DA) + cb * jb.da_cb + (size_t)row0 * W.A);
     return;
   }
-  // forward: pre-activation rows, act(P)^T stash, output-layer partials
-  if (jb.P) {
+  // forward: pre-activation rows (rows >= p_row0), act(P)^T stash, output-layer partials
+  if (jb.P && row0 >= jb.p_row0) {
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int p = tid + WG_T * u, r = p >> 4, q = p & 15;
@@ -610,20 +756,13 @@ __device__ __forceinline__ void wide_item(const AS_C EngineDev& E, const AS_C Wi
       if (col0 + n < jb.Np && b0 < W.Bp) {
         f32x4 v;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = act_fwd(jb.oact, Et[(4 * q + e) * WLDE + n]);
+        for (int e = 0; e < 4; ++e) v[e] = hact<HR>(jb.oact, Et[(4 * q + e) * WLDE + n]);
         st4<T>(jb.XT, (size_t)par * jb.xt_par + (size_t)(col0 + n) * jb.xt_ld + b0, v);
       }
     }
   }
-  if (jb.OUTP) {
-    const int No = jb.Nout;
-    for (int i = tid; i < 64 * No; i += WG_T) {
-      const int r = i / No, j = i % No;
-      float s = 0.f;
-      for (int k = 0; k < WBN; ++k) s += Ws[j * WBN + k] * act_fwd(jb.oact, Et[r * WLDE + k]);
-      GP(float, jb.OUTP)[cb * jb.outp_cb + (size_t)(row0 + r) * No + j] = s;
-    }
-  }
+  if (jb.OUTP)
+    wide_rowdot<HR, true>(Et, Ws, jb.Nout, jb.oact, GP(float, jb.OUTP) + cb * jb.outp_cb + (size_t)row0 * jb.Nout);
 }
 
 // ---------------------------------------------------------------------------- gather
@@ -842,8 +981,10 @@ __global__ void __launch_bounds__(WG_T) sac_wide_head(const EngineDev* __restric
 // flags: bit 0 = the step's last launch before phase D (advances the step),
 // bit 1 = the step's first GEMM stage (block 0 derives the step's Adam scalars),
 // bit 2 = blocks [nitems, grid) gather the next step's batch; bits 8.. = the
-// stage's index in the step (stamps builds)
-template <typename T>
+// stage's index in the step (stamps builds).  AM: the A-operand mode of every
+// job of the stage; HR: both networks' hidden activation is ReLU (applied and
+// differentiated inline, no switch).
+template <typename T, int AM, bool HR>
 __global__ void __launch_bounds__(WG_T, 4) sac_wide_stage(const EngineDev* __restrict__ Ep, const WideDev* __restrict__ Wd,
                                                        const WJob* __restrict__ jobs, int njobs, int flags, int nitems,
                                                        sac_replay rb, const int32_t* __restrict__ next_idx) {
@@ -867,7 +1008,8 @@ __global__ void __launch_bounds__(WG_T, 4) sac_wide_stage(const EngineDev* __res
   const AS_C WJob& jb = ((const AS_C WJob*)jobs)[j];
   wide_prefetch(jobs + j, Wd);
   const int par = (int)(*GPC(uint64_t, W.rng_step) & 1);
-  wide_item<T>(E, W, jb, (int)blockIdx.x - jb.item0, (lf*)lds_raw, par, wst);
+  const int it = (int)blockIdx.x - jb.item0;
+  wide_item<T, AM, HR>(E, W, jb, it, (lf*)lds_raw, par, wst);
 #ifdef SAC_STAMPS
   if (wst) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

@@ -249,7 +249,7 @@ def test_role_split_equals_fused(precision, monkeypatch):
 
 def test_large_batch_uses_fused_kernels_and_runs(monkeypatch):
     """C3 (B=4096): 256 row tiles do not fit the role split; the one-block-per-
-    row-tile kernels run (SAC_WIDE=0; the default is the stage path)."""
+    row-tile kernels run (C3's default; SAC_WIDE=0 also refuses the stage path)."""
     monkeypatch.setenv("SAC_WIDE", "0")
     eng, rb, c = _engine("c3", "bf16", capacity=20_000)
     assert not eng.roles and not eng.wide
@@ -558,11 +558,13 @@ def test_fused_step_equals_four_launches(lib, cfg, precision, monkeypatch):
 
 
 @pytest.mark.parametrize("precision", ["fp32", "bf16"])
-def test_stage_path_staged_batches_equal_fresh_gathers(precision):
-    """The stage path (csrc/sac_wide.h) gathers step t+1's batch inside step t's
-    last phase-C launch; the first step of every call gathers its own.  So one
-    call of 5 steps (device RNG) must equal 5 calls of one step, bit for bit,
-    and the same with injected indices; graph replay equals eager launches."""
+def test_stage_path_staged_batches_equal_fresh_gathers(precision, monkeypatch):
+    """The stage path (csrc/sac_wide.h, forced at C3 by SAC_WIDE=1) gathers step
+    t+1's batch inside step t's last phase-C launch; the first step of every
+    call gathers its own.  So one call of 5 steps (device RNG) must equal 5
+    calls of one step, bit for bit, and the same with injected indices; graph
+    replay equals eager launches."""
+    monkeypatch.setenv("SAC_WIDE", "1")
     out = {}
     for mode in ("one_call", "per_step", "graph"):
         eng, rb, c = _engine("c3", precision, capacity=12_000)

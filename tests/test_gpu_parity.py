@@ -86,6 +86,15 @@ def test_c3_batch_part_counts_match_oracle(precision, parts, monkeypatch):
     test_baseline_config_matches_oracle("c3", 12_288, 2, precision)
 
 
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_c3_stage_path_matches_oracle(precision, monkeypatch):
+    """C3 through the layer-synchronous stage path (SAC_WIDE=1; the row-tile
+    kernels are C3's default), against the oracle like
+    test_baseline_config_matches_oracle."""
+    monkeypatch.setenv("SAC_WIDE", "1")
+    test_baseline_config_matches_oracle("c3", 12_288, 2, precision)
+
+
 @pytest.mark.parametrize("name", ["c1_auto", "c2"])
 def test_engine_matches_reference_golden_directly(name):
     """Step 1 against the reference's own captured outputs (no oracle in between)."""
@@ -157,21 +166,32 @@ EDGE_SHAPES = {
 
 @pytest.mark.parametrize("precision", ["fp32", "bf16"])
 @pytest.mark.parametrize("shape", sorted(EDGE_SHAPES))
-def test_edge_shapes_match_oracle(shape, precision):
+def test_edge_shapes_match_oracle(shape, precision, monkeypatch):
     """Ragged and extreme shapes against the oracle, with the same checks and
     tolerances as the BASELINE configs (parity unpinned by the reference at
-    these shapes; the oracle is pinned by the 8 reference fixtures)."""
+    these shapes; the oracle is pinned by the 8 reference fixtures).
+    wide_deep_b1100 runs the stage path (forced: the row-tile kernels fit it)."""
+    if shape == "wide_deep_b1100":
+        monkeypatch.setenv("SAC_WIDE", "1")
     c = dict(EDGE_SHAPES[shape], name=shape)
     # y / log pi against the oracle's trajectory after step 1: 2e-3 at these
     # shapes (measured 6.1e-4 at obs 256, step 3: Adam sign flips of ~0 gradients)
     _check_config_against_oracle(c, precision, 2 if c["batch"] > 1024 else 3, traj_tol=2e-3)
 
 
+# shapes the phase kernels fit: the stage path runs them only when forced (SAC_WIDE=1)
+STAGE_FORCED = {"wide_deep_b1100", "rowtile_b4001"}
+
+
 @pytest.mark.parametrize("shape", ["obs300", "wide400_300", "wide512_b384", "wide_deep_b1100", "rowtile_b4001"])
-def test_stage_path_is_used_where_the_phase_kernels_do_not_fit(shape):
-    """Shapes past the phase kernels' LDS layout, and batches past the role
-    split, run the layer-synchronous stage path (no fallback, no refusal)."""
+def test_stage_path_is_used_where_the_phase_kernels_do_not_fit(shape, monkeypatch):
+    """Shapes past the phase kernels' LDS layout run the layer-synchronous stage
+    path (no fallback, no refusal); batches past the role split run it when
+    SAC_WIDE=1 forces it."""
     import bench
+
+    if shape in STAGE_FORCED:
+        monkeypatch.setenv("SAC_WIDE", "1")
 
     bench.CONFIGS["_stage"] = dict(EDGE_SHAPES[shape])
     try:
@@ -321,7 +341,7 @@ def _oracle_state_from_engine(eng, act):
                       opt_alpha_v=float(al[3]), opt_alpha_step=float(steps[3]))
 
 
-@pytest.mark.parametrize("shape", ["c2_split", "c4", "roles_b384", "rowtile_b2000", "rowtile_b2000_wide0",
+@pytest.mark.parametrize("shape", ["c2_split", "c4", "roles_b384", "rowtile_b2000", "stage_b2000",
                                    "wide512_b384", "wide400_300"])
 def test_one_step_from_the_engine_state(shape, monkeypatch):
     """Per-step parity without trajectory drift (fp32): before every step the
@@ -338,13 +358,13 @@ def test_one_step_from_the_engine_state(shape, monkeypatch):
          "c4": dict(obs=32, act=2, hidden=[256, 256], batch=256, capacity=2048),
          "roles_b384": dict(obs=24, act=4, hidden=[256, 256], batch=384, capacity=2048),
          "rowtile_b2000": dict(obs=17, act=6, hidden=[128, 128], batch=2000, capacity=4096),
-         "rowtile_b2000_wide0": dict(obs=17, act=6, hidden=[128, 128], batch=2000, capacity=4096),
+         "stage_b2000": dict(obs=17, act=6, hidden=[128, 128], batch=2000, capacity=4096),
          "wide512_b384": dict(obs=24, act=4, hidden=[512, 512], batch=384, capacity=2048),
          "wide400_300": dict(obs=17, act=6, hidden=[400, 300], batch=256, capacity=2048)}[shape]
     if shape == "roles_b384":
         monkeypatch.setenv("SAC_SPLIT", "0")
-    if shape == "rowtile_b2000_wide0":
-        monkeypatch.setenv("SAC_WIDE", "0")  # the one-block-per-row-tile kernels
+    if shape == "stage_b2000":
+        monkeypatch.setenv("SAC_WIDE", "1")  # the stage path (the row-tile kernels fit B = 2000)
     bench.CONFIGS["_local"] = c
     try:
         eng, rb, cc = bench.build_engine("_local", "fp32", 3, torch.device("cuda", 0))
