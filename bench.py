@@ -224,6 +224,15 @@ def bf16_deviation(cfgname, seed, device, steps=3):
             "losses": ["L_Q1", "L_Q2", "L_pi (floor mean|y|)", "L_alpha"]}
 
 
+def short_kernel(name):
+    """The phase-kernel family of a kernel name (tools/pmc_summary.short: the
+    split and stage variants count under their phase's family)."""
+    for k in ("sac_target_critic", "sac_critic_update", "sac_actor_update", "sac_actor", "sac_wide_stage"):
+        if k in name:
+            return k
+    return name
+
+
 def pmc_traffic(kernel, config, precision):
     """HBM-side bytes per launch of `kernel` from the newest committed PMC
     summary for this (config, precision) (profiles/<round>_pmc*.json, written
@@ -497,6 +506,22 @@ def run_rank(args, world, rank, local):
         dist.destroy_process_group()
 
 
+def mfma_busy(kernel, config, precision):
+    """Counter-based MFMA-busy fraction of `kernel` (SQ_VALU_MFMA_BUSY_CYCLES over
+    the launch's SIMD cycles) from the newest committed profiles/<round>_mfma_busy.json
+    (tools/sq_summary.py), or (None, None)."""
+    import glob
+
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_mfma_busy.json")), reverse=True):
+        with open(path) as f:
+            d = json.load(f)
+        for key in (f"{config}_{precision}/{kernel}", f"sq_{config}_{precision}/{kernel}"):
+            k = d.get("kernels", {}).get(key)
+            if k and "mfma_busy_frac" in k:
+                return k["mfma_busy_frac"], os.path.relpath(path, ROOT)
+    return None, None
+
+
 def measure_phases(args, eng, rb, c, elapsed, sps_one):
     """Per-phase device time (hipEvents on the launch stream) and the roofline
     of the dominant kernel.  Each interval also holds the cost of the event
@@ -519,10 +544,24 @@ def measure_phases(args, eng, rb, c, elapsed, sps_one):
         if eng.fused == 2:
             flops = [flops[0], 0, flops[2] + flops[1], 0]
     dom = int(np.argmax(phase_ms))
-    kname = E.load_library().sac_phase_kernel_name(dom).decode()
+    lib = E.load_library()
+    kname = lib.sac_phase_kernel_name(dom).decode()
     traffic, traffic_src = pmc_traffic(kname, args.config, args.precision)
     achieved = flops[dom] / (kern_ms[dom] * 1e-3) / 1e12
     peak = PEAK_TFLOPS[args.precision]
+    # phases A and C (the two heaviest launches) side by side: FLOP fraction of
+    # the dtype's dense peak over the event-timed launch, and the SQ counters'
+    # MFMA-busy fraction of the same kernel (committed counter file)
+    phases = {}
+    for i, ph in ((0, "A"), (2, "C")):
+        if kern_ms[i] <= 0:
+            continue
+        kn = lib.sac_phase_kernel_name(i).decode()
+        busy, busy_src = mfma_busy(short_kernel(kn), args.config, args.precision)
+        a = flops[i] / (kern_ms[i] * 1e-3) / 1e12
+        phases[ph] = {"kernel": kn, "flops_per_launch": flops[i], "avg_launch_ms": round(kern_ms[i], 5),
+                      "achieved": round(a, 3), "frac": round(a / peak, 5), "counter_mfma_busy_frac": busy,
+                      "counter_source": busy_src}
     W = 2 * c["obs"] + c["act"] + 2
     return {
         "replay_sample_GBps_in_step": round(sps_one * c["batch"] * W * 4 / 1e9, 4),
@@ -538,6 +577,7 @@ def measure_phases(args, eng, rb, c, elapsed, sps_one):
                      "timing": "hipEvents after every launch on the launch stream over 100 steps; "
                                "avg_launch_ms = mean interval of this kernel's launches minus the per-launch "
                                "event cost (event intervals of a step - event-free graph step time, per launch)"},
+        "roofline_phases": phases,
         "step_roofline": {"achieved_TFLOPs": round(f_total * sps_one / 1e12, 3), "peak": peak,
                           "frac": round(f_total * sps_one / 1e12 / peak, 5),
                           "note": "SURVEY F_alg per step x steps/s of one learner"},

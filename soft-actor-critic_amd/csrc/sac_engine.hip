@@ -304,7 +304,8 @@ static int fail(int code, const std::string& msg) {
 // Workspace offsets of the large-batch stage path (sac_wide.h), from plan()
 struct WideLay {
   int on = 0, Brw = 0, hp = 0, hq = 0;
-  size_t o_dev = 0, o_jobs = 0;
+  int flow = 0;  // the flow kernel (one persistent launch per phase A / C)
+  size_t o_dev = 0, o_jobs = 0, o_cnt = 0;
   size_t o_xpi0 = 0, o_xq0 = 0, o_xqt0 = 0, o_xc0 = 0, o_r = 0, o_d = 0, o_lp2 = 0, o_piop = 0;
   size_t o_outpi = 0, o_outq[2] = {0, 0}, o_outqt[2] = {0, 0}, o_outc[2] = {0, 0}, o_da[2] = {0, 0};
   size_t o_P[5][SAC_DEV_LAYERS] = {};      // phase A pre-activations (pi on [s'; s], Q1, Q2, Q1t, Q2t)
@@ -339,9 +340,10 @@ struct sac_engine {
   WJob* wjobs = nullptr;
   std::vector<WJob> hostW;
   struct WStage {
-    int kind;   // 0 gather, 1 GEMM jobs [j0, j1), 2 pi heads, 3 phase B, 4 phase D
-    int j0, j1, grid, phase, last;
+    int kind;   // 0 gather, 1 GEMM jobs [j0, j1), 2 pi heads, 3 phase B, 4 phase D, 5 flow launch of jobs [j0, j1)
+    int j0, j1, grid, phase, last;  // grid: workgroups (kind 5: items)
     size_t lds;
+    int G;      // kind 5: resident workgroups launched (create())
   };
   std::vector<WStage> wst;
   // graph cache
@@ -439,6 +441,7 @@ static void build_wide(sac_engine* e, char* base) {
   W.GTpi_out = np.l[hp].GT;
   W.dbppi_out = np.l[hp].dbp;
   W.rng_step = e->buf.rng_step;
+  W.cnt = (uint32_t*)(base + wl.o_cnt);
   W.stamp_stage = -1;
   if (const char* v = getenv("SAC_WIDE_STAMP_STAGE")) W.stamp_stage = atoi(v);
   e->wdd = (WideDev*)(base + wl.o_dev);
@@ -446,6 +449,10 @@ static void build_wide(sac_engine* e, char* base) {
   std::vector<WJob>& JB = e->hostW;
   JB.clear();
   e->wst.clear();
+  struct JTag {
+    int kind, ni, d, phase;  // kind 0 forward, 1 backward, 2 pi heads, 3 gather
+  };
+  std::vector<JTag> tags;  // one per job of JB, in order
   // the two K-block buffers + the epilogue's weight slices (WWS floats); WA_OUTBWD
   // adds the row seeds and the output layer's weights
   // K-block buffers: as many (2..4) as keep the stage's workgroups co-resident
@@ -470,8 +477,9 @@ static void build_wide(sac_engine* e, char* base) {
         break;
       }
     for (WJob& j : js) j.nbuf = nb;
+    for (size_t k = tags.size() - js.size(); k < tags.size(); ++k) tags[k].phase = phase;
     const size_t lf = nb * kbuf + extra;
-    sac_engine::WStage st{1, (int)JB.size(), (int)(JB.size() + js.size()), item, phase, last, lf * 4};
+    sac_engine::WStage st{1, (int)JB.size(), (int)(JB.size() + js.size()), item, phase, last, lf * 4, 0};
     e->wst.push_back(st);
     JB.insert(JB.end(), js.begin(), js.end());
   };
@@ -481,6 +489,7 @@ static void build_wide(sac_engine* e, char* base) {
     const LayerDev& ly = nd.l[l];
     WJob j;
     memset(&j, 0, sizeof(j));
+    tags.push_back(JTag{0, ni, l, -1});
     j.M = M;
     j.K = ly.K;
     j.Kp = ly.Kp;
@@ -524,6 +533,7 @@ static void build_wide(sac_engine* e, char* base) {
     const LayerDev& lo = nd.l[nd.L - 1];
     WJob j;
     memset(&j, 0, sizeof(j));
+    tags.push_back(JTag{1, ni, d, -1});
     j.M = M;
     j.K = ly.N;
     j.Kp = ly.Np;
@@ -570,7 +580,7 @@ static void build_wide(sac_engine* e, char* base) {
     return j;
   };
   auto add = [&](int kind, int grid, int phase) {
-    sac_engine::WStage st{kind, 0, 0, grid, phase, 0, 0};
+    sac_engine::WStage st{kind, 0, 0, grid, phase, 0, 0, 0};
     e->wst.push_back(st);
   };
   // ---- phase A
@@ -639,6 +649,105 @@ static void build_wide(sac_engine* e, char* base) {
     stage_gemm(js, 2, d == 1);
   }
   add(4, 0, 3);  // phase D
+  if (!wl.flow) return;
+
+  // ---- flow launches (sac_wide_flow): phase A's gather row blocks, GEMM items
+  // and pi head row blocks as one launch, phase C's GEMM items as another; each
+  // job waits per row block for the jobs whose outputs it reads
+  std::vector<WJob> FA, FC;
+  std::vector<JTag> TA, TC;
+  {
+    WJob g;
+    memset(&g, 0, sizeof(g));
+    g.amode = WA_GATHER;
+    g.M = Brw;
+    g.nrb = Brw / 64;
+    g.ncb = 1;
+    FA.push_back(g);
+    TA.push_back(JTag{3, -1, 0, 0});
+  }
+  for (const sac_engine::WStage& st : e->wst) {
+    if (st.kind == 2) {
+      WJob hj;
+      memset(&hj, 0, sizeof(hj));
+      hj.amode = WA_HEAD;
+      hj.M = 2 * Brw;
+      hj.nrb = 2 * Brw / 64;
+      hj.ncb = 1;
+      FA.push_back(hj);
+      TA.push_back(JTag{2, NET_PI, 0, 0});
+    } else if (st.kind == 1) {
+      for (int k = st.j0; k < st.j1; ++k) {
+        (st.phase == 0 ? FA : FC).push_back(JB[k]);
+        (st.phase == 0 ? TA : TC).push_back(tags[k]);
+      }
+    }
+  }
+  // (kbuf: the K-block buffer size above)
+  const size_t glds_f = (size_t)((WGR * (O + A) + 1) & ~1) + WGR * 2;  // the gather's LDS, floats
+  size_t cnt_off = 0, lf = glds_f;
+  auto finish = [&](std::vector<WJob>& F, std::vector<JTag>& T) {
+    auto find = [&](int kind, int ni, int d) {
+      for (size_t k = 0; k < T.size(); ++k)
+        if (T[k].kind == kind && (kind >= 2 || (T[k].ni == ni && T[k].d == d))) return (int)k;
+      fprintf(stderr, "sac_engine: internal: flow producer %d/%d/%d not planned\n", kind, ni, d);
+      abort();
+      return -1;
+    };
+    int item = 0;
+    for (size_t k = 0; k < F.size(); ++k) {
+      WJob& j = F[k];
+      const JTag& t = T[k];
+      j.item0 = item;
+      item += j.nrb * j.ncb;
+      j.cnt_off = (int)cnt_off;
+      cnt_off += j.nrb;
+      j.nbuf = 2;
+      std::vector<int> deps;
+      const bool critic = t.ni == NET_Q1 || t.ni == NET_Q2;
+      if (t.kind == 0) {
+        if (t.d > 0) deps.push_back(find(0, t.ni, t.d - 1));
+        else if (t.phase == 0) deps.push_back(t.ni == NET_Q1T || t.ni == NET_Q2T ? find(2, 0, 0) : find(3, 0, 0));
+      } else if (t.kind == 2) {
+        deps.push_back(find(0, NET_PI, hp - 1));
+      } else if (t.kind == 1) {
+        const int top = (t.ni == NET_PI ? hp : hq) - 1;
+        if (t.d < top) {
+          deps.push_back(find(1, t.ni, t.d + 1));
+        } else if (t.phase == 0) {  // y: target critics' outputs, this critic's output (and log pi' via Qt)
+          deps.push_back(find(0, t.ni, hq - 1));
+          deps.push_back(find(0, NET_Q1T, hq - 1));
+          deps.push_back(find(0, NET_Q2T, hq - 1));
+        } else if (critic) {  // min-Q weights: both critics' outputs
+          deps.push_back(find(0, NET_Q1, hq - 1));
+          deps.push_back(find(0, NET_Q2, hq - 1));
+        } else {  // pi head backward: both critics' d a~ partials (their layer-1 backward)
+          deps.push_back(find(1, NET_Q1, 1));
+          deps.push_back(find(1, NET_Q2, 1));
+        }
+      }
+      j.ndep = (int)deps.size();
+      for (int q = 0; q < j.ndep; ++q) {
+        j.dep_job[q] = deps[q];
+        j.dep_need[q] = F[deps[q]].ncb;
+      }
+      if (j.amode <= WA_OUTBWD) {
+        size_t x = 2 * kbuf + WWS;
+        if (j.amode == WA_OUTBWD) x += 64 * WLDD + (size_t)j.J * j.Kp;
+        lf = std::max(lf, x);
+      }
+    }
+    return item;
+  };
+  const int ia = finish(FA, TA), ic = finish(FC, TC);
+  JB.clear();
+  JB.insert(JB.end(), FA.begin(), FA.end());
+  JB.insert(JB.end(), FC.begin(), FC.end());
+  e->wst.clear();
+  e->wst.push_back(sac_engine::WStage{5, 0, (int)FA.size(), ia, 0, 0, lf * 4, 0});
+  e->wst.push_back(sac_engine::WStage{3, 0, 0, 0, 1, 0, 0, 0});
+  e->wst.push_back(sac_engine::WStage{5, (int)FA.size(), (int)JB.size(), ic, 2, 1, lf * 4, 0});
+  e->wst.push_back(sac_engine::WStage{4, 0, 0, 0, 3, 0, 0, 0});
 }
 
 static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
@@ -860,6 +969,8 @@ static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
     int on = able && too_big;
     if (const char* v = getenv("SAC_WIDE")) on = atoi(v) != 0 ? able : 0;
     wl.on = on;
+    wl.flow = 0;
+    if (const char* v = getenv("SAC_WIDE_FLOW")) wl.flow = on && atoi(v) != 0;
   }
   if (wl.on) {
     const int Brw = rup(B, 64);
@@ -871,6 +982,7 @@ static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
     wl.hq = hq;
     wl.o_dev = lay.take(sizeof(WideDev));
     wl.o_jobs = lay.take(WIDE_MAX_JOBS * sizeof(WJob));
+    wl.o_cnt = lay.take((size_t)WIDE_MAX_JOBS * (2 * Brw / 64) * 4);  // flow: per (job, row block) counters
     wl.o_xpi0 = lay.take((size_t)2 * Brw * np.l[0].Kp * 4);
     wl.o_xq0 = lay.take((size_t)Brw * nq.l[0].Kp * 4);
     wl.o_xqt0 = lay.take((size_t)Brw * nq.l[0].Kp * 4);
@@ -1287,6 +1399,8 @@ static void set_lds_attrs(size_t bytes) {
   (void)hipFuncSetAttribute((const void*)sac_wide_stage<T, WA_PLAIN, true>, hipFuncAttributeMaxDynamicSharedMemorySize, b);
   (void)hipFuncSetAttribute((const void*)sac_wide_stage<T, WA_ACT, true>, hipFuncAttributeMaxDynamicSharedMemorySize, b);
   (void)hipFuncSetAttribute((const void*)sac_wide_stage<T, WA_OUTBWD, true>, hipFuncAttributeMaxDynamicSharedMemorySize, b);
+  (void)hipFuncSetAttribute((const void*)sac_wide_flow<T, false>, hipFuncAttributeMaxDynamicSharedMemorySize, b);
+  (void)hipFuncSetAttribute((const void*)sac_wide_flow<T, true>, hipFuncAttributeMaxDynamicSharedMemorySize, b);
 }
 
 // empty kernel: the dispatch + event gap of sac_engine_time_phases
@@ -1368,6 +1482,13 @@ static void launch_wide_stage(sac_engine* e, const sac_engine::WStage& st, const
     case 2:
       sac_wide_head<T><<<st.grid, WG_T, 0, s>>>(e->d, e->wdd, eps);
       break;
+    case 5: {
+      const bool relu = e->cfg.q_hidden_act == ACT_RELU && e->cfg.pi_hidden_act == ACT_RELU;
+      const int flags = st.last | (st.phase == 2 ? 2 : 0);
+      auto k = relu ? sac_wide_flow<T, true> : sac_wide_flow<T, false>;
+      k<<<st.G, WG_T, st.lds, s>>>(e->d, e->wdd, e->wjobs + st.j0, st.j1 - st.j0, st.grid, flags, *rb, idx, eps);
+      break;
+    }
     case 3:
       launch_kind<T>(e, L_B, rb, idx, eps, s);
       break;
@@ -1570,6 +1691,23 @@ int sac_engine_create(const sac_engine_config* cfg, const sac_engine_buffers* bu
             ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, sac_persist<bf16>, SAC_THREADS, lds)
             : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, sac_persist<float>, SAC_THREADS, lds);
     if (oe != hipSuccess || nb < 1 || e->G > nb * e->ncu) e->persist = 0;
+  }
+  if (e->wide && e->wl.flow) {
+    // the flow launches' workgroups wait on each other: all of them resident at once
+    const bool relu = cfg->q_hidden_act == ACT_RELU && cfg->pi_hidden_act == ACT_RELU;
+    const bool bf = cfg->precision == SAC_PREC_BF16;
+    for (sac_engine::WStage& st : e->wst) {
+      if (st.kind != 5) continue;
+      int nb = 0;
+      const void* k = bf ? (relu ? (const void*)sac_wide_flow<bf16, true> : (const void*)sac_wide_flow<bf16, false>)
+                         : (relu ? (const void*)sac_wide_flow<float, true> : (const void*)sac_wide_flow<float, false>);
+      const hipError_t oe = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, WG_T, st.lds);
+      if (oe != hipSuccess || nb < 1) {
+        delete e;
+        return fail(SAC_E_HIP, "the flow kernel does not fit a CU");
+      }
+      st.G = std::min(st.grid, nb * e->ncu);
+    }
   }
   hipStream_t s = (hipStream_t)stream;
   hipError_t err = hipMemsetAsync(buf->workspace, 0, buf->workspace_bytes, s);

@@ -557,14 +557,16 @@ def test_fused_step_equals_four_launches(lib, cfg, precision, monkeypatch):
         assert torch.equal(out["1"][k], out["0"][k]), (k, (out["1"][k].double() - out["0"][k].double()).abs().max())
 
 
-@pytest.mark.parametrize("precision", ["fp32", "bf16"])
-def test_stage_path_staged_batches_equal_fresh_gathers(precision, monkeypatch):
+@pytest.mark.parametrize("precision,flow", [("fp32", "0"), ("bf16", "0"), ("fp32", "1"), ("bf16", "1")])
+def test_stage_path_staged_batches_equal_fresh_gathers(precision, flow, monkeypatch):
     """The stage path (csrc/sac_wide.h, forced at C3 by SAC_WIDE=1) gathers step
     t+1's batch inside step t's last phase-C launch; the first step of every
-    call gathers its own.  So one call of 5 steps (device RNG) must equal 5
-    calls of one step, bit for bit, and the same with injected indices; graph
+    call gathers its own (the flow kernel, SAC_WIDE_FLOW=1, gathers every step
+    inside its phase-A launch).  So one call of 5 steps (device RNG) must equal
+    5 calls of one step, bit for bit, and the same with injected indices; graph
     replay equals eager launches."""
     monkeypatch.setenv("SAC_WIDE", "1")
+    monkeypatch.setenv("SAC_WIDE_FLOW", flow)
     out = {}
     for mode in ("one_call", "per_step", "graph"):
         eng, rb, c = _engine("c3", precision, capacity=12_000)

@@ -95,6 +95,26 @@ def test_c3_stage_path_matches_oracle(precision, monkeypatch):
     test_baseline_config_matches_oracle("c3", 12_288, 2, precision)
 
 
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_c3_flow_path_matches_oracle(precision, monkeypatch):
+    """C3 through the flow kernel (SAC_WIDE=1 SAC_WIDE_FLOW=1: phases A and C
+    as one persistent launch each, row-block counters between the stage
+    items), against the oracle like test_baseline_config_matches_oracle."""
+    monkeypatch.setenv("SAC_WIDE", "1")
+    monkeypatch.setenv("SAC_WIDE_FLOW", "1")
+    test_baseline_config_matches_oracle("c3", 12_288, 2, precision)
+
+
+@pytest.mark.parametrize("shape", ["wide_deep_b1100", "wide512_b384", "wide400_300"])
+def test_flow_path_edge_shapes_match_oracle(shape, monkeypatch):
+    """The flow kernel at ragged column blocks, three hidden layers and the
+    widths past the phase kernels' LDS, fp32, tolerances as the edge shapes."""
+    monkeypatch.setenv("SAC_WIDE", "1")
+    monkeypatch.setenv("SAC_WIDE_FLOW", "1")
+    c = dict(EDGE_SHAPES[shape], name=shape)
+    _check_config_against_oracle(c, "fp32", 2 if c["batch"] > 1024 else 3, traj_tol=2e-3)
+
+
 @pytest.mark.parametrize("name", ["c1_auto", "c2"])
 def test_engine_matches_reference_golden_directly(name):
     """Step 1 against the reference's own captured outputs (no oracle in between)."""

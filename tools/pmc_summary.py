@@ -23,7 +23,8 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PHASE_KERNELS = ("sac_target_critic", "sac_critic_update", "sac_actor", "sac_actor_update",
                  "replay_gather_records_kernel", "replay_gather_kernel",
-                 "replay_sample_kernel", "replay_push_kernel", "sac_policy_act_kernel")
+                 "replay_sample_kernel", "replay_push_kernel", "sac_policy_act_kernel",
+                 "sac_wide_stage", "sac_wide_gather", "sac_wide_head")
 
 
 def short(name: str) -> str:
