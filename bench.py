@@ -535,9 +535,11 @@ def measure_phases(args, eng, rb, c, elapsed, sps_one):
     tp = eng.time_phases(rb, 100)
     phase_ms, empty_ms = tp[:4], tp[4]
     step_ms = elapsed / args.steps * 1e3
-    n_launch = sum(1 for x in phase_ms if x > 0)
-    ev_cost = max((sum(phase_ms) - step_ms) / n_launch, 0.0)
-    kern_ms = [x - ev_cost if x > 0 else 0.0 for x in phase_ms]
+    # launches per step of each phase (the stage path runs several per phase):
+    # each launch's interval also holds one event
+    nl = [n if x > 0 else 0 for n, x in zip(eng.phase_launches, phase_ms)]
+    ev_cost = max((sum(phase_ms) - step_ms) / max(sum(nl), 1), 0.0)
+    kern_ms = [x - ev_cost * n if x > 0 else 0.0 for x, n in zip(phase_ms, nl)]
     flops, f_total, _, _ = gemm_flops(c["obs"], c["act"], c["hidden"], c["batch"])
     if eng.fused:  # D inside the next A launch (and with layout 2, B inside the C launch)
         flops = [flops[0] + flops[3], flops[1], flops[2], 0]
@@ -568,6 +570,7 @@ def measure_phases(args, eng, rb, c, elapsed, sps_one):
         "phase_ms": [round(x, 5) for x in kern_ms],
         "phase_event_interval_ms": [round(x, 5) for x in phase_ms],
         "event_cost_ms": round(ev_cost, 5),
+        "phase_launches_per_step": nl,
         "empty_kernel_event_interval_ms": round(empty_ms, 5),
         "step_gemm_flops_survey": f_total,
         "roofline": {"bound": "mfma", "kernel": kname, "achieved": round(achieved, 3), "peak": peak,

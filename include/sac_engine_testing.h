@@ -33,6 +33,9 @@ int sac_engine_uses_fused_step(const sac_engine *e);
  * layer-synchronous GEMM stages for phases A and C, used where the per-network
  * role kernels do not fit), else 0. */
 int sac_engine_uses_wide(const sac_engine *e);
+/* Launches per step of each phase A, B, C, D into out[4] (the stage path runs
+   several per phase; its first-step gather is not counted); returns 0. */
+int sac_engine_phase_launches(const sac_engine *e, int32_t *out);
 /* Host evaluation of the device sampler (the same inline code as the sampler
  * inside sac_engine_train and sac_replay_sample_indices): out[b] = b-th element
  * of the Philox-keyed Feistel permutation of [0, size) for RNG (seed, step). */

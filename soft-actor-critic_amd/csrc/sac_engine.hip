@@ -925,12 +925,23 @@ static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
   int pi0_parts = 2, q0_parts = 2;
   if (const char* v = getenv("SAC_PI0_PARTS")) pi0_parts = std::max(1, std::min(4, atoi(v)));
   if (const char* v = getenv("SAC_Q0_PARTS")) q0_parts = std::max(1, std::min(4, atoi(v)));
+  // 64 x 64 update tiles (dw_adam_tile64) at large batches without the hidden
+  // split: half the operand bytes per weight (C3's B / D are operand-bound);
+  // SAC_TILE64=0 keeps 32 x 32
+  int t64 = !split && Bp > 1024;
+  if (const char* v = getenv("SAC_TILE64")) t64 = t64 && atoi(v) != 0;
+  const int TS = t64 ? 64 : 32;
+  const size_t part_stride = t64 ? SAC_PART_STRIDE64 : SAC_PART_STRIDE;
+  auto ntiles_of = [&](const LayerDev& ly) { return ((ly.Np + TS - 1) / TS) * ((ly.Kp + TS - 1) / TS); };
   int tilesBD[2] = {0, 0};  // [critics (B), policy (D)]
   for (int ni = NET_PI; ni <= NET_Q2; ++ni)
-    for (int l = 0; l < h.net[ni].L; ++l)
-      tilesBD[ni == NET_PI] += (h.net[ni].l[l].Np / 32) * (h.net[ni].l[l].Kp / 32);
+    for (int l = 0; l < h.net[ni].L; ++l) tilesBD[ni == NET_PI] += ntiles_of(h.net[ni].l[l]);
   auto batch_parts = [&](int ntiles, int extra) {
     if (Bp <= 1024) return 1;
+    if (t64) {  // one round: as many batch parts (<= 8) as keep the tiles within 256 workgroups
+      if (const char* v = getenv("SAC_BPARTS")) return std::max(1, std::min(8, atoi(v)));
+      return std::max(1, std::min(8, (256 - extra) / std::max(ntiles, 1)));
+    }
     if (const char* v = getenv("SAC_BPARTS")) return std::max(1, std::min(4, atoi(v)));
     int best = 4;
     double bc = 1e30;
@@ -949,7 +960,7 @@ static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
   int nB = 0, nD = 0, nhalf = 0;
   for (int ni = NET_PI; ni <= NET_Q2; ++ni)
     for (int l = 0; l < h.net[ni].L; ++l) {
-      const int t = (h.net[ni].l[l].Np / 32) * (h.net[ni].l[l].Kp / 32);
+      const int t = ntiles_of(h.net[ni].l[l]);
       const int parts = tile_parts(ni, l);
       (ni == NET_PI ? nD : nB) += t * parts;
       nhalf += t * (parts - 1);  // producer parts: one granule slot each
@@ -1019,7 +1030,7 @@ static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
   const size_t o_ptask = lay.take((size_t)1024 * sizeof(PTask));
   const size_t o_tB = lay.take((size_t)nB * sizeof(TileDesc));
   const size_t o_tD = lay.take((size_t)nD * sizeof(TileDesc));
-  const size_t o_part = lay.take((size_t)nhalf * SAC_PART_STRIDE * 8);  // batch-half partial dW granules of split tiles
+  const size_t o_part = lay.take((size_t)nhalf * part_stride * 8);  // batch-part partial dW granules
   const size_t total = lay.take(0);
 
   // LDS layout (floats) of the row-tile / role kernels (policy_act included).
@@ -1104,6 +1115,7 @@ static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
       const int bch = 512 / esz;
       e->h.upd_slots = std::min(4, (Bp + bch - 1) / bch);
       e->upd_lds = SAC_UPD_LDS_FOR(e->h.upd_slots);
+      if (t64) e->upd_lds = std::max((size_t)SAC_UPD64_LDS, (size_t)5 * 1024 * 4);  // (the alpha block: 5 x 1024 floats)
     }
     e->nrt = nrt;
     // self-contained update tiles (phase B: critics + Polyak, phase D: policy)
@@ -1117,14 +1129,15 @@ static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
       const NetDev& tn = h.net[ni == NET_PI ? NET_PI : ni + 2];
       for (int l = 0; l < nd.L; ++l) {
         const LayerDev& ly = nd.l[l];
-        for (int nt = 0; nt < ly.Np / 32; ++nt)
-          for (int kt = 0; kt < ly.Kp / 32; ++kt) {
+        for (int nt = 0; nt < (ly.Np + TS - 1) / TS; ++nt)
+          for (int kt = 0; kt < (ly.Kp + TS - 1) / TS; ++kt) {
             TileDesc t;
             memset(&t, 0, sizeof(t));
             const int bpl = (l == 0 && split) ? 2 * Bp : Bp;                     // X^T row stride
             const int bpg = (l == 0 && split) ? (ni == NET_PI ? wc : 2) * Bp : Bp;  // dY^T row stride
-            t.GT = (const char*)ly.GT + (size_t)nt * 32 * bpg * esz2;
-            t.XT = (const char*)ly.XT + (size_t)kt * 32 * bpl * esz2;
+            t.tile64 = t64;
+            t.GT = (const char*)ly.GT + (size_t)nt * TS * bpg * esz2;
+            t.XT = (const char*)ly.XT + (size_t)kt * TS * bpl * esz2;
             t.W = nd.P + ly.w_off;
             t.Wm = nd.M + ly.w_off;
             t.Wv = nd.V + ly.w_off;
@@ -1145,8 +1158,8 @@ static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
             t.N = ly.N;
             t.Kp = ly.Kp;
             t.Np = ly.Np;
-            t.n0 = nt * 32;
-            t.k0 = kt * 32;
+            t.n0 = nt * TS;
+            t.k0 = kt * TS;
             t.opt = ni;
             t.nrt = (l == 0 && split) ? bpg / SAC_ROWS : nrt;
             t.ld = t.bp;
@@ -1179,7 +1192,7 @@ static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
               t.bp = bpp;
               t.kpart = 1;
               t.nparts = parts;
-              t.part = (uint64_t*)(base + o_part) + (size_t)ihalf * SAC_PART_STRIDE;
+              t.part = (uint64_t*)(base + o_part) + (size_t)ihalf * part_stride;
               ihalf += parts - 1;
               for (int pp = 2; pp <= parts; ++pp) {
                 TileDesc pt = t;
@@ -1224,6 +1237,7 @@ static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
       e->fused = fuse;
     }
     plan_persist(e, esz);
+    if (t64) e->persist = 0;  // the fused step runs the 32 x 32 tiles only
     e->wl = wl;
     e->wide = wl.on;
     if (wl.on) build_wide(e, base);
@@ -1954,6 +1968,20 @@ int sac_engine_uses_split(const sac_engine* e) { return e && e->h.split ? 1 : 0;
 int sac_engine_uses_fused_step(const sac_engine* e) { return e && e->persist ? e->G : 0; }
 
 int sac_engine_uses_wide(const sac_engine* e) { return e && e->wide ? (int)e->wst.size() : 0; }
+
+int sac_engine_phase_launches(const sac_engine* e, int32_t* out) {
+  if (!e || !out) return fail(SAC_E_INVALID, "null argument");
+  for (int k = 0; k < 4; ++k) out[k] = 1;
+  if (e->wide) {
+    for (int k = 0; k < 4; ++k) out[k] = 0;
+    for (const sac_engine::WStage& st : e->wst)
+      if (st.kind != 0 && st.phase >= 0 && st.phase < 4) ++out[st.phase];
+  } else if (e->fused) {
+    out[1] = e->fused == 2 ? 0 : 1;
+    out[3] = 0;
+  }
+  return SAC_OK;
+}
 
 int sac_engine_phase_layout(const sac_engine* e) { return e ? e->fused : 0; }
 

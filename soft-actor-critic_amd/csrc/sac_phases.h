@@ -191,7 +191,8 @@ struct TileDesc {
   // column blocks (goff elements apart) are added elementwise while staging, in
   // part order, and reduced once against X -- no batch parts, no hand-off
   long goff;
-  int gsum, pad_;
+  int gsum;
+  int tile64;      // a 64 x 64 tile (dw_adam_tile64: large batches, no hidden split)
   // fp32 split critics (every layer): dY^T holds the unit-seed backward (phase
   // A's critic roles store it without waiting for y); every batch column b is
   // scaled by seed[b] (phase A's first target-critic half computes the seeds)
@@ -1309,11 +1310,280 @@ __device__ __forceinline__ void dw_adam_tile(const AS_C EngineDev& E, const Tile
   }
 }
 
+// ---------------------------------------------------------------------------- 64 x 64 update tiles
+// Large batches (Bp > 1024, no hidden split; TileDesc.tile64): one workgroup
+// updates a 64 x 64 block of a weight matrix -- the 32 x 32 tile's three steps
+// (dw_adam_tile above) on four times the outputs per staged operand row, so
+// half the operand bytes per weight.  At C3 the update phases are bound by the
+// operand bytes each CU has in flight (profiles/r04_pmc_c3_fp32.json: B fetches
+// 78 MB in 38 us, ~30 GB/s per CU), not by the MFMAs.  Rows past the padded
+// widths (Np, Kp) are neither loaded nor stored; elements past (N, K) are not
+// updated.  Batch parts as the 32 x 32 tiles (granule hand-off to part 1), with
+// SAC_PART_STRIDE64 granules per producer part and no bias granules (the bias
+// gradient is the row tiles' partial sums, read whole by part 1).
+#define SAC_PART_STRIDE64 4096
+#define SAC_UPD64_SLOT_BYTES (128 * 528)
+#define SAC_UPD64_LDS (2 * SAC_UPD64_SLOT_BYTES + 64 * 17 * 4)
+template <typename T, int UT>
+__device__ __forceinline__ void dw_adam_tile64(const AS_C EngineDev& E, const TileDesc* tdp_, bool polyak, int par,
+                                               int par_x, lf* lds) {
+  static_assert(UT == 1024, "16 waves: one 16 x 16 sub-tile each");
+  constexpr int KC = MM<T>::KC, KL = MM<T>::KL;
+  constexpr int EPR = 16 / sizeof(T);            // elements per 16-B piece
+  constexpr int BCH = 512 / (int)sizeof(T);      // batch columns per staged chunk (512 B per row)
+  constexpr int EPT = 4096 / UT;                 // elements per thread
+  constexpr int NS = 2;                          // chunks (LDS slots) per round
+  constexpr int PPO = 64 * (BCH / EPR) / UT;     // pieces per thread per operand per chunk
+  static_assert(PPO >= 1 && 64 * (BCH / EPR) % UT == 0, "whole pieces per thread");
+  const AS_C TileDesc& td = *(const AS_C TileDesc*)tdp_;
+  const int tid = threadIdx.x, lane = tid & 63, wave = wave_id();
+  const int c = lane & 15, g = lane >> 4;
+  const int Bp = td.bp;
+  constexpr int LROW = BCH + 16 / (int)sizeof(T);  // T elements per staged row (+16 B: rows on different banks)
+  static_assert(LROW * (int)sizeof(T) * 128 == SAC_UPD64_SLOT_BYTES, "slot size");
+  AS_L T* stage = (AS_L T*)lds;
+  constexpr int SLOT = 128 * LROW;  // T elements per slot: dY^T rows 0..63, then X^T rows 64..127
+  lf* red = lds + NS * SAC_UPD64_SLOT_BYTES / 4;  // [64][17] bias partial lanes
+  const float neg_step = GPC(float, E.adam_sc)[par * 6 + td.opt * 2];
+  const float bc2s = GPC(float, E.adam_sc)[par * 6 + td.opt * 2 + 1];
+  const AS_G T* const gsrc = GPC(T, td.GT);
+  const AS_G T* const xsrc = GPC(T, td.XT) + par_x * td.xt_par;
+  const int ldg = td.ld, ldx = td.ldx;
+  const int gr = min(64, td.Np - td.n0), xr = min(64, td.Kp - td.k0);  // operand rows that exist
+  u32x4 rg[NS][2][PPO];
+  auto issue = [&](int r0, auto slc) {
+    constexpr int sl = decltype(slc)::value;
+    const int b0 = r0 + sl * BCH;
+    if (b0 < Bp) {  // uniform
+      const int per_row = min(Bp - b0, BCH) / EPR;
+#pragma unroll
+      for (int op = 0; op < 2; ++op)
+#pragma unroll
+        for (int pi = 0; pi < PPO; ++pi) {
+          const int i = tid + pi * UT, row = i / per_row, pc = i % per_row;
+          const AS_G T* src = op ? xsrc + (size_t)row * ldx : gsrc + (size_t)row * ldg;
+          if (i < 64 * per_row && row < (op ? xr : gr)) rg[sl][op][pi] = *(const AS_G u32x4*)(src + b0 + pc * EPR);
+        }
+    }
+  };
+  static_for<NS>([&](auto sl) { issue(0, sl); });
+  // element state (4 elements per thread), bias state, bias partials: one round trip with the operands
+  AS_G float* W = GP(float, td.W);
+  AS_G float* Wm = GP(float, td.Wm);
+  AS_G float* Wv = GP(float, td.Wv);
+  AS_G float* tW = GP(float, td.tW);
+  float p[EPT], m[EPT], v[EPT], tp[EPT];
+  size_t idx[EPT];
+  bool ok[EPT];
+#pragma unroll
+  for (int e = 0; e < EPT; ++e) {
+    const int el = tid + e * UT, en = el >> 6, ek = el & 63;
+    const int n = td.n0 + en, k = td.k0 + ek;
+    ok[e] = n < td.N && k < td.K;
+    idx[e] = ok[e] ? (size_t)n * td.K + k : 0;
+    if (td.kpart < 2) {
+      p[e] = W[idx[e]];
+      m[e] = Wm[idx[e]];
+      v[e] = Wv[idx[e]];
+      tp[e] = polyak ? tW[idx[e]] : 0.f;
+    } else {
+      p[e] = m[e] = v[e] = tp[e] = 0.f;
+    }
+  }
+  const bool do_bias = td.k0 == 0 && td.kpart <= 1;
+  float pb = 0.f, mb = 0.f, vb = 0.f, tbv = 0.f;
+  if (do_bias && tid < 64 && td.n0 + tid < td.N) {
+    pb = GPC(float, td.b)[td.n0 + tid];
+    mb = GPC(float, td.bm)[td.n0 + tid];
+    vb = GPC(float, td.bv)[td.n0 + tid];
+    if (polyak) tbv = GPC(float, td.tb)[td.n0 + tid];
+  }
+  // bias gradient: the row tiles' partial sums, 16 lanes per column (64 x 16 = 1024 lanes),
+  // 16 loads in flight per lane, added in row-tile order
+  float bsum = 0.f;
+  {
+    const int bn = tid >> 4, bs = tid & 15;
+    if (do_bias && td.n0 + bn < td.N) {
+      const AS_G float* dbp = GPC(float, td.dbp) + td.n0 + bn;
+      constexpr int BU = 16;
+      for (int rt0 = bs; rt0 < td.nrt; rt0 += 16 * BU) {
+        float pv[BU];
+#pragma unroll
+        for (int u = 0; u < BU; ++u) {
+          const int rt = rt0 + 16 * u;
+          pv[u] = rt < td.nrt ? dbp[(size_t)rt * td.N] : 0.f;
+        }
+#pragma unroll
+        for (int u = 0; u < BU; ++u)
+          if (rt0 + 16 * u < td.nrt) bsum += pv[u];
+      }
+    }
+  }
+  // ---- dW = dY^T X over the batch: chunk by chunk through LDS, NS chunks per
+  // round, the next round's loads issued as soon as a chunk is in LDS; wave w
+  // owns the 16 x 16 sub-tile (rows 16 (w >> 2), columns 16 (w & 3)) over every chunk
+  const int sn = (wave >> 2) * 16, sk = (wave & 3) * 16;
+  f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+  for (int r0 = 0; r0 < Bp; r0 += NS * BCH) {
+    static_for<NS>([&](auto slc) {
+      constexpr int sl = decltype(slc)::value;
+      const int b0 = r0 + sl * BCH;
+      if (b0 < Bp) {  // uniform
+        const int bch = min(Bp - b0, BCH);
+        const int per_row = bch / EPR;
+#pragma unroll
+        for (int op = 0; op < 2; ++op)
+#pragma unroll
+          for (int pi = 0; pi < PPO; ++pi) {
+            const int i = tid + pi * UT, row = i / per_row, pc = i % per_row;
+            if (i < 64 * per_row && row < (op ? xr : gr))
+              *(AS_L u32x4*)(stage + sl * SLOT + (row + 64 * op) * LROW + pc * EPR) = rg[sl][op][pi];
+          }
+        issue(r0 + NS * BCH, slc);
+        __syncthreads();
+        const AS_L T* arow = stage + sl * SLOT + (sn + c) * LROW + g * KL;
+        const AS_L T* brow = stage + sl * SLOT + (64 + sk + c) * LROW + g * KL;
+        const int nchk = bch / KC;
+        auto frag = [&](const AS_L T* r, int ch) __attribute__((always_inline)) {
+          if constexpr (sizeof(T) == 2) return *(const AS_L bf16x8*)(r + ch * KC);
+          else return *(const AS_L f32x4*)(r + ch * KC);
+        };
+        for (int ch = 0; ch < nchk; ch += 2) {  // two accumulators: even / odd chunks
+          MM<T>::mma(acc0, frag(arow, ch), frag(brow, ch));
+          if (ch + 1 < nchk) MM<T>::mma(acc1, frag(arow, ch + 1), frag(brow, ch + 1));
+        }
+      }
+    });
+    __syncthreads();  // the slots are refilled by the next round
+  }
+  // ---- partial dW -> LDS [64][65] (the free stage), bias lanes -> red
+  lf* accs = (lf*)stage;
+  lf* tgts = accs + 64 * 65;
+  {
+    const f32x4 a = acc0 + acc1;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) accs[(sn + g * 4 + i) * 65 + sk + c] = a[i];
+  }
+  red[(tid >> 4) * 17 + (tid & 15)] = bsum;
+  __syncthreads();
+  if (td.kpart) {  // batch parts of this tile meet at part 1
+    const uint32_t ep = *GPC(uint32_t, E.sync) + 1u;
+    if (td.kpart >= 2) {
+      AS_G uint64_t* mine = GP(uint64_t, td.part) + (size_t)(td.kpart - 2) * SAC_PART_STRIDE64;
+#pragma unroll
+      for (int e = 0; e < EPT; ++e) {
+        const int el = tid + e * UT;
+        const uint64_t x = (uint64_t)__float_as_uint(accs[(el >> 6) * 65 + (el & 63)]) | ((uint64_t)ep << 32);
+        __hip_atomic_store((uint64_t*)(mine + el), x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      return;  // uniform: part 1 runs Adam on the sum
+    }
+    const int np = td.nparts - 1;  // producer parts (1..7)
+    float sum[EPT];
+#pragma unroll
+    for (int e = 0; e < EPT; ++e) {
+      const int el = tid + e * UT;
+      sum[e] = accs[(el >> 6) * 65 + (el & 63)];
+    }
+    for (int q = 0; q < np; ++q) {  // producer parts in order
+      float vq[EPT];
+      for (int it = 0;; ++it) {
+        bool all = true;
+#pragma unroll
+        for (int e = 0; e < EPT; ++e) {
+          const uint64_t x = __hip_atomic_load(td.part + (size_t)q * SAC_PART_STRIDE64 + tid + e * UT, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT);
+          all = all && (uint32_t)(x >> 32) == ep;
+          vq[e] = __uint_as_float((uint32_t)x);
+        }
+        if (all) break;
+        if (it > E.spin_limit) {  // a producer part never ran: flag the error, do not hang
+          __hip_atomic_store((uint32_t*)GP(uint32_t, E.sync) + 1 /* SYNC_TIMEOUT */, 1u, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+#pragma unroll
+      for (int e = 0; e < EPT; ++e) sum[e] += vq[e];
+    }
+    __syncthreads();  // every read of accs done
+#pragma unroll
+    for (int e = 0; e < EPT; ++e) {
+      const int el = tid + e * UT;
+      accs[(el >> 6) * 65 + (el & 63)] = sum[e];
+    }
+    __syncthreads();
+  }
+  // ---- elements: Adam + Polyak on the masters; new values -> LDS
+  const float w1 = (float)(1.0 - (double)E.beta1), b2 = E.beta2, w2 = (float)(1.0 - (double)E.beta2);
+  const float eps = E.adam_eps, tau = E.tau, omt = (float)(1.0 - (double)E.tau);
+  float pn[EPT], tn[EPT];
+#pragma unroll
+  for (int e = 0; e < EPT; ++e) {
+    const int el = tid + e * UT;
+    pn[e] = 0.f;
+    tn[e] = 0.f;
+    if (ok[e]) {
+      pn[e] = adam_elem(p[e], m[e], v[e], accs[(el >> 6) * 65 + (el & 63)], w1, b2, w2, bc2s, eps, neg_step);
+      W[idx[e]] = p[e];
+      Wm[idx[e]] = m[e];
+      Wv[idx[e]] = v[e];
+      if (polyak) {
+        tn[e] = tau * pn[e] + omt * tp[e];
+        tW[idx[e]] = tn[e];
+      }
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int e = 0; e < EPT; ++e) {
+    const int el = tid + e * UT;
+    accs[(el >> 6) * 65 + (el & 63)] = pn[e];  // padding elements: 0, as packed
+    if (polyak) tgts[(el >> 6) * 65 + (el & 63)] = tn[e];
+  }
+  if (do_bias && tid < 64 && td.n0 + tid < td.N) {
+    float gb = 0.f;
+    for (int q = 0; q < 16; ++q) gb += red[tid * 17 + q];
+    const float pbn = adam_elem(pb, mb, vb, gb, w1, b2, w2, bc2s, eps, neg_step);
+    GP(float, td.b)[td.n0 + tid] = pb;
+    GP(float, td.bm)[td.n0 + tid] = mb;
+    GP(float, td.bv)[td.n0 + tid] = vb;
+    if (polyak) GP(float, td.tb)[td.n0 + tid] = tau * pbn + omt * tbv;
+  }
+  __syncthreads();
+  // ---- packed copies as 16-B pieces (rows past Np / Kp do not exist)
+  constexpr int PPR = 64 / EPR;  // pieces per 64-element row
+  for (int mat = 0; mat < (polyak ? 3 : 2); ++mat) {
+    const void* base = mat == 0 ? td.Wc : mat == 1 ? td.WTc : td.tWc;
+    for (int i = tid; i < 64 * PPR; i += UT) {
+      const int row = i / PPR, pc = i % PPR;
+      T vv[EPR];
+      size_t off;
+      if (mat == 1) {  // W^T: row k = k0 + row, columns n = n0 + pc * EPR + j
+        if (row >= xr || pc * EPR >= gr) continue;
+#pragma unroll
+        for (int j = 0; j < EPR; ++j) vv[j] = MM<T>::cvt(accs[(pc * EPR + j) * 65 + row]);
+        off = packed_off<T>(td.k0 + row, td.n0 + pc * EPR, td.Np);
+      } else {  // W or target W: row n = n0 + row, columns k = k0 + pc * EPR + j
+        if (row >= gr || pc * EPR >= xr) continue;
+        const lf* srcm = mat == 0 ? accs : tgts;
+#pragma unroll
+        for (int j = 0; j < EPR; ++j) vv[j] = MM<T>::cvt(srcm[row * 65 + pc * EPR + j]);
+        off = packed_off<T>(td.n0 + row, td.k0 + pc * EPR, td.Kp);
+      }
+      *(AS_G u32x4*)((AS_G char*)base + off * sizeof(T)) = *(const u32x4*)vv;
+    }
+  }
+}
+
 // a tile with summed dY parts (fp32 hidden-split layer 0) runs its own instance
 template <typename T, int UT, bool COH, bool P = false, typename Wait = NoWait>
 __device__ __forceinline__ void dw_adam_tile_any(const AS_C EngineDev& E, const TileDesc* tdp_, bool polyak, int par,
                                                  int par_x, lf* lds, const UpdStep* us = nullptr,
                                                  const Wait& wait = Wait()) {
+  if constexpr (!P && UT == 1024)
+    if (((const AS_C TileDesc*)tdp_)->tile64) return dw_adam_tile64<T, UT>(E, tdp_, polyak, par, par_x, lds);
   if constexpr (sizeof(T) == 4) {
     const int gs = ((const AS_C TileDesc*)tdp_)->gsum;  // uniform
     if (gs == 4) return dw_adam_tile<T, UT, COH, 4, P>(E, tdp_, polyak, par, par_x, lds, us, wait);

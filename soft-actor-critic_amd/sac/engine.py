@@ -146,6 +146,10 @@ class SacEngine:
         # large-batch stage path (csrc/sac_wide.h): launches per step, 0 when the phase kernels run
         self.lib.sac_engine_uses_wide.argtypes = [ctypes.c_void_p]
         self.wide = int(self.lib.sac_engine_uses_wide(h))
+        pl = (ctypes.c_int32 * 4)()
+        self.lib.sac_engine_phase_launches.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+        self.lib.sac_engine_phase_launches(h, pl)
+        self.phase_launches = list(pl)  # launches per step of phases A, B, C, D
 
     # ------------------------------------------------------------------ plumbing
     def _stream(self):

@@ -303,8 +303,12 @@ def _check_config_against_oracle(c, precision, steps, roles=None, traj_tol=1e-4)
         torch.cuda.synchronize()
         got = eng.losses()
         floor = float(np.mean(np.abs(st.alpha * ref["log_pi"])) + np.mean(np.abs(ref["y"]))) + 1e-6
+        # bf16 L_alpha = -log(alpha) mean(log pi + H): relative to the scale of its
+        # terms, |log alpha| mean|log pi| (the mean cancels; measured 0.85% rel at obs 300)
+        a_floor = abs(float(np.log(alpha_pre))) * float(np.mean(np.abs(ref["log_pi"]))) + 1e-6
         for i, (gv, w) in enumerate(zip(got, ref["losses"])):
-            assert _loss_ok(gv, w, floor if i == 2 else 1e-3, rtol), (ckey, precision, k, i, gv, w)
+            fl = floor if i == 2 else (a_floor if i == 3 and precision == "bf16" else 1e-3)
+            assert _loss_ok(gv, w, fl, rtol), (ckey, precision, k, i, gv, w)
         y = eng.last_targets().cpu().numpy()
         lp = eng.last_log_pi().cpu().numpy()
         if precision == "fp32":
