@@ -926,10 +926,10 @@ static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
   if (const char* v = getenv("SAC_PI0_PARTS")) pi0_parts = std::max(1, std::min(4, atoi(v)));
   if (const char* v = getenv("SAC_Q0_PARTS")) q0_parts = std::max(1, std::min(4, atoi(v)));
   // 64 x 64 update tiles (dw_adam_tile64) at large batches without the hidden
-  // split: half the operand bytes per weight (C3's B / D are operand-bound);
-  // SAC_TILE64=0 keeps 32 x 32
-  int t64 = !split && Bp > 1024;
-  if (const char* v = getenv("SAC_TILE64")) t64 = t64 && atoi(v) != 0;
+  // split: half the operand bytes per weight; opt-in (SAC_TILE64=1) until it
+  // beats the 32 x 32 tiles (profiles/r04_ab_tile64_c3.txt)
+  int t64 = 0;
+  if (const char* v = getenv("SAC_TILE64")) t64 = !split && Bp > 1024 && atoi(v) != 0;
   const int TS = t64 ? 64 : 32;
   const size_t part_stride = t64 ? SAC_PART_STRIDE64 : SAC_PART_STRIDE;
   auto ntiles_of = [&](const LayerDev& ly) { return ((ly.Np + TS - 1) / TS) * ((ly.Kp + TS - 1) / TS); };

@@ -1360,9 +1360,12 @@ __device__ __forceinline__ void dw_adam_tile64(const AS_C EngineDev& E, const Ti
       for (int op = 0; op < 2; ++op)
 #pragma unroll
         for (int pi = 0; pi < PPO; ++pi) {
-          const int i = tid + pi * UT, row = i / per_row, pc = i % per_row;
+          // unconditional loads (a per-lane "load or not" makes hipcc wait for each
+          // load before the next): rows past the operand's end re-load its last row
+          const int i = tid + pi * UT, pc = i % per_row;
+          const int row = min(i / per_row, (op ? xr : gr) - 1);
           const AS_G T* src = op ? xsrc + (size_t)row * ldx : gsrc + (size_t)row * ldg;
-          if (i < 64 * per_row && row < (op ? xr : gr)) rg[sl][op][pi] = *(const AS_G u32x4*)(src + b0 + pc * EPR);
+          rg[sl][op][pi] = *(const AS_G u32x4*)(src + b0 + pc * EPR);
         }
     }
   };
@@ -1435,9 +1438,9 @@ __device__ __forceinline__ void dw_adam_tile64(const AS_C EngineDev& E, const Ti
         for (int op = 0; op < 2; ++op)
 #pragma unroll
           for (int pi = 0; pi < PPO; ++pi) {
-            const int i = tid + pi * UT, row = i / per_row, pc = i % per_row;
-            if (i < 64 * per_row && row < (op ? xr : gr))
-              *(AS_L u32x4*)(stage + sl * SLOT + (row + 64 * op) * LROW + pc * EPR) = rg[sl][op][pi];
+            const int i = tid + pi * UT, pc = i % per_row;
+            const int row = min(i / per_row, (op ? xr : gr) - 1);  // (same clamp: duplicates write equal data)
+            *(AS_L u32x4*)(stage + sl * SLOT + (row + 64 * op) * LROW + pc * EPR) = rg[sl][op][pi];
           }
         issue(r0 + NS * BCH, slc);
         __syncthreads();
@@ -1485,28 +1488,35 @@ __device__ __forceinline__ void dw_adam_tile64(const AS_C EngineDev& E, const Ti
       const int el = tid + e * UT;
       sum[e] = accs[(el >> 6) * 65 + (el & 63)];
     }
-    for (int q = 0; q < np; ++q) {  // producer parts in order
-      float vq[EPT];
-      for (int it = 0;; ++it) {
-        bool all = true;
+    // every producer part's granules of this thread in one batch of loads per
+    // attempt (one round trip, not one per part); parts added in order
+    constexpr int MAXP = 7;
+    float vq[MAXP][EPT];
+    for (int it = 0;; ++it) {
+      bool all = true;
 #pragma unroll
-        for (int e = 0; e < EPT; ++e) {
-          const uint64_t x = __hip_atomic_load(td.part + (size_t)q * SAC_PART_STRIDE64 + tid + e * UT, __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_AGENT);
-          all = all && (uint32_t)(x >> 32) == ep;
-          vq[e] = __uint_as_float((uint32_t)x);
-        }
-        if (all) break;
-        if (it > E.spin_limit) {  // a producer part never ran: flag the error, do not hang
-          __hip_atomic_store((uint32_t*)GP(uint32_t, E.sync) + 1 /* SYNC_TIMEOUT */, 1u, __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_AGENT);
-          break;
-        }
-        __builtin_amdgcn_s_sleep(1);
+      for (int q = 0; q < MAXP; ++q)
+        if (q < np)
+#pragma unroll
+          for (int e = 0; e < EPT; ++e) {
+            const uint64_t x = __hip_atomic_load(td.part + (size_t)q * SAC_PART_STRIDE64 + tid + e * UT,
+                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            all = all && (uint32_t)(x >> 32) == ep;
+            vq[q][e] = __uint_as_float((uint32_t)x);
+          }
+      if (all) break;
+      if (it > E.spin_limit) {  // a producer part never ran: flag the error, do not hang
+        __hip_atomic_store((uint32_t*)GP(uint32_t, E.sync) + 1 /* SYNC_TIMEOUT */, 1u, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+        break;
       }
-#pragma unroll
-      for (int e = 0; e < EPT; ++e) sum[e] += vq[e];
+      __builtin_amdgcn_s_sleep(1);
     }
+#pragma unroll
+    for (int q = 0; q < MAXP; ++q)
+      if (q < np)
+#pragma unroll
+        for (int e = 0; e < EPT; ++e) sum[e] += vq[q][e];
     __syncthreads();  // every read of accs done
 #pragma unroll
     for (int e = 0; e < EPT; ++e) {

@@ -95,6 +95,17 @@ def test_c3_stage_path_matches_oracle(precision, monkeypatch):
     test_baseline_config_matches_oracle("c3", 12_288, 2, precision)
 
 
+@pytest.mark.parametrize("precision,parts", [("fp32", None), ("bf16", None), ("fp32", "2")])
+def test_c3_tile64_matches_oracle(precision, parts, monkeypatch):
+    """C3 with the 64 x 64 update tiles (SAC_TILE64=1, dw_adam_tile64; default
+    part count and 2 parts), against the oracle like
+    test_baseline_config_matches_oracle."""
+    monkeypatch.setenv("SAC_TILE64", "1")
+    if parts:
+        monkeypatch.setenv("SAC_BPARTS", parts)
+    test_baseline_config_matches_oracle("c3", 12_288, 2, precision)
+
+
 @pytest.mark.parametrize("precision", ["fp32", "bf16"])
 def test_c3_flow_path_matches_oracle(precision, monkeypatch):
     """C3 through the flow kernel (SAC_WIDE=1 SAC_WIDE_FLOW=1: phases A and C
