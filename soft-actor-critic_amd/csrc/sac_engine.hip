@@ -921,8 +921,13 @@ static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
   // B, 5 / 3 operand row sets) is also split into pi0_parts / q0_parts batch
   // parts with a granule hand-off (the critics' producer parts also hand over
   // their seeded bias sums): 2 parts measured D 8.3 -> 7.6 us on C2
-  const bool gsum_on = esz == 4;
-  int pi0_parts = 2, q0_parts = 2;
+  // bf16 too (SAC_GSUM_BF16=0: a block per dY part with a granule hand-off, the
+  // round-3 layout): the parts' bf16 dY added in fp32 and rounded once while staging
+  bool gsum_on = true;
+  if (const char* v = getenv("SAC_GSUM_BF16")) gsum_on = esz == 4 || atoi(v) != 0;
+  // (bf16: one block per summed tile -- 23.1K -> 23.6K steps/s on C2, B 7.0 -> 6.6,
+  // D 6.7 -> 6.2 us, profiles/r04_ab_gsum_bf16_c2.txt)
+  int pi0_parts = esz == 4 ? 2 : 1, q0_parts = esz == 4 ? 2 : 1;
   if (const char* v = getenv("SAC_PI0_PARTS")) pi0_parts = std::max(1, std::min(4, atoi(v)));
   if (const char* v = getenv("SAC_Q0_PARTS")) q0_parts = std::max(1, std::min(4, atoi(v)));
   // 64 x 64 update tiles (dw_adam_tile64) at large batches without the hidden

@@ -927,7 +927,6 @@ template <typename T, int UT, bool COH, int GS = 1, bool P = false, typename Wai
 __device__ __forceinline__ void dw_adam_tile(const AS_C EngineDev& E, const TileDesc* tdp_, bool polyak, int par,
                                              int par_x, lf* lds, const UpdStep* us = nullptr,
                                              const Wait& wait = Wait()) {
-  static_assert(GS == 1 || sizeof(T) == 4, "dY parts are summed in fp32 only");
   constexpr int KC = MM<T>::KC, KL = MM<T>::KL;
   constexpr int EPR = 16 / sizeof(T);  // elements per 16-B piece (= KL)
   constexpr int EPT = 1024 / UT;       // elements per thread
@@ -1094,10 +1093,26 @@ __device__ __forceinline__ void dw_adam_tile(const AS_C EngineDev& E, const Tile
             u32x4 v = rg[sl][op ? GS : 0][pi];
             if constexpr (GS > 1)
               if (op == 0) {  // dY: the parts' partials added in part order (fp32)
-                f32x4 a = __builtin_bit_cast(f32x4, v);
+                if constexpr (sizeof(T) == 4) {
+                  f32x4 a = __builtin_bit_cast(f32x4, v);
 #pragma unroll
-                for (int q = 1; q < GS; ++q) a += __builtin_bit_cast(f32x4, rg[sl][q][pi]);
-                v = __builtin_bit_cast(u32x4, a);
+                  for (int q = 1; q < GS; ++q) a += __builtin_bit_cast(f32x4, rg[sl][q][pi]);
+                  v = __builtin_bit_cast(u32x4, a);
+                } else {  // bf16: added in fp32, rounded to bf16 once
+                  bf16x8 h = __builtin_bit_cast(bf16x8, v);
+                  float a[8];
+#pragma unroll
+                  for (int e = 0; e < 8; ++e) a[e] = (float)h[e];
+#pragma unroll
+                  for (int q = 1; q < GS; ++q) {
+                    const bf16x8 hq = __builtin_bit_cast(bf16x8, rg[sl][q][pi]);
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) a[e] += (float)hq[e];
+                  }
+#pragma unroll
+                  for (int e = 0; e < 8; ++e) h[e] = (bf16)a[e];
+                  v = __builtin_bit_cast(u32x4, h);
+                }
               }
             if constexpr (sizeof(T) == 4)
               if (op == 0 && seedp) v = __builtin_bit_cast(u32x4, __builtin_bit_cast(f32x4, v) * sdr[sl][pi]);
@@ -1587,16 +1602,17 @@ __device__ __forceinline__ void dw_adam_tile64(const AS_C EngineDev& E, const Ti
   }
 }
 
-// a tile with summed dY parts (fp32 hidden-split layer 0) runs its own instance
+// a tile with summed dY parts (hidden-split layer 0) runs its own instance
 template <typename T, int UT, bool COH, bool P = false, typename Wait = NoWait>
 __device__ __forceinline__ void dw_adam_tile_any(const AS_C EngineDev& E, const TileDesc* tdp_, bool polyak, int par,
                                                  int par_x, lf* lds, const UpdStep* us = nullptr,
                                                  const Wait& wait = Wait()) {
   if constexpr (!P && UT == 1024)
     if (((const AS_C TileDesc*)tdp_)->tile64) return dw_adam_tile64<T, UT>(E, tdp_, polyak, par, par_x, lds);
-  if constexpr (sizeof(T) == 4) {
+  {
     const int gs = ((const AS_C TileDesc*)tdp_)->gsum;  // uniform
-    if (gs == 4) return dw_adam_tile<T, UT, COH, 4, P>(E, tdp_, polyak, par, par_x, lds, us, wait);
+    if constexpr (sizeof(T) == 4)
+      if (gs == 4) return dw_adam_tile<T, UT, COH, 4, P>(E, tdp_, polyak, par, par_x, lds, us, wait);
     if (gs == 2) return dw_adam_tile<T, UT, COH, 2, P>(E, tdp_, polyak, par, par_x, lds, us, wait);
   }
   dw_adam_tile<T, UT, COH, 1, P>(E, tdp_, polyak, par, par_x, lds, us, wait);
