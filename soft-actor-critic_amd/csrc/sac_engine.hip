@@ -936,6 +936,14 @@ static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
   int t64 = 0;
   if (const char* v = getenv("SAC_TILE64")) t64 = !split && Bp > 1024 && atoi(v) != 0;
   const int TS = t64 ? 64 : 32;
+  // the 32 x 32 tiles sum the bias gradient from their staged dY rows
+  // (TileDesc.bstage, 16-B LDS reads) instead of loading the row tiles' partials
+  // (at C3 256 strided loads per column made the k0 == 0 tiles the tail of
+  // phases B and D): C3 4.47K -> 4.57K fp32, 7.63K -> 8.0K bf16; C2 19.3K ->
+  // 19.5K fp32, 23.45K -> 24.0K bf16 (profiles/r04_ab_bias_staged.txt);
+  // SAC_BIAS_STAGED=0 keeps the partials
+  int bstage = 1;
+  if (const char* v = getenv("SAC_BIAS_STAGED")) bstage = atoi(v) != 0;
   const size_t part_stride = t64 ? SAC_PART_STRIDE64 : SAC_PART_STRIDE;
   auto ntiles_of = [&](const LayerDev& ly) { return ((ly.Np + TS - 1) / TS) * ((ly.Kp + TS - 1) / TS); };
   int tilesBD[2] = {0, 0};  // [critics (B), policy (D)]
@@ -1141,6 +1149,7 @@ static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
             const int bpl = (l == 0 && split) ? 2 * Bp : Bp;                     // X^T row stride
             const int bpg = (l == 0 && split) ? (ni == NET_PI ? wc : 2) * Bp : Bp;  // dY^T row stride
             t.tile64 = t64;
+            t.bstage = bstage;
             t.GT = (const char*)ly.GT + (size_t)nt * TS * bpg * esz2;
             t.XT = (const char*)ly.XT + (size_t)kt * TS * bpl * esz2;
             t.W = nd.P + ly.w_off;

@@ -193,6 +193,11 @@ struct TileDesc {
   long goff;
   int gsum;
   int tile64;      // a 64 x 64 tile (dw_adam_tile64: large batches, no hidden split)
+  // the bias gradient is summed from the staged dY rows (every batch part its
+  // own columns, handed over like the seeded sums) instead of from the row
+  // tiles' partials, whose strided loads (256 row tiles at C3) made the
+  // k0 == 0 tiles the phase's tail (the default; SAC_BIAS_STAGED=0 clears it)
+  int bstage;
   // fp32 split critics (every layer): dY^T holds the unit-seed backward (phase
   // A's critic roles store it without waiting for y); every batch column b is
   // scaled by seed[b] (phase A's first target-critic half computes the seeds)
@@ -1020,8 +1025,10 @@ __device__ __forceinline__ void dw_adam_tile(const AS_C EngineDev& E, const Tile
     }
   }
   const bool do_bias = td.k0 == 0 && td.kpart <= 1;
-  // the seeded bias gradient is summed from the staged rows: every part sums its own columns
-  const bool bias_acc = td.k0 == 0 && (td.kpart <= 1 || seedp);
+  // seeded or TileDesc.bstage: the bias gradient is summed from the staged rows,
+  // every part its own columns
+  const bool bst = seedp || td.bstage;  // uniform
+  const bool bias_acc = td.k0 == 0 && (td.kpart <= 1 || bst);
   float pb = 0.f, mb = 0.f, vb = 0.f, tbv = 0.f;
   if (do_bias && tid < 32 && td.n0 + tid < td.N) {
     pb = ldf<P>((const float*)td.b + td.n0 + tid);
@@ -1048,7 +1055,7 @@ __device__ __forceinline__ void dw_adam_tile(const AS_C EngineDev& E, const Tile
   for (int j = 0; j < BPT; ++j) {
     const int t = tid + j * UT, bn = t >> 4, bs = t & 15;
     bsum[j] = 0.f;
-    if (do_bias && !seedp && t < 512 && td.n0 + bn < td.N) {
+    if (do_bias && !bst && t < 512 && td.n0 + bn < td.N) {
       const AS_G float* dbp = GPC(float, td.dbp) + td.n0 + bn;
       for (int rt0 = bs; rt0 < td.nrt; rt0 += 16 * BU) {
         float pv[BU];
@@ -1121,12 +1128,24 @@ __device__ __forceinline__ void dw_adam_tile(const AS_C EngineDev& E, const Tile
         issue(r0 + rstep, slc);
         __syncthreads();
         if (r0 == 0 && sl == 0) STAMP(polyak ? 51 : 55);
-        if (seedp && bias_acc) {  // bias gradient: this lane's columns of the slot's scaled dY rows
+        if (bst && bias_acc) {  // bias gradient: this lane's columns of the slot's (scaled) dY rows
 #pragma unroll
           for (int j = 0; j < BPT; ++j) {
             const int t = tid + j * UT, bn = t >> 4, bs = t & 15;
-            if (t < 512)
-              for (int c = bs; c < bch; c += 16) bsum[j] += (float)stage[sl * slot_el + bn * lds_row + c];
+            if (t < 512)  // 16-B LDS reads: lane bs takes the row's 16-B pieces bs, bs + 16, ...
+              for (int c = bs * EPR; c < bch; c += 16 * EPR) {
+                const AS_L T* q = stage + sl * slot_el + bn * lds_row + c;
+                if constexpr (sizeof(T) == 4) {
+                  const f32x4 x = *(const AS_L f32x4*)q;
+                  bsum[j] += (x[0] + x[1]) + (x[2] + x[3]);
+                } else {
+                  const bf16x8 x = *(const AS_L bf16x8*)q;
+                  float s = 0.f;
+#pragma unroll
+                  for (int e = 0; e < 8; ++e) s += (float)x[e];
+                  bsum[j] += s;
+                }
+              }
           }
         }
 #pragma unroll
@@ -1177,7 +1196,7 @@ __device__ __forceinline__ void dw_adam_tile(const AS_C EngineDev& E, const Tile
     if (bias_acc && t < 512) red[(t >> 4) * 17 + (t & 15)] = bsum[j];
   }
   __syncthreads();
-  float gbx[3] = {0.f, 0.f, 0.f};  // seeded bias: the producer parts' column sums (consumer, tid < 32)
+  float gbx[3] = {0.f, 0.f, 0.f};  // staged-row bias: the producer parts' column sums (consumer, tid < 32)
   if (td.kpart) {  // hidden-split layer 0: the batch parts of this tile meet here
     const uint32_t ep = P ? us->ep : *GPC(uint32_t, E.sync) + 1u;  // per launch (B and D have their own granules)
     if (td.kpart >= 2) {
@@ -1186,7 +1205,7 @@ __device__ __forceinline__ void dw_adam_tile(const AS_C EngineDev& E, const Tile
         const uint64_t x = (uint64_t)__float_as_uint(accs[(el >> 5) * 33 + (el & 31)]) | ((uint64_t)ep << 32);
         __hip_atomic_store((uint64_t*)(mine + el), x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
-      if (seedp && bias_acc && tid < 32) {
+      if (bst && bias_acc && tid < 32) {
         float gb = 0.f;
         for (int q = 0; q < 16; ++q) gb += red[tid * 17 + q];
         const uint64_t x = (uint64_t)__float_as_uint(gb) | ((uint64_t)ep << 32);
@@ -1200,7 +1219,7 @@ __device__ __forceinline__ void dw_adam_tile(const AS_C EngineDev& E, const Tile
     constexpr int EL = 1024 / UT;
     static_assert(EL * UT == 1024 && EL <= 4, "granules per thread");
     const int np = td.nparts - 1;  // producer parts (1..3)
-    const bool pb_here = seedp && do_bias && tid < 32;
+    const bool pb_here = bst && do_bias && tid < 32;
     float v[3][EL];
     for (int it = 0;; ++it) {
       bool all = true;
@@ -1274,7 +1293,7 @@ __device__ __forceinline__ void dw_adam_tile(const AS_C EngineDev& E, const Tile
   if (do_bias && tid < 32 && td.n0 + tid < td.N) {
     float gb = 0.f;
     for (int q = 0; q < 16; ++q) gb += red[tid * 17 + q];
-    if (seedp && td.kpart) {  // the other batch parts' sums, in part order
+    if (bst && td.kpart) {  // the other batch parts' sums, in part order
 #pragma unroll
       for (int q = 0; q < 3; ++q)
         if (q < td.nparts - 1) gb += gbx[q];

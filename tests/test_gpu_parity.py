@@ -86,6 +86,18 @@ def test_c3_batch_part_counts_match_oracle(precision, parts, monkeypatch):
     test_baseline_config_matches_oracle("c3", 12_288, 2, precision)
 
 
+@pytest.mark.parametrize("name,batch,steps", [("c3", 12_288, 2), ("c2", 4096, 3)])
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_bias_gradient_sources_match_oracle(name, batch, steps, precision, monkeypatch):
+    """The update tiles' bias gradient from the row tiles' partial sums
+    (SAC_BIAS_STAGED=0; the default sums the staged dY rows) at C3 and C2,
+    against the oracle like test_baseline_config_matches_oracle."""
+    import bench
+
+    monkeypatch.setenv("SAC_BIAS_STAGED", "0")
+    _check_config_against_oracle(dict(bench.CONFIGS[name], capacity=batch), precision, steps, roles=name != "c3")
+
+
 @pytest.mark.parametrize("precision", ["fp32", "bf16"])
 def test_c3_stage_path_matches_oracle(precision, monkeypatch):
     """C3 through the layer-synchronous stage path (SAC_WIDE=1; the row-tile
