@@ -325,6 +325,8 @@ struct sac_engine {
   int nB = 0, nD = 0;
   size_t lds_bytes = 0;
   size_t upd_lds = 0;  // dynamic LDS of an update tile (SAC_UPD_LDS_FOR(upd_slots))
+  int upd_ut_b = SAC_UPD_THREADS;  // phase B's workgroup size (SAC_UPD_UT=512: two per CU, two slots)
+  size_t upd_lds_b = 0;
   int nrt = 0;
   int fused = 0;  // 0: A B C D per step; 1: D inside the next A's launch; 2: also B inside C's
   // persistent step (sac_persist.h): one launch of G workgroups per run of steps
@@ -1129,6 +1131,18 @@ static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
       e->h.upd_slots = std::min(4, (Bp + bch - 1) / bch);
       e->upd_lds = SAC_UPD_LDS_FOR(e->h.upd_slots);
       if (t64) e->upd_lds = std::max((size_t)SAC_UPD64_LDS, (size_t)5 * 1024 * 4);  // (the alpha block: 5 x 1024 floats)
+      // phase B in 2 rounds of 1024-thread blocks (C3: 480 blocks) -> 512-thread
+      // blocks with 2 slots, two per CU, one round: C3 B 37.0 -> 33.5 us fp32,
+      // 20.0 -> 18.1 bf16 (profiles/r04_ab_upd_ut512_c3.txt); SAC_UPD_UT=512 / 1024
+      // forces it (no summed layer-0 tiles: GS 1 only, so never with the hidden split)
+      int ut512 = nB > 256 && nB <= 512;
+      if (const char* v = getenv("SAC_UPD_UT")) ut512 = atoi(v) == 512;
+      e->upd_ut_b = SAC_UPD_THREADS;
+      e->upd_lds_b = e->upd_lds;
+      if (ut512 && !t64 && !split) {
+        e->upd_ut_b = 512;
+        e->upd_lds_b = SAC_UPD_LDS_FOR(std::min(2, e->h.upd_slots));
+      }
     }
     e->nrt = nrt;
     // self-contained update tiles (phase B: critics + Polyak, phase D: policy)
@@ -1419,6 +1433,7 @@ static void set_lds_attrs(size_t bytes) {
   (void)hipFuncSetAttribute((const void*)sac_target_critic_split<T>, hipFuncAttributeMaxDynamicSharedMemorySize, b);
   (void)hipFuncSetAttribute((const void*)sac_actor_split<T>, hipFuncAttributeMaxDynamicSharedMemorySize, b);
   (void)hipFuncSetAttribute((const void*)sac_critic_update<T>, hipFuncAttributeMaxDynamicSharedMemorySize, b);
+  (void)hipFuncSetAttribute((const void*)sac_critic_update<T, 512>, hipFuncAttributeMaxDynamicSharedMemorySize, b);
   (void)hipFuncSetAttribute((const void*)sac_actor_update<T>, hipFuncAttributeMaxDynamicSharedMemorySize, b);
   (void)hipFuncSetAttribute((const void*)sac_persist<T>, hipFuncAttributeMaxDynamicSharedMemorySize, b);
   (void)hipFuncSetAttribute((const void*)sac_wide_stage<T, WA_PLAIN, false>, hipFuncAttributeMaxDynamicSharedMemorySize, b);
@@ -1462,7 +1477,10 @@ static void launch_kind(sac_engine* e, int kind, const sac_replay* rb, const int
         sac_target_critic<T, false, false><<<e->nrt * e->h.xs, SAC_THREADS, lf, s>>>(e->d, *rb, idx, eps);
       break;
     case L_B:
-      sac_critic_update<T><<<e->nB, SAC_UPD_THREADS, e->upd_lds, s>>>(e->d, e->tilesB);
+      if (e->upd_ut_b == 512)
+        sac_critic_update<T, 512><<<e->nB, 512, e->upd_lds_b, s>>>(e->d, e->tilesB);
+      else
+        sac_critic_update<T><<<e->nB, SAC_UPD_THREADS, e->upd_lds, s>>>(e->d, e->tilesB);
       break;
     case L_C:
       if (e->h.split)

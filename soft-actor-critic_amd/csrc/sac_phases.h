@@ -928,7 +928,7 @@ __device__ __forceinline__ u32x4 opnd16(const void* base, uint32_t byte_off) {
                                                                           0, 16));
   return *(const AS_G u32x4*)((const AS_G char*)base + byte_off);
 }
-template <typename T, int UT, bool COH, int GS = 1, bool P = false, typename Wait = NoWait>
+template <typename T, int UT, bool COH, int GS = 1, bool P = false, int MS = 4, typename Wait = NoWait>
 __device__ __forceinline__ void dw_adam_tile(const AS_C EngineDev& E, const TileDesc* tdp_, bool polyak, int par,
                                              int par_x, lf* lds, const UpdStep* us = nullptr,
                                              const Wait& wait = Wait()) {
@@ -944,8 +944,12 @@ __device__ __forceinline__ void dw_adam_tile(const AS_C EngineDev& E, const Tile
   const int lds_row = SAC_UPD_BCH + 16 / (int)sizeof(T);  // +16 B per row: rows start on different banks
   AS_L T* stage = (AS_L T*)lds;
   const int nslot = E.upd_slots;
+  // slots (2 with summed dY parts: register room; MS: the kernel's cap), pieces
+  // per thread per operand (32 rows) per full chunk
+  constexpr int MAXS = GS > 1 ? (MS < 2 ? MS : 2) : MS, PPO = 32 * (SAC_UPD_BCH / EPR) / UT;
+  const int ns = nslot < MAXS ? nslot : MAXS;  // slots per round
   const int slot_el = 64 * lds_row;  // T elements per stage slot
-  lf* accs = lds + (nslot * slot_el * (int)sizeof(T) + 15) / 16 * 4;
+  lf* accs = lds + (ns * slot_el * (int)sizeof(T) + 15) / 16 * 4;
   lf* tgts = accs + 32 * 33;
   lf* red = tgts + 32 * 33;
   // this step's Adam scalars (written by phase A; persistent: the caller's)
@@ -954,11 +958,7 @@ __device__ __forceinline__ void dw_adam_tile(const AS_C EngineDev& E, const Tile
   // ---- 1. loads: the first round of staged operands, then element state + bias
   // state + bias partials, all before the first wait (one round trip; the bias
   // sums below wait for everything issued before them, in issue order)
-  // slots (2 with summed dY parts: register room), pieces per thread per operand
-  // (32 rows) per full chunk
-  constexpr int MAXS = GS > 1 ? 2 : 4, PPO = 32 * (SAC_UPD_BCH / EPR) / UT;
   static_assert(PPO >= 1 && (32 * (SAC_UPD_BCH / EPR)) % UT == 0, "whole pieces per thread");
-  const int ns = nslot < MAXS ? nslot : MAXS;  // slots per round
   const int rstep = ns * SAC_UPD_BCH;          // batch columns per round
   u32x4 rg[MAXS][GS + 1][PPO];                 // [slot][dY part 0..GS-1, then X][piece]
   const AS_G float* const seedp = sizeof(T) == 4 ? GPC(float, td.seed) : nullptr;  // uniform
@@ -1622,19 +1622,19 @@ __device__ __forceinline__ void dw_adam_tile64(const AS_C EngineDev& E, const Ti
 }
 
 // a tile with summed dY parts (hidden-split layer 0) runs its own instance
-template <typename T, int UT, bool COH, bool P = false, typename Wait = NoWait>
+template <typename T, int UT, bool COH, bool P = false, int MS = 4, typename Wait = NoWait>
 __device__ __forceinline__ void dw_adam_tile_any(const AS_C EngineDev& E, const TileDesc* tdp_, bool polyak, int par,
                                                  int par_x, lf* lds, const UpdStep* us = nullptr,
                                                  const Wait& wait = Wait()) {
   if constexpr (!P && UT == 1024)
     if (((const AS_C TileDesc*)tdp_)->tile64) return dw_adam_tile64<T, UT>(E, tdp_, polyak, par, par_x, lds);
-  {
+  if constexpr (MS >= 4) {  // (MS 2: the 512-thread phase B, never with the hidden split's summed tiles)
     const int gs = ((const AS_C TileDesc*)tdp_)->gsum;  // uniform
     if constexpr (sizeof(T) == 4)
-      if (gs == 4) return dw_adam_tile<T, UT, COH, 4, P>(E, tdp_, polyak, par, par_x, lds, us, wait);
-    if (gs == 2) return dw_adam_tile<T, UT, COH, 2, P>(E, tdp_, polyak, par, par_x, lds, us, wait);
+      if (gs == 4) return dw_adam_tile<T, UT, COH, 4, P, MS>(E, tdp_, polyak, par, par_x, lds, us, wait);
+    if (gs == 2) return dw_adam_tile<T, UT, COH, 2, P, MS>(E, tdp_, polyak, par, par_x, lds, us, wait);
   }
-  dw_adam_tile<T, UT, COH, 1, P>(E, tdp_, polyak, par, par_x, lds, us, wait);
+  dw_adam_tile<T, UT, COH, 1, P, MS>(E, tdp_, polyak, par, par_x, lds, us, wait);
 }
 
 // One block: reduces the step's loss partials into stats[0..3] and runs the
@@ -2712,14 +2712,16 @@ __global__ void __launch_bounds__(SAC_THREADS) sac_actor(const EngineDev* __rest
 }
 
 // ============================================================================ phases B / D kernels
-template <typename T>
-__global__ void __launch_bounds__(SAC_UPD_THREADS) sac_critic_update(const EngineDev* __restrict__ Ep,
+// UT = 512 (SAC_UPD_UT=512): two slots per round and at most 128 VGPRs, so two
+// workgroups share a CU (SAC_UPD_LDS_FOR(2) = 76 KB each)
+template <typename T, int UT = SAC_UPD_THREADS>
+__global__ void __launch_bounds__(UT, UT == 512 ? 4 : 1) sac_critic_update(const EngineDev* __restrict__ Ep,
                                                          const TileDesc* __restrict__ tiles) {
   const AS_C EngineDev& E = *(const AS_C EngineDev*)Ep;
   extern __shared__ float upd_lds[];
   // critic tiles: one X^T copy (xt_par = 0), so their operand loads need not wait for the step's parity
-  dw_adam_tile_any<T, SAC_UPD_THREADS, false>(E, tiles + blockIdx.x, true, (int)(*GPC(uint64_t, E.rng_step) & 1), 0,
-                                          (lf*)upd_lds);
+  dw_adam_tile_any<T, UT, false, false, UT == 512 ? 2 : 4>(E, tiles + blockIdx.x, true,
+                                                          (int)(*GPC(uint64_t, E.rng_step) & 1), 0, (lf*)upd_lds);
   END_STAMP(62);  // standalone: the launch boundary publishes (no counter)
 }
 

@@ -98,6 +98,18 @@ def test_bias_gradient_sources_match_oracle(name, batch, steps, precision, monke
     _check_config_against_oracle(dict(bench.CONFIGS[name], capacity=batch), precision, steps, roles=name != "c3")
 
 
+@pytest.mark.parametrize("precision,parts", [("fp32", None), ("bf16", None), ("fp32", "4")])
+def test_c3_update_block_sizes_match_oracle(precision, parts, monkeypatch):
+    """C3's phase B with the 1024-thread update tiles (SAC_UPD_UT=1024; C3's
+    default runs its 480 B blocks as 512-thread tiles, two per CU), default
+    batch parts, and the 512-thread tiles at 4 parts (640 blocks, two rounds),
+    against the oracle like test_baseline_config_matches_oracle."""
+    monkeypatch.setenv("SAC_UPD_UT", "512" if parts else "1024")
+    if parts:
+        monkeypatch.setenv("SAC_BPARTS", parts)
+    test_baseline_config_matches_oracle("c3", 12_288, 2, precision)
+
+
 @pytest.mark.parametrize("precision", ["fp32", "bf16"])
 def test_c3_stage_path_matches_oracle(precision, monkeypatch):
     """C3 through the layer-synchronous stage path (SAC_WIDE=1; the row-tile
