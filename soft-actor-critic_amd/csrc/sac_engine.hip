@@ -327,6 +327,8 @@ struct sac_engine {
   size_t upd_lds = 0;  // dynamic LDS of an update tile (SAC_UPD_LDS_FOR(upd_slots))
   int upd_ut_b = SAC_UPD_THREADS;  // phase B's workgroup size (SAC_UPD_UT=512: two per CU, two slots)
   size_t upd_lds_b = 0;
+  int upd_ut_d = SAC_UPD_THREADS;  // phase D's (SAC_UPD_UT_D=512)
+  size_t upd_lds_d = 0;
   int nrt = 0;
   int fused = 0;  // 0: A B C D per step; 1: D inside the next A's launch; 2: also B inside C's
   // persistent step (sac_persist.h): one launch of G workgroups per run of steps
@@ -967,7 +969,16 @@ static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
     }
     return best;
   };
-  const int bpartsB = batch_parts(tilesBD[0], 0), bpartsD = batch_parts(tilesBD[1], 1);
+  // phase D as 512-thread tiles, two per CU (SAC_UPD_UT_D=512, opt-in): up to 8
+  // batch parts within 512 blocks (SAC_BPARTS_D overrides)
+  int ut512_d = 0;
+  if (const char* v = getenv("SAC_UPD_UT_D")) ut512_d = !split && !t64 && Bp > 1024 && atoi(v) == 512;
+  const int bpartsB = batch_parts(tilesBD[0], 0);
+  int bpartsD = batch_parts(tilesBD[1], 1);
+  if (ut512_d) {
+    bpartsD = std::max(1, std::min(8, 511 / std::max(tilesBD[1], 1)));
+    if (const char* v = getenv("SAC_BPARTS_D")) bpartsD = std::max(1, std::min(8, atoi(v)));
+  }
   auto tile_parts = [&](int ni, int l) {
     if (l == 0 && split) return gsum_on ? std::min(ni == NET_PI ? pi0_parts : q0_parts, Bp / 32) : ni == NET_PI ? wc : 2;
     return ni == NET_PI ? bpartsD : bpartsB;
@@ -1143,6 +1154,9 @@ static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
         e->upd_ut_b = 512;
         e->upd_lds_b = SAC_UPD_LDS_FOR(std::min(2, e->h.upd_slots));
       }
+      e->upd_ut_d = ut512_d ? 512 : SAC_UPD_THREADS;
+      e->upd_lds_d = ut512_d ? std::max((size_t)SAC_UPD_LDS_FOR(std::min(2, e->h.upd_slots)), (size_t)5 * 512 * 4)
+                             : e->upd_lds;
     }
     e->nrt = nrt;
     // self-contained update tiles (phase B: critics + Polyak, phase D: policy)
@@ -1435,6 +1449,7 @@ static void set_lds_attrs(size_t bytes) {
   (void)hipFuncSetAttribute((const void*)sac_critic_update<T>, hipFuncAttributeMaxDynamicSharedMemorySize, b);
   (void)hipFuncSetAttribute((const void*)sac_critic_update<T, 512>, hipFuncAttributeMaxDynamicSharedMemorySize, b);
   (void)hipFuncSetAttribute((const void*)sac_actor_update<T>, hipFuncAttributeMaxDynamicSharedMemorySize, b);
+  (void)hipFuncSetAttribute((const void*)sac_actor_update<T, 512>, hipFuncAttributeMaxDynamicSharedMemorySize, b);
   (void)hipFuncSetAttribute((const void*)sac_persist<T>, hipFuncAttributeMaxDynamicSharedMemorySize, b);
   (void)hipFuncSetAttribute((const void*)sac_wide_stage<T, WA_PLAIN, false>, hipFuncAttributeMaxDynamicSharedMemorySize, b);
   (void)hipFuncSetAttribute((const void*)sac_wide_stage<T, WA_ACT, false>, hipFuncAttributeMaxDynamicSharedMemorySize, b);
@@ -1491,7 +1506,10 @@ static void launch_kind(sac_engine* e, int kind, const sac_replay* rb, const int
         sac_actor<T, false, false><<<e->nrt * e->h.xs + stg, SAC_THREADS, lf, s>>>(e->d, *rb);
       break;
     case L_D:
-      sac_actor_update<T><<<e->nD + 1, SAC_UPD_THREADS, e->upd_lds, s>>>(e->d, e->tilesD, e->nD);
+      if (e->upd_ut_d == 512)
+        sac_actor_update<T, 512><<<e->nD + 1, 512, e->upd_lds_d, s>>>(e->d, e->tilesD, e->nD);
+      else
+        sac_actor_update<T><<<e->nD + 1, SAC_UPD_THREADS, e->upd_lds, s>>>(e->d, e->tilesD, e->nD);
       break;
     case L_DA:
       sac_target_critic<T, true, true><<<e->nD + 1 + e->nrt * 6, SAC_THREADS, lf, s>>>(e->d, *rb, idx, eps);

@@ -1196,7 +1196,11 @@ __device__ __forceinline__ void dw_adam_tile(const AS_C EngineDev& E, const Tile
     if (bias_acc && t < 512) red[(t >> 4) * 17 + (t & 15)] = bsum[j];
   }
   __syncthreads();
-  float gbx[3] = {0.f, 0.f, 0.f};  // staged-row bias: the producer parts' column sums (consumer, tid < 32)
+  // producer parts a consumer takes (the 512-thread tiles: up to 7, else 3)
+  constexpr int MAXP = MS == 2 ? 7 : 3;
+  float gbx[MAXP];  // staged-row bias: the producer parts' column sums (consumer, tid < 32)
+#pragma unroll
+  for (int q = 0; q < MAXP; ++q) gbx[q] = 0.f;
   if (td.kpart) {  // hidden-split layer 0: the batch parts of this tile meet here
     const uint32_t ep = P ? us->ep : *GPC(uint32_t, E.sync) + 1u;  // per launch (B and D have their own granules)
     if (td.kpart >= 2) {
@@ -1218,13 +1222,13 @@ __device__ __forceinline__ void dw_adam_tile(const AS_C EngineDev& E, const Tile
     // per element); parts are added in order
     constexpr int EL = 1024 / UT;
     static_assert(EL * UT == 1024 && EL <= 4, "granules per thread");
-    const int np = td.nparts - 1;  // producer parts (1..3)
+    const int np = td.nparts - 1;  // producer parts (1..MAXP)
     const bool pb_here = bst && do_bias && tid < 32;
-    float v[3][EL];
+    float v[MAXP][EL];
     for (int it = 0;; ++it) {
       bool all = true;
 #pragma unroll
-      for (int q = 0; q < 3; ++q)
+      for (int q = 0; q < MAXP; ++q)
         if (q < np) {
 #pragma unroll
           for (int j = 0; j < EL; ++j) {
@@ -1253,7 +1257,7 @@ __device__ __forceinline__ void dw_adam_tile(const AS_C EngineDev& E, const Tile
       const int el = tid + j * UT, o = (el >> 5) * 33 + (el & 31);
       float sum = accs[o];
 #pragma unroll
-      for (int q = 0; q < 3; ++q)
+      for (int q = 0; q < MAXP; ++q)
         if (q < np) sum += v[q][j];
       accs[o] = sum;
     }
@@ -1295,7 +1299,7 @@ __device__ __forceinline__ void dw_adam_tile(const AS_C EngineDev& E, const Tile
     for (int q = 0; q < 16; ++q) gb += red[tid * 17 + q];
     if (bst && td.kpart) {  // the other batch parts' sums, in part order
 #pragma unroll
-      for (int q = 0; q < 3; ++q)
+      for (int q = 0; q < MAXP; ++q)
         if (q < td.nparts - 1) gb += gbx[q];
     }
     const float pbn = adam_elem(pb, mb, vb, gb, w1, b2, w2, bc2s, eps, neg_step);
@@ -2725,14 +2729,14 @@ __global__ void __launch_bounds__(UT, UT == 512 ? 4 : 1) sac_critic_update(const
   END_STAMP(62);  // standalone: the launch boundary publishes (no counter)
 }
 
-template <typename T>
-__global__ void __launch_bounds__(SAC_UPD_THREADS) sac_actor_update(const EngineDev* __restrict__ Ep, const TileDesc* __restrict__ tiles,
-                                                        int ntiles) {
+template <typename T, int UT = SAC_UPD_THREADS>
+__global__ void __launch_bounds__(UT, UT == 512 ? 4 : 1) sac_actor_update(const EngineDev* __restrict__ Ep,
+                                                                         const TileDesc* __restrict__ tiles, int ntiles) {
   const AS_C EngineDev& E = *(const AS_C EngineDev*)Ep;
   const int par = (int)((*GPC(uint64_t, E.rng_step) - 1) & 1);  // phase C already advanced the step
   extern __shared__ float upd_lds[];
   if ((int)blockIdx.x < ntiles)
-    dw_adam_tile_any<T, SAC_UPD_THREADS, false>(E, tiles + blockIdx.x, false, par, par, (lf*)upd_lds);
+    dw_adam_tile_any<T, UT, false, false, UT == 512 ? 2 : 4>(E, tiles + blockIdx.x, false, par, par, (lf*)upd_lds);
   else
     alpha_and_losses(E, par, (lf*)upd_lds);
   END_STAMP(63);  // standalone: the launch boundary publishes (no counter)

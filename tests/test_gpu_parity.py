@@ -110,6 +110,17 @@ def test_c3_update_block_sizes_match_oracle(precision, parts, monkeypatch):
     test_baseline_config_matches_oracle("c3", 12_288, 2, precision)
 
 
+@pytest.mark.parametrize("precision,parts", [("fp32", None), ("bf16", None), ("fp32", "8")])
+def test_c3_half_size_policy_update_blocks_match_oracle(precision, parts, monkeypatch):
+    """C3's phase D as 512-thread update tiles (SAC_UPD_UT_D=512: up to 8 batch
+    parts, 7 producer parts per consumer; default 6 and 8 parts), against the
+    oracle like test_baseline_config_matches_oracle."""
+    monkeypatch.setenv("SAC_UPD_UT_D", "512")
+    if parts:
+        monkeypatch.setenv("SAC_BPARTS_D", parts)
+    test_baseline_config_matches_oracle("c3", 12_288, 2, precision)
+
+
 @pytest.mark.parametrize("precision", ["fp32", "bf16"])
 def test_c3_stage_path_matches_oracle(precision, monkeypatch):
     """C3 through the layer-synchronous stage path (SAC_WIDE=1; the row-tile
