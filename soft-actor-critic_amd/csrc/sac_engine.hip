@@ -1000,7 +1000,8 @@ static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
   WideLay wl;
   {
     int roles_pre = 6 * nrt0 <= 256 && SAC_ROWS * (A + 1) <= SAC_HAND_STRIDE;
-    if (const char* v = getenv("SAC_ROLES")) roles_pre = roles_pre && atoi(v) != 0;
+    if (const char* v = getenv("SAC_ROLES"))
+      roles_pre = atoi(v) == 2 ? SAC_ROWS * (A + 1) <= SAC_HAND_STRIDE : roles_pre && atoi(v) != 0;
     const bool too_big = !(roles_pre ? lds_fits_roles : lds_fits_rows);
     const bool able = !split && c->q_layers >= 3 && c->pi_layers >= 3 && 2 * A <= WJMAX;
     int on = able && too_big;
@@ -1065,8 +1066,13 @@ static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
   // tile kernels run pi on [s'; s] (2R rows); with roles every MLP pass is R rows.
   // The stage path (wl.on) launches none of them but policy_act: R rows, no
   // pre-activation buffers.
+  // SAC_ROLES=2: the role kernels past co-residency (6 nrt > 256 blocks).  Every
+  // role waits only for roles of LOWER block ids (phase A: pi(s') < Qt < critics;
+  // phase C: critics < pi), so in-order dispatch still guarantees progress: a
+  // spinning block's producers were dispatched before it.
   int roles = 6 * nrt <= 256 && SAC_ROWS * (A + 1) <= SAC_HAND_STRIDE;
-  if (const char* v = getenv("SAC_ROLES")) roles = roles && atoi(v) != 0;
+  if (const char* v = getenv("SAC_ROLES"))
+    roles = atoi(v) == 2 ? SAC_ROWS * (A + 1) <= SAC_HAND_STRIDE : roles && atoi(v) != 0;
   roles = roles && !wl.on;
   const int lo = lds_layout(h, wl.on || roles ? SAC_ROWS : 2 * SAC_ROWS, !wl.on);
 

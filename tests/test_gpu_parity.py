@@ -122,6 +122,17 @@ def test_c3_half_size_policy_update_blocks_match_oracle(precision, parts, monkey
 
 
 @pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_c3_forced_role_kernels_match_oracle(precision, monkeypatch):
+    """C3 through the per-network role kernels past co-residency (SAC_ROLES=2:
+    6 x 256 phase-A blocks, progress by in-order dispatch), against the oracle
+    like test_baseline_config_matches_oracle."""
+    import bench
+
+    monkeypatch.setenv("SAC_ROLES", "2")
+    _check_config_against_oracle(dict(bench.CONFIGS["c3"], capacity=12_288), precision, 2, roles=True)
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
 def test_c3_stage_path_matches_oracle(precision, monkeypatch):
     """C3 through the layer-synchronous stage path (SAC_WIDE=1; the row-tile
     kernels are C3's default), against the oracle like
