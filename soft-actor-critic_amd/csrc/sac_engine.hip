@@ -1075,6 +1075,15 @@ static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
     roles = atoi(v) == 2 ? SAC_ROWS * (A + 1) <= SAC_HAND_STRIDE : roles && atoi(v) != 0;
   roles = roles && !wl.on;
   const int lo = lds_layout(h, wl.on || roles ? SAC_ROWS : 2 * SAC_ROWS, !wl.on);
+  // with the bias gradients summed from the update tiles' staged rows nobody reads
+  // the row tiles' partials: the phase kernels skip them (store_T, dbp == null).
+  // The 64 x 64 tiles read them and the stage path writes them unconditionally.
+  // (SAC_DBP_SKIP=0 keeps the stores: A/B)
+  int dbp_skip = bstage && !t64 && !wl.on;
+  if (const char* v = getenv("SAC_DBP_SKIP")) dbp_skip = dbp_skip && atoi(v) != 0;
+  if (dbp_skip)
+    for (int ni = 0; ni < 5; ++ni)
+      for (int l = 0; l < h.net[ni].L; ++l) h.net[ni].l[l].dbp = nullptr;
 
   if (e) {
     h.B = B;

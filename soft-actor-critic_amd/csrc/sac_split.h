@@ -790,7 +790,7 @@ __device__ __forceinline__ void target_critic_split_body(const EngineDev* __rest
         __syncthreads();
         store_T<T, R, P>(g2, ldo, L2.Np, L2.N, L2.GT, Bp, r0, nvalid, L2.dbp, qtB);
       }
-      store_T<T, R, P>(U1, ldu1, HH, HH, (T*)L1.GT + (size_t)h * HH * Bp, Bp, r0, nvalid, L1.dbp + h * HH, qtB, L1.N);
+      store_T<T, R, P>(U1, ldu1, HH, HH, (T*)L1.GT + (size_t)h * HH * Bp, Bp, r0, nvalid, L1.dbp ? L1.dbp + h * HH : nullptr, qtB, L1.N);
       store_T<T, R, P>(Xb, ld, L0.Np, L0.N, L0.GT, 2 * Bp, h * Bp + r0, nvalid, L0.dbp, qtB);
     }
     STAMP(11 + 2 * qi);
@@ -1203,7 +1203,7 @@ __device__ __forceinline__ void actor_split_body(const EngineDev* __restrict__ E
   });
   if (act != ACT_RELU && act != ACT_ID) act_pass_bwd<R>(U1, ldu1, P1, ldp1, HH >> 4, HH, act);
   __syncthreads();
-  store_T<T, R, P>(U1, ldu1, HH, HH, (T*)L1.GT + (size_t)h * HH * Bp, Bp, r0, nvalid, L1.dbp + h * HH, nullptr, L1.N);
+  store_T<T, R, P>(U1, ldu1, HH, HH, (T*)L1.GT + (size_t)h * HH * Bp, Bp, r0, nvalid, L1.dbp ? L1.dbp + h * HH : nullptr, nullptr, L1.N);
   // dY0 partial = act'(P0) * (dY1 W1[half])
   gemm_hs<T, 2, NCH_HH, false>(U1, ldu1, wt1, &ht1, [&](int j, int col, const f32x4& acc) {
     const bool kv = col < L1.K;
