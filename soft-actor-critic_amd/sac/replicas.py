@@ -21,7 +21,13 @@ import torch
 
 # order of the replica metric vector, host (aggregate_metrics) and
 # device (metric_vector / replica_train / ReplicaAggregator) forms alike
-METRICS = ("steps", "wall_s", "q1_loss", "q2_loss", "policy_loss", "alpha_loss", "alpha", "mean_return")
+# mean_return is reduced over the ranks that have finished an episode only:
+# the vector carries the return (0 on a rank without one) and the 0/1 flag
+# "return_ranks", so one slow rank's NaN does not hide the other ranks'
+# returns; the host view divides by the flag count (None while it is 0)
+METRICS = ("steps", "wall_s", "q1_loss", "q2_loss", "policy_loss", "alpha_loss", "alpha", "mean_return",
+           "return_ranks")
+I_RET, I_NRET = METRICS.index("mean_return"), METRICS.index("return_ranks")
 REPLICA_METRICS = METRICS
 
 
@@ -52,15 +58,24 @@ def aggregate_metrics(values: Sequence[float], group=None, device: Optional[torc
     return {"sum": s.tolist(), "mean": (s / world).tolist(), "max": m.tolist(), "world": world}
 
 
-def metric_vector(engine, wall_s: float = 0.0, mean_return: float = float("nan")) -> torch.Tensor:
+def metric_vector(engine, wall_s: float = 0.0, mean_return: float = float("nan"),
+                  steps: Optional[int] = None) -> torch.Tensor:
     """METRICS of the engine's last step as a float64 device tensor: the step
     counter, losses and alpha come from the engine's own buffers by device ops
     (no host read); the host scalars wall_s and mean_return enter as fill
-    kernels (torch.full: a kernel argument, not a copy), so nothing waits."""
+    kernels (torch.full: a kernel argument, not a copy), so nothing waits.
+    engine None (a learner that never built the HIP engine, e.g. no gradient
+    step was due yet): a host vector with the loop's step count ``steps`` and
+    NaN losses and alpha."""
+    has_ret = math.isfinite(mean_return)
+    ret = [float(mean_return) if has_ret else 0.0, 1.0 if has_ret else 0.0]
+    if engine is None:
+        nan = float("nan")
+        return torch.tensor([float(steps or 0), float(wall_s), nan, nan, nan, nan, nan] + ret, dtype=torch.float64)
     dev = engine.stats.device
     host = lambda x: torch.full((1,), float(x), dtype=torch.float64, device=dev)  # noqa: E731
     return torch.cat([engine.rng_step.double().reshape(1), host(wall_s), engine.stats[:4].double(),
-                      engine.alpha_state[1:2].double(), host(mean_return)])
+                      engine.alpha_state[1:2].double(), host(ret[0]), host(ret[1])])
 
 
 def aggregate_device(v: torch.Tensor, group=None) -> Tuple[torch.Tensor, torch.Tensor]:
@@ -70,6 +85,8 @@ def aggregate_device(v: torch.Tensor, group=None) -> Tuple[torch.Tensor, torch.T
     import torch.distributed as dist
 
     s, m = v.clone(), v.clone()
+    # the max of mean_return runs over the ranks that have one: -inf elsewhere
+    m[I_RET] = torch.where(v[I_NRET] > 0, v[I_RET], torch.full_like(v[I_RET], -math.inf))
     dist.all_reduce(s, op=dist.ReduceOp.SUM, group=group)
     dist.all_reduce(m, op=dist.ReduceOp.MAX, group=group)
     return s, m
@@ -115,8 +132,15 @@ class ReplicaAggregator:
         self.last: dict = {}
 
     def _aggregate(self, st: dict) -> None:
-        v = metric_vector(self.engine, time.perf_counter() - self.t0, st.get("avg_return", float("nan")))
-        self.aggs.append(aggregate_device(v, self.group) if _initialised() else (v, v))
+        v = metric_vector(self.engine, time.perf_counter() - self.t0, st.get("avg_return", float("nan")),
+                          steps=st.get("gradient_steps", 0))
+        if _initialised():
+            self.aggs.append(aggregate_device(v, self.group))
+        else:
+            m = v.clone()
+            if m[I_NRET] <= 0:
+                m[I_RET] = -math.inf
+            self.aggs.append((v, m))
 
     def __call__(self, st: dict) -> None:
         self.last = st
@@ -140,8 +164,14 @@ def summarise_aggregates(aggs, world: int, every: int) -> dict:
     s, m = aggs[-1]
     s, m = s.tolist(), m.tolist()
     fin = lambda xs: [x if math.isfinite(x) else None for x in xs]  # noqa: E731  (JSON: no NaN)
+    mean = [x / world for x in s]
+    n_ret = s[I_NRET]
+    # mean_return: over the ranks that have finished an episode
+    mean[I_RET] = s[I_RET] / n_ret if n_ret > 0 else float("nan")
+    if n_ret <= 0:
+        s[I_RET] = float("nan")
     return {"every": every, "aggregations": len(aggs), "world": world, "fields": list(REPLICA_METRICS),
-            "last_sum": fin(s), "last_mean": fin([x / world for x in s]), "last_max": fin(m)}
+            "last_sum": fin(s), "last_mean": fin(mean), "last_max": fin(m)}
 
 
 def timed_region(run, sync, device: Optional[torch.device] = None, group=None) -> float:

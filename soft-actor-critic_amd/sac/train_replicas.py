@@ -84,6 +84,14 @@ def train_replica(config: dict, make_env: Callable[[], object], num_envs: int, e
         lg["agent_name"] = f"{lg['agent_name']}_rank{rank}"  # per-replica run directories
     vec = vec_env_cls([make_env] * num_envs)
     agent = agent_cls(vec, cfg)
+    if getattr(agent, "engine", None) is None:
+        # no HIP engine (no MI355X visible, or train.engine_device: cpu): the
+        # learner cannot step and there is no CPU fallback -- say so here,
+        # before the loop, instead of failing inside it
+        from sac import _engine as E
+
+        raise E.EngineUnavailable(f"replica {rank}: replica training needs the HIP engine on an MI355X "
+                                  f"(train.device={cfg['train'].get('device')!r}); there is no CPU fallback")
     agg = ReplicaAggregator(agent.engine, every)
     metrics = agent.run_vectorized_training_loop(env_steps, callback=agg, seed=cfg["train"]["seed"])
     return {"metrics": metrics, "aggregate": agg.finish()}
@@ -102,17 +110,15 @@ def main(argv=None) -> int:
     with open(a.config) as f:
         config = yaml.safe_load(f)
     rank, world, local = rank_env()
-    device = None
+    if not torch.cuda.is_available():
+        raise SystemExit("train_replicas: no HIP device visible; replica training runs the HIP engine, one "
+                         "process per MI355X (there is no CPU fallback)")
+    device = f"cuda:{local}"
     if world > 1:
         import torch.distributed as dist
 
-        backend = "nccl" if torch.cuda.is_available() else "gloo"
-        if backend == "nccl":
-            torch.cuda.set_device(local)
-            device = f"cuda:{local}"
-        dist.init_process_group(backend)
-    elif torch.cuda.is_available():
-        device = "cuda:0"
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")  # RCCL on ROCm: the metric all-reduce only
     try:
         out = train_replica(config, env_factory(a.env), a.num_envs, a.env_steps, a.aggregate_every, rank, device)
     finally:

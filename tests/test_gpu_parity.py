@@ -16,6 +16,7 @@ import numpy as np
 import pytest
 import torch
 
+import _ties
 from _fixtures import CONFIGS, batch, eps, oracle_state
 from oracle import sac_oracle as O
 
@@ -281,40 +282,6 @@ def test_stage_path_is_used_where_the_phase_kernels_do_not_fit(shape, monkeypatc
     assert all(np.isfinite(eng.losses()))
 
 
-def _relu_ties(mlp, x, rel=1e-7):
-    """Does a hidden ReLU pre-activation of this forward sit within fp32
-    summation-order noise of 0?  |p| <= rel * (|W| |x| + |b|): its sign -- and
-    so the unit's whole backward for that row -- then depends on the order of
-    the fp32 sum, and a correct fp32 engine may decide it the other way from
-    the numpy oracle.  tools/debug/pi0_grad.py found one at [512, 512], B = 384,
-    step 2 (profiles/r04_debug_wide512_relu_tie.txt): pi layer 1, one row,
-    pre-activation 5.8e-8; the engine's pi layer-0 gradient differed from
-    float64 by exactly that row's rank-one term (singular values 3.7e-4 vs
-    1e-8).  The stage path and round 3's role variant both decided it the same way."""
-    h = np.asarray(x, np.float64)
-    for i in range(len(mlp.W) - 1):
-        W, b = mlp.W[i].astype(np.float64), mlp.b[i].astype(np.float64)
-        p = h @ W.T + b
-        if np.any(np.abs(p) <= rel * (np.abs(h) @ np.abs(W).T + np.abs(b))):
-            return True
-        h = np.maximum(p, 0.0)
-    return False
-
-
-def _tied_nets(st, bt):
-    """Networks whose element-fraction check a ReLU tie of this step voids (the
-    max-error bound still applies): pi on the actor rows s, each critic (and its
-    target) on the batch (s, a)."""
-    tied = set()
-    if _relu_ties(st.pi, bt.s):
-        tied.add("policy")
-    sa = np.concatenate([bt.s, bt.a], 1)
-    for k, net in (("q1", st.q1), ("q2", st.q2)):
-        if _relu_ties(net, sa):
-            tied |= {k, k + "t"}
-    return tied
-
-
 def _engine_mlp(eng, key):
     """Oracle MLP holding the engine's current parameters of one network."""
     return O.MLP.from_state_dict({kk: v.detach().cpu().numpy().copy() for kk, v in eng.nets[key].state_dict().items()},
@@ -322,6 +289,20 @@ def _engine_mlp(eng, key):
 
 
 def _check_config_against_oracle(c, precision, steps, roles=None, traj_tol=1e-4):
+    """`steps` engine steps of config c against two oracles, with injected
+    indices and eps:
+      the trajectory oracle, started from the engine's initial state and run
+        on its own from there (losses, y, log pi, log alpha, parameter bounds,
+        and in fp32 >= 99.5% of every network's elements within 1e-6);
+      fp32 only, the local oracle, loaded with the engine's FULL state before
+        each step (tests/test_gpu_parity.py::_oracle_state_from_engine): the
+        losses to 1e-5 rel and >= 99.9% of every network's post-step elements
+        within 1e-6, free of trajectory drift.
+    fp32 steps are drawn tie-free from both states (tests/_ties.py: the rows of
+    any summation-order tie -- a ReLU pre-activation within fp32 noise of 0 on
+    any pass, a min-Q near-tie of the actor pass -- get a fresh index and eps
+    until none is left), so the element checks hold on all five networks at
+    every shape; the test prints how many rows it redrew and the ties seen."""
     import bench
 
     ckey = "_parity_" + c.get("name", "cfg")
@@ -344,17 +325,19 @@ def _check_config_against_oracle(c, precision, steps, roles=None, traj_tol=1e-4)
     rtol = 1e-4 if precision == "fp32" else 2e-3 * max(1.0, (256 / B) ** 0.5)
     lrs = {"policy": hp.actor_lr, "q1": hp.critic_lr, "q2": hp.critic_lr, "q1t": hp.critic_lr * hp.tau,
            "q2t": hp.critic_lr * hp.tau}
-    tied = set()
+    fp32 = precision == "fp32"
     for k in range(1, steps + 1):
-        idx = g.choice(len(rb), size=B, replace=False).astype(np.int32)
-        et = g.standard_normal((B, A)).astype(np.float32)
-        ea = g.standard_normal((B, A)).astype(np.float32)
-        bt = O.Batch(rows["obs"][idx], rows["act"][idx], rows["rew"][idx], rows["next_obs"][idx], rows["done"][idx])
-        # the engine's own pre-step state, for the one-step (local) check of y and log pi
+        # the engine's own pre-step state: the local oracle (fp32), y / log pi one step from it
+        loc = _oracle_state_from_engine(eng, A) if fp32 else None
         pre = {n: _engine_mlp(eng, n) for n in ("pi", "q1t", "q2t")}
         alpha_pre = np.float32(eng.alpha_state[1].item())
-        tied |= _tied_nets(st, bt)  # once the trajectories split at a tie they stay split
-        ref = O.training_step(st, hp, bt, et, ea)
+        idx, et, ea, bt, outs, redrawn, seen = _ties.tie_free_draw(g, rows, len(rb), B, A, hp,
+                                                                    [st, loc] if fp32 else [])
+        if fp32:
+            print(f"[ties] {ckey} step {k}: {redrawn} rows redrawn, ties seen {seen}")
+            (ref, st), (ref_loc, post_loc) = outs
+        else:
+            ref = O.training_step(st, hp, bt, et, ea)
         eng.train(rb, 1, indices=torch.from_numpy(idx).reshape(1, B),
                   eps=torch.from_numpy(np.stack([et, ea])).reshape(1, 2, B, A))
         torch.cuda.synchronize()
@@ -368,14 +351,19 @@ def _check_config_against_oracle(c, precision, steps, roles=None, traj_tol=1e-4)
             assert _loss_ok(gv, w, fl, rtol), (ckey, precision, k, i, gv, w)
         y = eng.last_targets().cpu().numpy()
         lp = eng.last_log_pi().cpu().numpy()
-        if precision == "fp32":
+        if fp32:
             # one step from the engine's own state: the kernels' arithmetic alone
-            _, lp_loc, _ = O.policy_sample(pre["pi"], bt.s, ea, hp.policy)
-            a2, lp2, _ = O.policy_sample(pre["pi"], bt.s2, et, hp.policy)
-            mq = np.minimum(O.q_forward(pre["q1t"], bt.s2, a2)[0], O.q_forward(pre["q2t"], bt.s2, a2)[0])
-            y_loc = (bt.r + (np.float32(hp.gamma) * (np.float32(1) - bt.d)) * (mq - alpha_pre * lp2)).astype(np.float32)
-            np.testing.assert_allclose(y, y_loc, rtol=1e-4, atol=1e-4)
-            np.testing.assert_allclose(lp, lp_loc, rtol=1e-4, atol=1e-4)
+            np.testing.assert_allclose(y, ref_loc["y"], rtol=1e-4, atol=1e-4)
+            np.testing.assert_allclose(lp, ref_loc["log_pi"], rtol=1e-4, atol=1e-4)
+            fl_loc = float(np.mean(np.abs(loc.alpha * ref_loc["log_pi"])) + np.mean(np.abs(ref_loc["y"])))
+            for i, (gv, w) in enumerate(zip(got, ref_loc["losses"])):
+                assert abs(gv - w) <= 1e-5 * max(abs(w), fl_loc if i == 2 else 1e-3), (ckey, "local", k, i, gv, w)
+            for n, net in (("pi", post_loc.pi), ("q1", post_loc.q1), ("q2", post_loc.q2), ("q1t", post_loc.q1t),
+                           ("q2t", post_loc.q2t)):
+                mine = {kk: v.detach().cpu().numpy() for kk, v in eng.nets[n].state_dict().items()}
+                for pk, want in net.state_dict().items():
+                    d = np.abs(mine[pk] - want)
+                    assert np.mean(d <= 1e-6) >= 0.999, (ckey, "local", k, n, pk, np.mean(d <= 1e-6))
             # against the oracle's own trajectory: from step 2 on, an Adam update
             # whose gradient is ~0 may take the other sign under another
             # summation order (that element moves +-lr instead of -+lr, inside
@@ -395,7 +383,7 @@ def _check_config_against_oracle(c, precision, steps, roles=None, traj_tol=1e-4)
             for pk, want in _oracle_net(st, key).state_dict().items():
                 d = np.abs(mine[pk] - want)
                 assert d.max() <= 2 * lr + 1e-5, (c.get('name'), precision, k, key, pk, d.max())
-                if precision == "fp32" and key not in tied:
+                if fp32:  # every network: the step was drawn tie-free
                     assert np.mean(d <= 1e-6) >= 0.995, (c.get('name'), k, key, pk, np.mean(d <= 1e-6))
                 ds.append(d.ravel())
             if precision == "bf16":
@@ -457,13 +445,10 @@ def test_one_step_from_the_engine_state(shape, monkeypatch):
     g = np.random.default_rng(11)
     lrs = {"pi": hp.actor_lr, "q1": hp.critic_lr, "q2": hp.critic_lr, "q1t": hp.critic_lr, "q2t": hp.critic_lr}
     for k in range(1, 5):
-        idx = g.choice(len(rb), size=B, replace=False).astype(np.int32)
-        et = g.standard_normal((B, A)).astype(np.float32)
-        ea = g.standard_normal((B, A)).astype(np.float32)
         st = _oracle_state_from_engine(eng, A)
-        bt = O.Batch(rows["obs"][idx], rows["act"][idx], rows["rew"][idx], rows["next_obs"][idx], rows["done"][idx])
-        tied = {{"policy": "pi"}.get(n, n) for n in _tied_nets(st, bt)}  # this step only: the state is reloaded
-        ref = O.training_step(st, hp, bt, et, ea)
+        idx, et, ea, bt, outs, redrawn, seen = _ties.tie_free_draw(g, rows, len(rb), B, A, hp, [st])
+        print(f"[ties] {shape} step {k}: {redrawn} rows redrawn, ties seen {seen}")
+        (ref, post), = outs
         eng.train(rb, 1, indices=torch.from_numpy(idx).reshape(1, B),
                   eps=torch.from_numpy(np.stack([et, ea])).reshape(1, 2, B, A))
         torch.cuda.synchronize()
@@ -471,12 +456,11 @@ def test_one_step_from_the_engine_state(shape, monkeypatch):
         floor = float(np.mean(np.abs(st.alpha * ref["log_pi"])) + np.mean(np.abs(ref["y"])))
         for i, (gv, w) in enumerate(zip(eng.losses(), ref["losses"])):
             assert abs(gv - w) <= 1e-5 * max(abs(w), floor if i == 2 else 1e-3), (shape, k, i, gv, w)
-        for n, net in (("pi", st.pi), ("q1", st.q1), ("q2", st.q2), ("q1t", st.q1t), ("q2t", st.q2t)):
+        for n, net in (("pi", post.pi), ("q1", post.q1), ("q2", post.q2), ("q1t", post.q1t), ("q2t", post.q2t)):
             mine = {kk: v.detach().cpu().numpy() for kk, v in eng.nets[n].state_dict().items()}
             for pk, want in net.state_dict().items():
                 d = np.abs(mine[pk] - want)
                 assert d.max() <= 2 * lrs[n], (shape, k, n, pk, d.max())
-                if n not in tied:
-                    assert np.mean(d <= 1e-6) >= 0.999, (shape, k, n, pk, np.mean(d <= 1e-6))
-        assert abs(float(eng.alpha_state[0].item()) - st.log_alpha) <= 1e-7
+                assert np.mean(d <= 1e-6) >= 0.999, (shape, k, n, pk, np.mean(d <= 1e-6))
+        assert abs(float(eng.alpha_state[0].item()) - post.log_alpha) <= 1e-7
     eng.check()

@@ -52,4 +52,4 @@ def test_replica_aggregation_gloo(world):
         assert agg["mean"][2] == pytest.approx(1.5)           # losses averaged
         assert tput == pytest.approx(3000.0 / 3.0)            # total steps / slowest replica
         assert seeds == [42, 43]                              # distinct replica seeds
-    assert len(METRICS) == 8
+    assert len(METRICS) == 9 and METRICS[7] == "mean_return"

@@ -108,3 +108,81 @@ def test_replica_seed_and_logger_name_per_rank():
     train_replica(cfg, lambda: None, 2, 10, 1000, rank=3, agent_cls=Rec, vec_env_cls=_StubVecEnv)
     assert seen == {"seed": 45, "name": "SAC_rank3"}
     assert cfg["train"]["seed"] == 42  # the caller's config is not modified
+
+
+class _NoEngineAgent(_StubAgent):
+    """A rank whose learner never built the engine (an agent on a host without
+    a HIP device): the loop ran no gradient step and the engine is None."""
+
+    def __init__(self, vec_env, config):
+        super().__init__(vec_env, config)
+        self.engine = None
+
+
+def test_real_agent_on_cpu_is_refused_clearly():
+    """The real sac.agent.SAC on a host without a GPU (engine None): train_replica
+    raises EngineUnavailable up front, not an AttributeError from the
+    aggregator."""
+    import copy
+
+    from _fixtures import load
+    from sac import _engine as E
+
+    _, meta = load("c1_auto")
+    cfg = copy.deepcopy(meta["cfg"])
+    cfg["train"]["device"] = "cpu"
+    cfg["train"]["engine_device"] = "cpu"
+    cfg["logger"]["enabled"] = False
+    from sac.train_replicas import train_replica
+
+    with pytest.raises(E.EngineUnavailable, match="no CPU fallback"):
+        train_replica(cfg, __import__("sac.train_replicas", fromlist=["env_factory"]).env_factory("point_mass"),
+                      num_envs=2, env_steps=8, every=4, rank=0)
+
+
+def test_aggregator_without_engine_and_without_returns():
+    """ReplicaAggregator with no engine builds the metric vector from the loop's
+    host counters (NaN losses), and a rank without a finished episode leaves
+    mean_return out of the reduction instead of turning it NaN."""
+    from sac.replicas import ReplicaAggregator
+
+    agg = ReplicaAggregator(None, every=4)
+    agg({"env_steps": 8, "gradient_steps": 8, "episodes": 0, "avg_return": float("nan")})
+    out = agg.finish()
+    f = list(METRICS)
+    assert out["aggregations"] == 2
+    assert out["last_sum"][f.index("steps")] == 8
+    assert out["last_sum"][f.index("q1_loss")] is None
+    assert out["last_sum"][f.index("mean_return")] is None and out["last_max"][f.index("mean_return")] is None
+    assert out["last_sum"][f.index("return_ranks")] == 0
+
+
+def _worker_uneven(rank, world, port, out):
+    """Rank 1 has not finished an episode (avg_return NaN): the aggregate's
+    mean_return is rank 0's alone, not NaN."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from sac.replicas import ReplicaAggregator
+
+        agg = ReplicaAggregator(_StubEngine(rank), every=4)
+        agg({"env_steps": 8, "gradient_steps": 8, "episodes": 1 - rank,
+             "avg_return": 7.0 if rank == 0 else float("nan")})
+        out[rank] = agg.finish()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_mean_return_over_ranks_with_episodes():
+    world = 2
+    port = _free_port()
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_worker_uneven, args=(world, port, out), nprocs=world, join=True)
+    f = list(METRICS)
+    for r in range(world):
+        a = out[r]
+        assert a["last_mean"][f.index("mean_return")] == pytest.approx(7.0)
+        assert a["last_max"][f.index("mean_return")] == pytest.approx(7.0)
+        assert a["last_sum"][f.index("return_ranks")] == 1
+        assert a["last_mean"][f.index("q1_loss")] == pytest.approx(1.5)
