@@ -82,7 +82,9 @@ def synthetic_replay(rb, cap, obs, act, seed):
     torch.cuda.synchronize()
 
 
-def build_engine(cfgname, precision, seed, device, capacity=None):
+def build_engine(cfgname, precision, seed, device, capacity=None, layout=None):
+    """Engine + synthetic replay of a CONFIGS entry.  ``layout``: kernel layout
+    overrides for the tests (sac.engine.SacEngine); None = the engine's choice."""
     from sac.engine import SacEngine
     from sac.models import PolicyNetwork, QNetwork
     from sac.replay_buffer import ReplayBuffer
@@ -99,7 +101,7 @@ def build_engine(cfgname, precision, seed, device, capacity=None):
     # notebooks/configs/bipedal_walker.yaml:4-38 with auto_entropy_tuning on
     eng = SacEngine(pi, q1, q2, q1t, q2t, batch_size=c["batch"], gamma=0.99, tau=0.005, actor_lr=3e-4,
                     critic_lr=3e-4, alpha_lr=3e-4, alpha=0.1, auto_entropy_tuning=True, device=device,
-                    precision=precision, seed=seed)
+                    precision=precision, seed=seed, layout=layout)
     rb = ReplayBuffer(c["capacity"], device=device, obs_dim=c["obs"], act_dim=c["act"])
     synthetic_replay(rb, c["capacity"], c["obs"], c["act"], seed)
     return eng, rb, c
@@ -391,6 +393,9 @@ def main():
     ap.add_argument("--no-sweep", action="store_true")
     ap.add_argument("--no-bf16", action="store_true")
     ap.add_argument("--no-c3", action="store_true", help="skip the C3 (B = 4096) legs of the c2 line")
+    ap.add_argument("--layout", default="", help="A/B runs only: kernel layout overrides of the headline leg, "
+                    "'key=value,...' over sac._engine.LAYOUT_KEYS (e.g. layout=rows,upd_parts=4); default: "
+                    "the engine's own choice")
     args = ap.parse_args()
 
     if args.gpus < 1:
@@ -433,6 +438,11 @@ def run_rank(args, world, rank, local):
     chunk = max(1, min(args.chunk, args.steps))
     every = args.aggregate_every
 
+    layout = {}
+    for kv in filter(None, args.layout.split(",")):
+        k, v = kv.split("=")
+        layout[k] = v if k == "layout" else int(v)
+
     def timed(precision, cfgname, steps=None, warmup=None):
         steps = args.steps if steps is None else steps
         warmup = args.warmup if warmup is None else warmup
@@ -440,7 +450,7 @@ def run_rank(args, world, rank, local):
             c = dict(CONFIGS[cfgname])
             eng, rb = _StubEngine(c["batch"], rank), None
         else:
-            eng, rb, c = build_engine(cfgname, precision, seed, device)
+            eng, rb, c = build_engine(cfgname, precision, seed, device, layout=layout or None)
             # capture (+ upload) the chunk graph first (runs no step): its host-side work
             # would otherwise leave the device idle between the warm-up and the timed region
             eng.train_graph(rb, 0, chunk)
@@ -480,6 +490,8 @@ def run_rank(args, world, rank, local):
                    "global_batch": c["batch"] * world, "parallelism": f"replicas{world}",
                    "graph_chunk": chunk, "device_prewarm_s": args.prewarm},
     }
+    if layout:
+        line["config"]["layout_override"] = layout  # an A/B run, not the engine's own choice
     if stub:
         line["stub"] = "SAC_BENCH_STUB=1: rank/launcher logic only, no engine"
     else:
@@ -541,10 +553,6 @@ def measure_phases(args, eng, rb, c, elapsed, sps_one):
     ev_cost = max((sum(phase_ms) - step_ms) / max(sum(nl), 1), 0.0)
     kern_ms = [x - ev_cost * n if x > 0 else 0.0 for x, n in zip(phase_ms, nl)]
     flops, f_total, _, _ = gemm_flops(c["obs"], c["act"], c["hidden"], c["batch"])
-    if eng.fused:  # D inside the next A launch (and with layout 2, B inside the C launch)
-        flops = [flops[0] + flops[3], flops[1], flops[2], 0]
-        if eng.fused == 2:
-            flops = [flops[0], 0, flops[2] + flops[1], 0]
     dom = int(np.argmax(phase_ms))
     lib = E.load_library()
     kname = lib.sac_phase_kernel_name(dom).decode()

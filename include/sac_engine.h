@@ -84,7 +84,23 @@ typedef struct sac_engine_config {
   float target_entropy;                     /* -act_dim (agent.py:43) */
   int32_t precision;                        /* enum sac_precision */
   uint64_t seed;                            /* device RNG (replay indices, eps) */
+  /* Kernel layout overrides.  0 everywhere = the engine's own choice: what the
+   * drop-in classes pass and what every measured number uses.  The other
+   * values exist for the parity tests and A/B runs; every setting computes the
+   * same step (fp32 summation order aside).  The library reads no environment. */
+  int32_t layout;        /* enum sac_layout */
+  int32_t stage_path;    /* 0: only where the phase kernels' LDS layout does not fit;
+                            1: force the layer-synchronous stage path; -1: refuse it (create fails) */
+  int32_t stage_batch;   /* 0: phase C gathers the next step's batch; -1: phase A gathers its own */
+  int32_t upd_parts;     /* 0: cost model; 1..4: batch parts of the large-batch (B > 1024) update tiles */
+  int32_t upd_threads;   /* 0: auto; 512 / 1024: workgroup size of phase B's large-batch update tiles */
 } sac_engine_config;
+
+enum sac_layout {         /* phase A / C workgroup layouts (sac_engine_config.layout) */
+  SAC_LAYOUT_AUTO = 0,    /* hidden-split role kernels where they apply, else roles, else row tiles */
+  SAC_LAYOUT_ROLES = 1,   /* one workgroup per (network role, row tile): no hidden split */
+  SAC_LAYOUT_ROWS = 2     /* one workgroup per row tile running every network */
+};
 
 /* Caller-owned device state of one learner. */
 typedef struct sac_engine_buffers {
@@ -191,10 +207,7 @@ int sac_replay_sample_gather(const sac_replay *rb, int32_t batch, uint64_t seed,
  * the same way (diagnostic: an event + dispatch pair alone).  Each interval
  * includes its event's cost; bench.py removes it using the event-free graph
  * step time.  The sequence is queued behind a spin kernel, so the intervals are
- * device time, not host-submission time.
- * Fused layouts (sac_engine_phase_layout()): 1 = D shares the next step's A
- * launch ([0] is that launch, [3] = 0); 2 = also B shares C's launch ([1] = 0).
- * Synchronises the stream. */
+ * device time, not host-submission time.  Synchronises the stream. */
 int sac_engine_time_phases(sac_engine *e, const sac_replay *rb, int32_t n_steps,
                            float *ms_host, void *stream);
 
@@ -218,11 +231,6 @@ int sac_engine_check(sac_engine *e, void *stream);
  * no per-step synchronisation).  sac_engine_clear_status resets the flag. */
 int sac_engine_read_status(sac_engine *e, uint32_t *host_dst, void *stream);
 int sac_engine_clear_status(sac_engine *e, void *stream);
-
-/* Launch layout of a step: 0 = four launches (A B C D); 1 = phase D of step
- * k runs inside phase A's launch of step k + 1 (three launches); 2 = also phase
- * B inside phase C's launch (two launches). */
-int sac_engine_phase_layout(const sac_engine *e);
 
 /* Phase kernel names as they appear in rocprofv3 kernel traces. */
 const char *sac_phase_kernel_name(int32_t phase);

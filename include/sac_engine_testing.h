@@ -12,8 +12,8 @@ extern "C" {
  * ([grid][64]); only builds with -DSAC_STAMPS write them. */
 int sac_engine_debug_stamps(sac_engine *e, long long *dev_buf, void *stream);
 int sac_engine_debug_stamped(void);
-/* Launch ONE phase kernel of the current step (kind: 0 A, 1 B, 2 C, 3 D, 4 A
- * with D inside, 5 C with B inside) on the stream.  Timing experiments only:
+/* Launch ONE phase kernel of the current step (kind: 0 A, 1 B, 2 C, 3 D) on
+ * the stream.  Timing experiments only:
  * re-running a phase out of sequence advances or corrupts the training state. */
 int sac_engine_debug_launch(sac_engine* e, const sac_replay* rb, int32_t kind, void* stream);
 /* The last step whose phase A took its batch from the record phase C staged
@@ -25,10 +25,6 @@ int sac_engine_uses_roles(const sac_engine *e);
 /* 1 if phases A/C run the hidden-split role kernels (sac_split.h: two
  * workgroups per role and row tile, each with half of the 256-wide layer 1). */
 int sac_engine_uses_split(const sac_engine *e);
-/* Workgroups of the fused-step launch (sac_persist.h: the four phases of a
- * step in ONE launch, counters between them) when the engine uses it, else 0
- * (four launches per step). */
-int sac_engine_uses_fused_step(const sac_engine *e);
 /* Launches per gradient step of the large-batch stage path (sac_wide.h:
  * layer-synchronous GEMM stages for phases A and C, used where the per-network
  * role kernels do not fit), else 0. */
@@ -41,7 +37,7 @@ int sac_engine_phase_launches(const sac_engine *e, int32_t *out);
  * of the Philox-keyed Feistel permutation of [0, size) for RNG (seed, step). */
 int sac_debug_sample_indices_host(int64_t size, int32_t batch, uint64_t seed, uint64_t step, int32_t *out);
 /* Host evaluation of the device eps draws of one step (the same inline
- * philox_normal2 the fused step calls in its default device-RNG mode, compiled
+ * philox_normal2 the phase kernels call in their default device-RNG mode, compiled
  * for the host): out[which][b][j], which = 0 the target rsample (agent.py:204),
  * 1 the actor rsample (agent.py:241), rows b < batch, action dims j < act_dim
  * (models.py:83: eps of rsample).  Counter (step, b, which << 16 | j / 2), key

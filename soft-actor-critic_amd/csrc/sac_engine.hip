@@ -34,7 +34,6 @@
 
 #include "sac_phases.h"
 #include "sac_split.h"
-#include "sac_persist.h"
 #include "sac_wide.h"
 
 // ============================================================================ params / replay
@@ -304,8 +303,7 @@ static int fail(int code, const std::string& msg) {
 // Workspace offsets of the large-batch stage path (sac_wide.h), from plan()
 struct WideLay {
   int on = 0, Brw = 0, hp = 0, hq = 0;
-  int flow = 0;  // the flow kernel (one persistent launch per phase A / C)
-  size_t o_dev = 0, o_jobs = 0, o_cnt = 0;
+  size_t o_dev = 0, o_jobs = 0;
   size_t o_xpi0 = 0, o_xq0 = 0, o_xqt0 = 0, o_xc0 = 0, o_r = 0, o_d = 0, o_lp2 = 0, o_piop = 0;
   size_t o_outpi = 0, o_outq[2] = {0, 0}, o_outqt[2] = {0, 0}, o_outc[2] = {0, 0}, o_da[2] = {0, 0};
   size_t o_P[5][SAC_DEV_LAYERS] = {};      // phase A pre-activations (pi on [s'; s], Q1, Q2, Q1t, Q2t)
@@ -327,15 +325,8 @@ struct sac_engine {
   size_t upd_lds = 0;  // dynamic LDS of an update tile (SAC_UPD_LDS_FOR(upd_slots))
   int upd_ut_b = SAC_UPD_THREADS;  // phase B's workgroup size (SAC_UPD_UT=512: two per CU, two slots)
   size_t upd_lds_b = 0;
-  int upd_ut_d = SAC_UPD_THREADS;  // phase D's (SAC_UPD_UT_D=512)
-  size_t upd_lds_d = 0;
   int nrt = 0;
-  int fused = 0;  // 0: A B C D per step; 1: D inside the next A's launch; 2: also B inside C's
-  // persistent step (sac_persist.h): one launch of G workgroups per run of steps
-  int persist = 0;
-  int ncu = 256;  // compute units of the device (the persistent grid's bound)
-  int G = 0;
-  std::vector<PTask> hostP;
+  int ncu = 256;  // compute units of the device
   // large-batch stage path (sac_wide.h): layout offsets, stages, jobs
   WideLay wl;
   int wide = 0;
@@ -344,10 +335,9 @@ struct sac_engine {
   WJob* wjobs = nullptr;
   std::vector<WJob> hostW;
   struct WStage {
-    int kind;   // 0 gather, 1 GEMM jobs [j0, j1), 2 pi heads, 3 phase B, 4 phase D, 5 flow launch of jobs [j0, j1)
-    int j0, j1, grid, phase, last;  // grid: workgroups (kind 5: items)
+    int kind;   // 0 gather, 1 GEMM jobs [j0, j1), 2 pi heads, 3 phase B, 4 phase D
+    int j0, j1, grid, phase, last;  // grid: workgroups
     size_t lds;
-    int G;      // kind 5: resident workgroups launched (create())
   };
   std::vector<WStage> wst;
   // graph cache
@@ -389,13 +379,16 @@ static int validate(const sac_engine_config* c) {
   for (int a : acts)
     if (a < 0 || a > 6) return fail(SAC_E_INVALID, "bad activation code");
   if (c->precision != SAC_PREC_FP32 && c->precision != SAC_PREC_BF16) return fail(SAC_E_INVALID, "bad precision");
+  if (c->layout < SAC_LAYOUT_AUTO || c->layout > SAC_LAYOUT_ROWS || c->stage_path < -1 || c->stage_path > 1 ||
+      c->stage_batch < -1 || c->stage_batch > 0 || c->upd_parts < 0 || c->upd_parts > 4 ||
+      (c->upd_threads != 0 && c->upd_threads != 512 && c->upd_threads != 1024))
+    return fail(SAC_E_INVALID, "bad layout override (layout 0..2, stage_path -1..1, stage_batch -1..0, "
+                               "upd_parts 0..4, upd_threads 0 / 512 / 1024)");
   return SAC_OK;
 }
 
 // Lays out everything; when e != nullptr also fills e->h pointers (base = workspace).
 static void xcd_order(std::vector<TileDesc>& tiles);
-static void plan_persist(sac_engine* e, int esz);
-static bool xcd_order_parts(std::vector<TileDesc>& tiles, int P);
 
 
 // The large-batch path's device descriptor, jobs and stage list (sac_wide.h):
@@ -445,18 +438,15 @@ static void build_wide(sac_engine* e, char* base) {
   W.GTpi_out = np.l[hp].GT;
   W.dbppi_out = np.l[hp].dbp;
   W.rng_step = e->buf.rng_step;
-  W.cnt = (uint32_t*)(base + wl.o_cnt);
   W.stamp_stage = -1;
+#ifdef SAC_STAMPS  // diagnostic build only: the stage that writes stamps (tools/wide_stamps.py)
   if (const char* v = getenv("SAC_WIDE_STAMP_STAGE")) W.stamp_stage = atoi(v);
+#endif
   e->wdd = (WideDev*)(base + wl.o_dev);
   e->wjobs = (WJob*)(base + wl.o_jobs);
   std::vector<WJob>& JB = e->hostW;
   JB.clear();
   e->wst.clear();
-  struct JTag {
-    int kind, ni, d, phase;  // kind 0 forward, 1 backward, 2 pi heads, 3 gather
-  };
-  std::vector<JTag> tags;  // one per job of JB, in order
   // the two K-block buffers + the epilogue's weight slices (WWS floats); WA_OUTBWD
   // adds the row seeds and the output layer's weights
   // K-block buffers: as many (2..4) as keep the stage's workgroups co-resident
@@ -481,9 +471,8 @@ static void build_wide(sac_engine* e, char* base) {
         break;
       }
     for (WJob& j : js) j.nbuf = nb;
-    for (size_t k = tags.size() - js.size(); k < tags.size(); ++k) tags[k].phase = phase;
     const size_t lf = nb * kbuf + extra;
-    sac_engine::WStage st{1, (int)JB.size(), (int)(JB.size() + js.size()), item, phase, last, lf * 4, 0};
+    sac_engine::WStage st{1, (int)JB.size(), (int)(JB.size() + js.size()), item, phase, last, lf * 4};
     e->wst.push_back(st);
     JB.insert(JB.end(), js.begin(), js.end());
   };
@@ -493,7 +482,6 @@ static void build_wide(sac_engine* e, char* base) {
     const LayerDev& ly = nd.l[l];
     WJob j;
     memset(&j, 0, sizeof(j));
-    tags.push_back(JTag{0, ni, l, -1});
     j.M = M;
     j.K = ly.K;
     j.Kp = ly.Kp;
@@ -537,7 +525,6 @@ static void build_wide(sac_engine* e, char* base) {
     const LayerDev& lo = nd.l[nd.L - 1];
     WJob j;
     memset(&j, 0, sizeof(j));
-    tags.push_back(JTag{1, ni, d, -1});
     j.M = M;
     j.K = ly.N;
     j.Kp = ly.Np;
@@ -584,7 +571,7 @@ static void build_wide(sac_engine* e, char* base) {
     return j;
   };
   auto add = [&](int kind, int grid, int phase) {
-    sac_engine::WStage st{kind, 0, 0, grid, phase, 0, 0, 0};
+    sac_engine::WStage st{kind, 0, 0, grid, phase, 0, 0};
     e->wst.push_back(st);
   };
   // ---- phase A
@@ -653,105 +640,6 @@ static void build_wide(sac_engine* e, char* base) {
     stage_gemm(js, 2, d == 1);
   }
   add(4, 0, 3);  // phase D
-  if (!wl.flow) return;
-
-  // ---- flow launches (sac_wide_flow): phase A's gather row blocks, GEMM items
-  // and pi head row blocks as one launch, phase C's GEMM items as another; each
-  // job waits per row block for the jobs whose outputs it reads
-  std::vector<WJob> FA, FC;
-  std::vector<JTag> TA, TC;
-  {
-    WJob g;
-    memset(&g, 0, sizeof(g));
-    g.amode = WA_GATHER;
-    g.M = Brw;
-    g.nrb = Brw / 64;
-    g.ncb = 1;
-    FA.push_back(g);
-    TA.push_back(JTag{3, -1, 0, 0});
-  }
-  for (const sac_engine::WStage& st : e->wst) {
-    if (st.kind == 2) {
-      WJob hj;
-      memset(&hj, 0, sizeof(hj));
-      hj.amode = WA_HEAD;
-      hj.M = 2 * Brw;
-      hj.nrb = 2 * Brw / 64;
-      hj.ncb = 1;
-      FA.push_back(hj);
-      TA.push_back(JTag{2, NET_PI, 0, 0});
-    } else if (st.kind == 1) {
-      for (int k = st.j0; k < st.j1; ++k) {
-        (st.phase == 0 ? FA : FC).push_back(JB[k]);
-        (st.phase == 0 ? TA : TC).push_back(tags[k]);
-      }
-    }
-  }
-  // (kbuf: the K-block buffer size above)
-  const size_t glds_f = (size_t)((WGR * (O + A) + 1) & ~1) + WGR * 2;  // the gather's LDS, floats
-  size_t cnt_off = 0, lf = glds_f;
-  auto finish = [&](std::vector<WJob>& F, std::vector<JTag>& T) {
-    auto find = [&](int kind, int ni, int d) {
-      for (size_t k = 0; k < T.size(); ++k)
-        if (T[k].kind == kind && (kind >= 2 || (T[k].ni == ni && T[k].d == d))) return (int)k;
-      fprintf(stderr, "sac_engine: internal: flow producer %d/%d/%d not planned\n", kind, ni, d);
-      abort();
-      return -1;
-    };
-    int item = 0;
-    for (size_t k = 0; k < F.size(); ++k) {
-      WJob& j = F[k];
-      const JTag& t = T[k];
-      j.item0 = item;
-      item += j.nrb * j.ncb;
-      j.cnt_off = (int)cnt_off;
-      cnt_off += j.nrb;
-      j.nbuf = 2;
-      std::vector<int> deps;
-      const bool critic = t.ni == NET_Q1 || t.ni == NET_Q2;
-      if (t.kind == 0) {
-        if (t.d > 0) deps.push_back(find(0, t.ni, t.d - 1));
-        else if (t.phase == 0) deps.push_back(t.ni == NET_Q1T || t.ni == NET_Q2T ? find(2, 0, 0) : find(3, 0, 0));
-      } else if (t.kind == 2) {
-        deps.push_back(find(0, NET_PI, hp - 1));
-      } else if (t.kind == 1) {
-        const int top = (t.ni == NET_PI ? hp : hq) - 1;
-        if (t.d < top) {
-          deps.push_back(find(1, t.ni, t.d + 1));
-        } else if (t.phase == 0) {  // y: target critics' outputs, this critic's output (and log pi' via Qt)
-          deps.push_back(find(0, t.ni, hq - 1));
-          deps.push_back(find(0, NET_Q1T, hq - 1));
-          deps.push_back(find(0, NET_Q2T, hq - 1));
-        } else if (critic) {  // min-Q weights: both critics' outputs
-          deps.push_back(find(0, NET_Q1, hq - 1));
-          deps.push_back(find(0, NET_Q2, hq - 1));
-        } else {  // pi head backward: both critics' d a~ partials (their layer-1 backward)
-          deps.push_back(find(1, NET_Q1, 1));
-          deps.push_back(find(1, NET_Q2, 1));
-        }
-      }
-      j.ndep = (int)deps.size();
-      for (int q = 0; q < j.ndep; ++q) {
-        j.dep_job[q] = deps[q];
-        j.dep_need[q] = F[deps[q]].ncb;
-      }
-      if (j.amode <= WA_OUTBWD) {
-        size_t x = 2 * kbuf + WWS;
-        if (j.amode == WA_OUTBWD) x += 64 * WLDD + (size_t)j.J * j.Kp;
-        lf = std::max(lf, x);
-      }
-    }
-    return item;
-  };
-  const int ia = finish(FA, TA), ic = finish(FC, TC);
-  JB.clear();
-  JB.insert(JB.end(), FA.begin(), FA.end());
-  JB.insert(JB.end(), FC.begin(), FC.end());
-  e->wst.clear();
-  e->wst.push_back(sac_engine::WStage{5, 0, (int)FA.size(), ia, 0, 0, lf * 4, 0});
-  e->wst.push_back(sac_engine::WStage{3, 0, 0, 0, 1, 0, 0, 0});
-  e->wst.push_back(sac_engine::WStage{5, (int)FA.size(), (int)JB.size(), ic, 2, 1, lf * 4, 0});
-  e->wst.push_back(sac_engine::WStage{4, 0, 0, 0, 3, 0, 0, 0});
 }
 
 static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
@@ -840,8 +728,7 @@ static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
               c->pi_dims[1] == SPLIT_H && c->pi_dims[2] == SPLIT_H && c->pi_out_act == SAC_ACT_IDENTITY &&
               2 * A <= 32 && (10 + split_wpi(esz)) * nrt0 <= 256 && (3 * split_wc(esz) + 1) * nrt0 <= 256 &&
               SAC_ROWS * (A + 1) <= SAC_HAND_STRIDE;
-  if (const char* v = getenv("SAC_SPLIT")) split = split && atoi(v) != 0;
-  if (const char* v = getenv("SAC_ROLES")) split = split && atoi(v) != 0;
+  split = split && c->layout == SAC_LAYOUT_AUTO;
   // batch columns of layer 0's operands under the split: X^T 2 Bp (phase A's two
   // halves store it), dY^T 2 Bp for the critics (phase A halves), split_wc Bp for
   // pi (phase C parts)
@@ -887,8 +774,9 @@ static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
         }
         const int bpg = (l == 0 && is_pi) ? bp0_pi : bpl;
         ly.GT = P(lay.take((size_t)ly.Np * bpg * esz));
-        // bias-gradient partials: one row per row tile (split layer 0: per part and row tile)
-        ly.dbp = (float*)P(lay.take((size_t)(l == 0 && split ? bpg / SAC_ROWS : nrt) * ly.N * 4));
+        // the update tiles sum the bias gradient from their staged dY^T rows:
+        // no per-row-tile partials (TileDesc / store_T with dbp == null)
+        ly.dbp = nullptr;
       }
       if (is_pi) ly.pstash = (float*)P(lay.take((size_t)Br * ly.Np * 4));
     }
@@ -922,44 +810,26 @@ static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
   // seeded bias sums of TileDesc.seed rely on that; bf16: a block per dY part
   // with a granule hand-off to part 1
   // fp32 split layer 0 (wc / 2 summed dY parts: the longest tiles of phases D /
-  // B, 5 / 3 operand row sets) is also split into pi0_parts / q0_parts batch
-  // parts with a granule hand-off (the critics' producer parts also hand over
-  // their seeded bias sums): 2 parts measured D 8.3 -> 7.6 us on C2
-  // bf16 too (SAC_GSUM_BF16=0: a block per dY part with a granule hand-off, the
-  // round-3 layout): the parts' bf16 dY added in fp32 and rounded once while staging
-  bool gsum_on = true;
-  if (const char* v = getenv("SAC_GSUM_BF16")) gsum_on = esz == 4 || atoi(v) != 0;
-  // (bf16: one block per summed tile -- 23.1K -> 23.6K steps/s on C2, B 7.0 -> 6.6,
-  // D 6.7 -> 6.2 us, profiles/r04_ab_gsum_bf16_c2.txt)
-  int pi0_parts = esz == 4 ? 2 : 1, q0_parts = esz == 4 ? 2 : 1;
-  if (const char* v = getenv("SAC_PI0_PARTS")) pi0_parts = std::max(1, std::min(4, atoi(v)));
-  if (const char* v = getenv("SAC_Q0_PARTS")) q0_parts = std::max(1, std::min(4, atoi(v)));
-  // 64 x 64 update tiles (dw_adam_tile64) at large batches without the hidden
-  // split: half the operand bytes per weight; opt-in (SAC_TILE64=1) until it
-  // beats the 32 x 32 tiles (profiles/r04_ab_tile64_c3.txt)
-  int t64 = 0;
-  if (const char* v = getenv("SAC_TILE64")) t64 = !split && Bp > 1024 && atoi(v) != 0;
-  const int TS = t64 ? 64 : 32;
-  // the 32 x 32 tiles sum the bias gradient from their staged dY rows
-  // (TileDesc.bstage, 16-B LDS reads) instead of loading the row tiles' partials
-  // (at C3 256 strided loads per column made the k0 == 0 tiles the tail of
-  // phases B and D): C3 4.47K -> 4.57K fp32, 7.63K -> 8.0K bf16; C2 19.3K ->
-  // 19.5K fp32, 23.45K -> 24.0K bf16 (profiles/r04_ab_bias_staged.txt);
-  // SAC_BIAS_STAGED=0 keeps the partials
-  int bstage = 1;
-  if (const char* v = getenv("SAC_BIAS_STAGED")) bstage = atoi(v) != 0;
-  const size_t part_stride = t64 ? SAC_PART_STRIDE64 : SAC_PART_STRIDE;
+  // B, 5 / 3 operand row sets) is also split into 2 batch parts with a granule
+  // hand-off (the critics' producer parts also hand over their seeded bias
+  // sums): measured D 8.3 -> 7.6 us on C2.  bf16: the parts' bf16 dY added in
+  // fp32 and rounded once while staging, one block per tile (23.1K -> 23.6K
+  // steps/s on C2, B 7.0 -> 6.6, D 6.7 -> 6.2 us, profiles/r04_ab_gsum_bf16_c2.txt)
+  const int pi0_parts = esz == 4 ? 2 : 1, q0_parts = esz == 4 ? 2 : 1;
+  const int TS = 32;  // update tiles are 32 x 32 weight blocks (64 x 64 measured slower at C3: profiles/r04_ab_tile64_c3.txt)
+  // the 32 x 32 tiles sum the bias gradient from their staged dY rows (16-B
+  // LDS reads) instead of loading per-row-tile partials (at C3 256 strided
+  // loads per column made the k0 == 0 tiles the tail of phases B and D): C3
+  // 4.47K -> 4.57K fp32, 7.63K -> 8.0K bf16; C2 19.3K -> 19.5K fp32, 23.45K ->
+  // 24.0K bf16 (profiles/r04_ab_bias_staged.txt)
+  const size_t part_stride = SAC_PART_STRIDE;
   auto ntiles_of = [&](const LayerDev& ly) { return ((ly.Np + TS - 1) / TS) * ((ly.Kp + TS - 1) / TS); };
   int tilesBD[2] = {0, 0};  // [critics (B), policy (D)]
   for (int ni = NET_PI; ni <= NET_Q2; ++ni)
     for (int l = 0; l < h.net[ni].L; ++l) tilesBD[ni == NET_PI] += ntiles_of(h.net[ni].l[l]);
   auto batch_parts = [&](int ntiles, int extra) {
     if (Bp <= 1024) return 1;
-    if (t64) {  // one round: as many batch parts (<= 8) as keep the tiles within 256 workgroups
-      if (const char* v = getenv("SAC_BPARTS")) return std::max(1, std::min(8, atoi(v)));
-      return std::max(1, std::min(8, (256 - extra) / std::max(ntiles, 1)));
-    }
-    if (const char* v = getenv("SAC_BPARTS")) return std::max(1, std::min(4, atoi(v)));
+    if (c->upd_parts > 0) return std::min(4, (int)c->upd_parts);
     int best = 4;
     double bc = 1e30;
     for (int P = 2; P <= 4; ++P) {
@@ -969,18 +839,10 @@ static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
     }
     return best;
   };
-  // phase D as 512-thread tiles, two per CU (SAC_UPD_UT_D=512, opt-in): up to 8
-  // batch parts within 512 blocks (SAC_BPARTS_D overrides)
-  int ut512_d = 0;
-  if (const char* v = getenv("SAC_UPD_UT_D")) ut512_d = !split && !t64 && Bp > 1024 && atoi(v) == 512;
   const int bpartsB = batch_parts(tilesBD[0], 0);
-  int bpartsD = batch_parts(tilesBD[1], 1);
-  if (ut512_d) {
-    bpartsD = std::max(1, std::min(8, 511 / std::max(tilesBD[1], 1)));
-    if (const char* v = getenv("SAC_BPARTS_D")) bpartsD = std::max(1, std::min(8, atoi(v)));
-  }
+  const int bpartsD = batch_parts(tilesBD[1], 1);
   auto tile_parts = [&](int ni, int l) {
-    if (l == 0 && split) return gsum_on ? std::min(ni == NET_PI ? pi0_parts : q0_parts, Bp / 32) : ni == NET_PI ? wc : 2;
+    if (l == 0 && split) return std::min(ni == NET_PI ? pi0_parts : q0_parts, Bp / 32);
     return ni == NET_PI ? bpartsD : bpartsB;
   };
   int nB = 0, nD = 0, nhalf = 0;
@@ -995,20 +857,17 @@ static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
   // kernels' LDS layout does not fit a CU (hidden layers wider than 256, wide
   // inputs: the stage path takes any width), for nets with at least two hidden
   // layers.  At C3 the row-tile kernels are faster (profiles/r04_ab_c3_paths.txt),
-  // so they keep the batches they fit; SAC_WIDE=1 forces the stage path on any
-  // batch past the hidden split, SAC_WIDE=0 refuses it.
+  // so they keep the batches they fit; config.stage_path = 1 forces the stage
+  // path on any batch past the hidden split, -1 refuses it.
   WideLay wl;
   {
-    int roles_pre = 6 * nrt0 <= 256 && SAC_ROWS * (A + 1) <= SAC_HAND_STRIDE;
-    if (const char* v = getenv("SAC_ROLES"))
-      roles_pre = atoi(v) == 2 ? SAC_ROWS * (A + 1) <= SAC_HAND_STRIDE : roles_pre && atoi(v) != 0;
+    const int roles_pre = 6 * nrt0 <= 256 && SAC_ROWS * (A + 1) <= SAC_HAND_STRIDE && c->layout != SAC_LAYOUT_ROWS;
     const bool too_big = !(roles_pre ? lds_fits_roles : lds_fits_rows);
     const bool able = !split && c->q_layers >= 3 && c->pi_layers >= 3 && 2 * A <= WJMAX;
     int on = able && too_big;
-    if (const char* v = getenv("SAC_WIDE")) on = atoi(v) != 0 ? able : 0;
+    if (c->stage_path > 0) on = able;
+    if (c->stage_path < 0) on = 0;
     wl.on = on;
-    wl.flow = 0;
-    if (const char* v = getenv("SAC_WIDE_FLOW")) wl.flow = on && atoi(v) != 0;
   }
   if (wl.on) {
     const int Brw = rup(B, 64);
@@ -1020,7 +879,6 @@ static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
     wl.hq = hq;
     wl.o_dev = lay.take(sizeof(WideDev));
     wl.o_jobs = lay.take(WIDE_MAX_JOBS * sizeof(WJob));
-    wl.o_cnt = lay.take((size_t)WIDE_MAX_JOBS * (2 * Brw / 64) * 4);  // flow: per (job, row block) counters
     wl.o_xpi0 = lay.take((size_t)2 * Brw * np.l[0].Kp * 4);
     wl.o_xq0 = lay.take((size_t)Brw * nq.l[0].Kp * 4);
     wl.o_xqt0 = lay.take((size_t)Brw * nq.l[0].Kp * 4);
@@ -1052,9 +910,6 @@ static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
       }
     }
   }
-  // persistent step: readiness counters (+ the exit word) and the task table
-  const size_t o_pctr = lay.take((size_t)(PC_COUNT * PC_SHARDS * PC_STRIDE + PC_STRIDE) * 4);
-  const size_t o_ptask = lay.take((size_t)1024 * sizeof(PTask));
   const size_t o_tB = lay.take((size_t)nB * sizeof(TileDesc));
   const size_t o_tD = lay.take((size_t)nD * sizeof(TileDesc));
   const size_t o_part = lay.take((size_t)nhalf * part_stride * 8);  // batch-part partial dW granules
@@ -1066,24 +921,9 @@ static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
   // tile kernels run pi on [s'; s] (2R rows); with roles every MLP pass is R rows.
   // The stage path (wl.on) launches none of them but policy_act: R rows, no
   // pre-activation buffers.
-  // SAC_ROLES=2: the role kernels past co-residency (6 nrt > 256 blocks).  Every
-  // role waits only for roles of LOWER block ids (phase A: pi(s') < Qt < critics;
-  // phase C: critics < pi), so in-order dispatch still guarantees progress: a
-  // spinning block's producers were dispatched before it.
-  int roles = 6 * nrt <= 256 && SAC_ROWS * (A + 1) <= SAC_HAND_STRIDE;
-  if (const char* v = getenv("SAC_ROLES"))
-    roles = atoi(v) == 2 ? SAC_ROWS * (A + 1) <= SAC_HAND_STRIDE : roles && atoi(v) != 0;
+  int roles = 6 * nrt <= 256 && SAC_ROWS * (A + 1) <= SAC_HAND_STRIDE && c->layout != SAC_LAYOUT_ROWS;
   roles = roles && !wl.on;
   const int lo = lds_layout(h, wl.on || roles ? SAC_ROWS : 2 * SAC_ROWS, !wl.on);
-  // with the bias gradients summed from the update tiles' staged rows nobody reads
-  // the row tiles' partials: the phase kernels skip them (store_T, dbp == null).
-  // The 64 x 64 tiles read them and the stage path writes them unconditionally.
-  // (SAC_DBP_SKIP=0 keeps the stores: A/B)
-  int dbp_skip = bstage && !t64 && !wl.on;
-  if (const char* v = getenv("SAC_DBP_SKIP")) dbp_skip = dbp_skip && atoi(v) != 0;
-  if (dbp_skip)
-    for (int ni = 0; ni < 5; ++ni)
-      for (int l = 0; l < h.net[ni].L; ++l) h.net[ni].l[l].dbp = nullptr;
 
   if (e) {
     h.B = B;
@@ -1095,19 +935,15 @@ static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
     {
       int xs = 1;  // largest power of two <= 8 with nrt * xs <= 256 blocks
       while (xs < 8 && nrt * xs * 2 <= 256) xs *= 2;
-      if (const char* v = getenv("SAC_XS")) xs = std::max(1, atoi(v));
       h.xs = xs;
       // phase A's weight parts on one or two XCDs each: A's fetched bytes 11.0 -> 5.1
       // MB per launch, phase B 8.6 -> 8.1 us, +1.2% steps/s (C2 fp32,
       // profiles/r03_ab_role_xcd.txt)
       h.role_xcd = split && (10 + split_wpi(esz)) * nrt % 8 == 0;
-      if (const char* v = getenv("SAC_ROLE_XCD")) h.role_xcd = h.role_xcd && atoi(v) != 0;
       // role split of phases A/C: 6 * nrt workgroups must be co-resident (one per CU)
       h.roles = roles;
-      // phase C stages the next step's batch (SAC_STAGE=0 turns it off)
-      int stage = 1;
-      if (const char* v = getenv("SAC_STAGE")) stage = atoi(v) != 0;
-      h.stage = stage;
+      // phase C stages the next step's batch (config.stage_batch = -1 turns it off)
+      h.stage = c->stage_batch >= 0;
     }
     h.auto_entropy = c->auto_entropy;
     h.alpha_update = 1;
@@ -1149,29 +985,24 @@ static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
     e->h.nB = nB;
     e->h.nD = nD;
     e->lds_bytes = (size_t)lo * 4;
-    e->h.pctr = (uint32_t*)(base + o_pctr);
-    e->h.ptasks = (const void*)(base + o_ptask);
     {  // update tiles stage up to 4 batch chunks of 512 B per operand row per round
        // (every tile reduces over at most Bp columns: split layer 0 is two half tiles)
       const int bch = 512 / esz;
       e->h.upd_slots = std::min(4, (Bp + bch - 1) / bch);
       e->upd_lds = SAC_UPD_LDS_FOR(e->h.upd_slots);
-      if (t64) e->upd_lds = std::max((size_t)SAC_UPD64_LDS, (size_t)5 * 1024 * 4);  // (the alpha block: 5 x 1024 floats)
       // phase B in 2 rounds of 1024-thread blocks (C3: 480 blocks) -> 512-thread
       // blocks with 2 slots, two per CU, one round: C3 B 37.0 -> 33.5 us fp32,
-      // 20.0 -> 18.1 bf16 (profiles/r04_ab_upd_ut512_c3.txt); SAC_UPD_UT=512 / 1024
-      // forces it (no summed layer-0 tiles: GS 1 only, so never with the hidden split)
+      // 20.0 -> 18.1 bf16 (profiles/r04_ab_upd_ut512_c3.txt); config.upd_threads =
+      // 512 / 1024 forces it (no summed layer-0 tiles: GS 1 only, so never with the
+      // hidden split)
       int ut512 = nB > 256 && nB <= 512;
-      if (const char* v = getenv("SAC_UPD_UT")) ut512 = atoi(v) == 512;
+      if (c->upd_threads) ut512 = c->upd_threads == 512;
       e->upd_ut_b = SAC_UPD_THREADS;
       e->upd_lds_b = e->upd_lds;
-      if (ut512 && !t64 && !split) {
+      if (ut512 && !split) {
         e->upd_ut_b = 512;
         e->upd_lds_b = SAC_UPD_LDS_FOR(std::min(2, e->h.upd_slots));
       }
-      e->upd_ut_d = ut512_d ? 512 : SAC_UPD_THREADS;
-      e->upd_lds_d = ut512_d ? std::max((size_t)SAC_UPD_LDS_FOR(std::min(2, e->h.upd_slots)), (size_t)5 * 512 * 4)
-                             : e->upd_lds;
     }
     e->nrt = nrt;
     // self-contained update tiles (phase B: critics + Polyak, phase D: policy)
@@ -1191,8 +1022,6 @@ static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
             memset(&t, 0, sizeof(t));
             const int bpl = (l == 0 && split) ? 2 * Bp : Bp;                     // X^T row stride
             const int bpg = (l == 0 && split) ? (ni == NET_PI ? wc : 2) * Bp : Bp;  // dY^T row stride
-            t.tile64 = t64;
-            t.bstage = bstage;
             t.GT = (const char*)ly.GT + (size_t)nt * TS * bpg * esz2;
             t.XT = (const char*)ly.XT + (size_t)kt * TS * bpl * esz2;
             t.W = nd.P + ly.w_off;
@@ -1208,7 +1037,6 @@ static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
               t.tb = tn.P + ly.b_off;
               t.tWc = tn.l[l].Wc;
             }
-            t.dbp = ly.dbp;
             t.xt_par = ly.xt_par;
             t.bp = (l == 0 && split) ? 2 * Bp : Bp;
             t.K = ly.K;
@@ -1218,7 +1046,6 @@ static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
             t.n0 = nt * TS;
             t.k0 = kt * TS;
             t.opt = ni;
-            t.nrt = (l == 0 && split) ? bpg / SAC_ROWS : nrt;
             t.ld = t.bp;
             t.ldx = t.bp;
             t.kpart = 0;
@@ -1227,7 +1054,7 @@ static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
             t.goff = 0;
             t.seed = nullptr;
             if (split && esz == 4 && ni != NET_PI) t.seed = h.seedq + (size_t)(ni - NET_Q1) * Bp;
-            if (l == 0 && split && gsum_on) {  // one block: dY parts [p Bp, (p+1) Bp) summed, X^T [0, Bp)
+            if (l == 0 && split) {  // one block: dY parts [p Bp, (p+1) Bp) summed, X^T [0, Bp)
               t.gsum = ni == NET_PI ? wc : 2;
               t.goff = Bp;
               t.bp = Bp;
@@ -1236,15 +1063,13 @@ static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
             }
             const int parts = tile_parts(ni, l);
             if (parts > 1) {
-              // consumer part 1 (batch columns [0, bpp)) + producer parts 2..P ([(p-1) bpp, p bpp))
-              // bf16 split layer 0: a part per dY part, X^T columns [0, Bp) serve every part;
-              // fp32 (gsum) split layer 0: batch parts of the summed operands
-              const bool xsame = l == 0 && split && !gsum_on;
-              const int total = xsame ? parts * Bp : Bp;
-              const int bpp = xsame ? Bp : rup((Bp + parts - 1) / parts, 32);
-              if (!(l == 0 && split && gsum_on)) {
-                t.ld = xsame ? parts * Bp : Bp;
-                t.ldx = xsame ? 2 * Bp : Bp;
+              // consumer part 1 (batch columns [0, bpp)) + producer parts 2..P ([(p-1) bpp, p bpp));
+              // split layer 0 (gsum): batch parts of the summed operands
+              const int total = Bp;
+              const int bpp = rup((Bp + parts - 1) / parts, 32);
+              if (!(l == 0 && split)) {
+                t.ld = Bp;
+                t.ldx = Bp;
               }
               t.bp = bpp;
               t.kpart = 1;
@@ -1257,8 +1082,8 @@ static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
                 pt.kpart = pp;
                 pt.bp = std::min(bpp, total - off);
                 pt.GT = (const char*)t.GT + (size_t)off * esz2;
-                if (!xsame) pt.XT = (const char*)t.XT + (size_t)off * esz2;
-                if (t.seed && !xsame) pt.seed = t.seed + off;
+                pt.XT = (const char*)t.XT + (size_t)off * esz2;
+                if (t.seed) pt.seed = t.seed + off;
                 (ni == NET_PI ? halvesD : halvesB).push_back(pt);
               }
             }
@@ -1266,114 +1091,20 @@ static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
           }
       }
     }
-    const int bpartsQ = (split || Bp <= 1024) ? 1 : bpartsB, bpartsP = (split || Bp <= 1024) ? 1 : bpartsD;
-    auto order = [&](std::vector<TileDesc>& cons, std::vector<TileDesc>& prod, int bparts) {
-      std::vector<TileDesc> all = cons;
-      all.insert(all.end(), prod.begin(), prod.end());
-      int xpart = 0;  // measured 2-6% slower on C3 (B 54.5 -> 57.8 us fp32): opt-in
-      if (const char* v = getenv("SAC_XCD_PARTS")) xpart = atoi(v) != 0;
-      if (bparts > 1 && xpart && cons.size() < 256 && xcd_order_parts(all, bparts)) {
-        cons.swap(all);
-        return;
-      }
+    auto order = [&](std::vector<TileDesc>& cons, std::vector<TileDesc>& prod) {
       xcd_order(cons);
       // producer parts first: in-order dispatch starts every producer before its consumer
       cons.insert(cons.begin(), prod.begin(), prod.end());
     };
-    order(e->hostB, halvesB, bpartsQ);
-    order(e->hostD, halvesD, bpartsP);
+    order(e->hostB, halvesB);
+    order(e->hostD, halvesD);
     e->h.nBq[0] = e->h.nBq[1] = 0;
     for (const TileDesc& t : e->hostB) ++e->h.nBq[t.opt - 1];
-    {
-      // Fused layouts are exact (tests/test_gpu_engine.py) but measured no faster
-      // on C2: four launches stay the default; SAC_FUSE=1|2 opts in.
-      int fuse = 0;
-      if (const char* v = getenv("SAC_FUSE")) fuse = std::max(0, std::min(2, atoi(v)));
-      if (!e->h.roles || e->h.split || nhalf || nD + 1 + 6 * nrt > 256) fuse = 0;
-      if (fuse == 2 && nB + 3 * nrt > 256) fuse = 1;
-      e->fused = fuse;
-    }
-    plan_persist(e, esz);
-    if (t64) e->persist = 0;  // the fused step runs the 32 x 32 tiles only
     e->wl = wl;
     e->wide = wl.on;
     if (wl.on) build_wide(e, base);
   }
   return total + 256;
-}
-
-// The persistent step's task table (sac_persist.h).  Workgroup w runs phase-A
-// role w (the role kernels' block order: pi(s') parts, target critics,
-// critics, pi(s)); the other phases' tasks go to the workgroups that are free
-// when those tasks can start:
-//   B tiles      -> pi(s') workgroups (done first), target critics, spares, pi(s), critics
-//   C pi roles   -> pi(s') workgroups (after their B tile; they then wait for the critics)
-//   C critics    -> critic workgroups (no B tile), pi(s), spares, target critics, pi(s')
-//   D tiles      -> target-critic workgroups (idle until the next step's pi(s')), spares, ...
-// so the next step's pi(s') workgroups carry no phase-D tile and can sample and
-// gather their rows while phase D runs.  Lists are concatenations of whole
-// classes (multiples of 8 workgroups at C2/C4), so a tile keeps the XCD bucket
-// xcd_order gave its position (blocks are dealt round-robin over the XCDs).
-#ifndef SAC_FUSED_DEFAULT
-#define SAC_FUSED_DEFAULT 0  // four launches per step stay the default until the fused step measures faster
-#endif
-static void plan_persist(sac_engine* e, int esz) {
-  e->persist = 0;
-  if (!e->h.split) return;
-  int on = SAC_FUSED_DEFAULT;
-  if (const char* v = getenv("SAC_PERSIST")) on = atoi(v) != 0;
-  if (!on) return;
-  const int nrt = e->h.nrt, WP = split_wpi(esz), W = split_wc(esz);
-  const int nA = (WP + 10) * nrt, nCq = 2 * W * nrt, nCp = W * nrt, nB = e->nB, nD1 = e->nD + 1;
-  int G = e->ncu;
-  if (const char* v = getenv("SAC_PERSIST_G")) G = std::max(1, atoi(v));
-  G = std::min(G, 1024);
-  if (nA > G || nB > G || nCq + nCp > G || nD1 > G) return;
-  std::vector<int> pis2, qt, cr, pis, spare;
-  for (int w = 0; w < G; ++w) {
-    if (w < WP * nrt) pis2.push_back(w);
-    else if (w < (WP + 4) * nrt) qt.push_back(w);
-    else if (w < (WP + 8) * nrt) cr.push_back(w);
-    else if (w < nA) pis.push_back(w);
-    else spare.push_back(w);
-  }
-  auto cat = [](std::initializer_list<const std::vector<int>*> ls) {
-    std::vector<int> o;
-    for (const auto* l : ls) o.insert(o.end(), l->begin(), l->end());
-    return o;
-  };
-  std::vector<PTask> t((size_t)G, PTask{-1, -1, -1, -1});
-  for (int w = 0; w < nA; ++w) t[w].a = (int16_t)w;
-  const std::vector<int> ob = cat({&pis2, &qt, &spare, &pis, &cr});
-  for (int i = 0; i < nB; ++i) t[ob[i]].b = (int16_t)i;
-  for (int i = 0; i < nCp; ++i) t[ob[i]].c = (int16_t)(nCq + i);
-  int ic = 0;
-  for (int w : cat({&cr, &pis, &spare, &qt, &pis2}))
-    if (ic < nCq && t[w].c < 0) t[w].c = (int16_t)ic++;
-  // stagers (phase C, E.stage): the next step's batch per row tile, on
-  // workgroups left without a phase-C task (target critics: between their B
-  // and D tiles)
-  int is = 0;
-  const int nS = e->h.stage ? nrt : 0;
-  for (int w : cat({&qt, &spare, &pis, &cr, &pis2}))
-    if (is < nS && t[w].c < 0) t[w].c = (int16_t)(nCq + nCp + is++);
-  if (is < nS) return;
-  const std::vector<int> od = cat({&qt, &spare, &cr, &pis, &pis2});
-  for (int i = 0; i < nD1; ++i) t[od[i]].d = (int16_t)i;
-  e->hostP = t;
-  e->G = G;
-  e->h.pc_n[PC_AQ] = (uint32_t)(8 * nrt);
-  e->h.pc_n[PC_PS] = (uint32_t)(2 * nrt);
-  e->h.pc_n[PC_BQ1] = (uint32_t)e->h.nBq[0];
-  e->h.pc_n[PC_BQ2] = (uint32_t)e->h.nBq[1];
-  e->h.pc_n[PC_CP] = (uint32_t)nCp;
-  e->h.pc_n[PC_D] = (uint32_t)nD1;
-  e->h.pc_n[PC_AQP] = (uint32_t)(4 * nrt);  // critic roles (2 critics x 2 halves x nrt)
-  e->h.p_aqp = 1;
-  if (const char* v = getenv("SAC_PERSIST_AQP")) e->h.p_aqp = atoi(v) != 0;
-  e->h.o_pflag = (int)((std::max(e->lds_bytes, e->upd_lds) + 15) / 16 * 4);
-  if ((size_t)e->h.o_pflag * 4 + 16 > 160 * 1024) return;
-  e->persist = 1;
 }
 
 // Update-tile order for the XCDs (speed only; any order gives the same bits).
@@ -1416,64 +1147,28 @@ static void xcd_order(std::vector<TileDesc>& tiles) {
   tiles.swap(out);
 }
 
-// Batch-part tiles (Bp > 1024, P parts, P | 8; C3: 4 x 1024 columns): part p
-// of every tile goes to the XCDs {x : x * P / 8 == p - 1}, split among them by
-// the tile's longer index (nt when NT >= KT, else kt), in tile order.  Every
-// 32-row dY^T / X^T batch slice is read by the 8 tiles of its row or column;
-// this way they share one XCD's L2 (one fetch per XCD instead of one per tile:
-// the operand re-reads, not the MFMAs, set the B/D time at C3).  Position q
-// holds a tile of bucket q % 8 (blocks are dealt round-robin to the XCDs).
-// Consumers (part 1) no longer follow their producers in dispatch order;
-// progress holds because producers never wait and the caller keeps the
-// consumers fewer than the CUs.  Same bits in any order.  False (tiles
-// untouched) when the buckets come out uneven.
-static bool xcd_order_parts(std::vector<TileDesc>& tiles, int P) {
-  if (P < 2 || 8 % P) return false;
-  const int xs = 8 / P;  // XCDs per part
-  std::vector<TileDesc> bucket[8];
-  for (const TileDesc& d : tiles) {
-    const int NT = d.Np / 32, KT = d.Kp / 32, nt = d.n0 / 32, kt = d.k0 / 32;
-    const int pi = d.kpart <= 1 ? 0 : d.kpart - 1;
-    if (d.nparts != P || pi >= P) return false;
-    const int sub = NT >= KT ? nt * xs / NT : kt * xs / KT;
-    bucket[pi * xs + sub].push_back(d);
-  }
-  for (int x = 1; x < 8; ++x)
-    if (bucket[x].size() != bucket[0].size()) return false;
-  std::vector<TileDesc> out;
-  out.reserve(tiles.size());
-  for (size_t i = 0; i < bucket[0].size(); ++i)
-    for (int x = 0; x < 8; ++x) out.push_back(bucket[x][i]);
-  tiles.swap(out);
-  return true;
-}
-
 template <typename T>
 static void set_lds_attrs(size_t bytes) {
   (void)bytes;
   const int b = 160 * 1024;  // the launch passes what it needs; the attribute is the cap
-  (void)hipFuncSetAttribute((const void*)sac_target_critic<T, false, false>, hipFuncAttributeMaxDynamicSharedMemorySize, b);
-  (void)hipFuncSetAttribute((const void*)sac_target_critic<T, true, false>, hipFuncAttributeMaxDynamicSharedMemorySize, b);
-  (void)hipFuncSetAttribute((const void*)sac_target_critic<T, true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, b);
-  (void)hipFuncSetAttribute((const void*)sac_actor<T, false, false>, hipFuncAttributeMaxDynamicSharedMemorySize, b);
-  (void)hipFuncSetAttribute((const void*)sac_actor<T, true, false>, hipFuncAttributeMaxDynamicSharedMemorySize, b);
-  (void)hipFuncSetAttribute((const void*)sac_actor<T, true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, b);
+  (void)hipFuncSetAttribute((const void*)sac_target_critic<T, false>, hipFuncAttributeMaxDynamicSharedMemorySize, b);
+  (void)hipFuncSetAttribute((const void*)sac_target_critic<T, true>, hipFuncAttributeMaxDynamicSharedMemorySize, b);
+  (void)hipFuncSetAttribute((const void*)sac_actor<T, false>, hipFuncAttributeMaxDynamicSharedMemorySize, b);
+  (void)hipFuncSetAttribute((const void*)sac_actor<T, true>, hipFuncAttributeMaxDynamicSharedMemorySize, b);
   (void)hipFuncSetAttribute((const void*)sac_policy_act_kernel<T>, hipFuncAttributeMaxDynamicSharedMemorySize, b);
   (void)hipFuncSetAttribute((const void*)sac_target_critic_split<T>, hipFuncAttributeMaxDynamicSharedMemorySize, b);
   (void)hipFuncSetAttribute((const void*)sac_actor_split<T>, hipFuncAttributeMaxDynamicSharedMemorySize, b);
   (void)hipFuncSetAttribute((const void*)sac_critic_update<T>, hipFuncAttributeMaxDynamicSharedMemorySize, b);
   (void)hipFuncSetAttribute((const void*)sac_critic_update<T, 512>, hipFuncAttributeMaxDynamicSharedMemorySize, b);
   (void)hipFuncSetAttribute((const void*)sac_actor_update<T>, hipFuncAttributeMaxDynamicSharedMemorySize, b);
-  (void)hipFuncSetAttribute((const void*)sac_actor_update<T, 512>, hipFuncAttributeMaxDynamicSharedMemorySize, b);
-  (void)hipFuncSetAttribute((const void*)sac_persist<T>, hipFuncAttributeMaxDynamicSharedMemorySize, b);
   (void)hipFuncSetAttribute((const void*)sac_wide_stage<T, WA_PLAIN, false>, hipFuncAttributeMaxDynamicSharedMemorySize, b);
   (void)hipFuncSetAttribute((const void*)sac_wide_stage<T, WA_ACT, false>, hipFuncAttributeMaxDynamicSharedMemorySize, b);
   (void)hipFuncSetAttribute((const void*)sac_wide_stage<T, WA_OUTBWD, false>, hipFuncAttributeMaxDynamicSharedMemorySize, b);
   (void)hipFuncSetAttribute((const void*)sac_wide_stage<T, WA_PLAIN, true>, hipFuncAttributeMaxDynamicSharedMemorySize, b);
   (void)hipFuncSetAttribute((const void*)sac_wide_stage<T, WA_ACT, true>, hipFuncAttributeMaxDynamicSharedMemorySize, b);
   (void)hipFuncSetAttribute((const void*)sac_wide_stage<T, WA_OUTBWD, true>, hipFuncAttributeMaxDynamicSharedMemorySize, b);
-  (void)hipFuncSetAttribute((const void*)sac_wide_flow<T, false>, hipFuncAttributeMaxDynamicSharedMemorySize, b);
-  (void)hipFuncSetAttribute((const void*)sac_wide_flow<T, true>, hipFuncAttributeMaxDynamicSharedMemorySize, b);
+  (void)hipFuncSetAttribute((const void*)sac_wide_gather<T>, hipFuncAttributeMaxDynamicSharedMemorySize, b);
+  (void)hipFuncSetAttribute((const void*)sac_wide_head<T>, hipFuncAttributeMaxDynamicSharedMemorySize, b);
 }
 
 // empty kernel: the dispatch + event gap of sac_engine_time_phases
@@ -1486,10 +1181,8 @@ __global__ void sac_spin_kernel(long long ticks) {
   while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(8);
 }
 
-// Launch kinds of a step sequence.  Unfused: A B C D per step.  Fused (role
-// split with every block co-resident): A, then per step BC, and DA for the next
-// step, closed by a D: D(k) shares a launch with A(k + 1), B(k) with C(k).
-enum LaunchKind { L_A = 0, L_B = 1, L_C = 2, L_D = 3, L_DA = 4, L_BC = 5 };
+// Launch kinds of a step: A B C D.
+enum LaunchKind { L_A = 0, L_B = 1, L_C = 2, L_D = 3 };
 
 template <typename T>
 static void launch_kind(sac_engine* e, int kind, const sac_replay* rb, const int32_t* idx, const float* eps,
@@ -1502,9 +1195,9 @@ static void launch_kind(sac_engine* e, int kind, const sac_replay* rb, const int
         sac_target_critic_split<T><<<e->nrt * (10 + split_wpi((int)sizeof(T))), SAC_THREADS, lf, s>>>(e->d, *rb, idx,
                                                                                                   eps);
       else if (e->h.roles)
-        sac_target_critic<T, true, false><<<e->nrt * 6, SAC_THREADS, lf, s>>>(e->d, *rb, idx, eps);
+        sac_target_critic<T, true><<<e->nrt * 6, SAC_THREADS, lf, s>>>(e->d, *rb, idx, eps);
       else
-        sac_target_critic<T, false, false><<<e->nrt * e->h.xs, SAC_THREADS, lf, s>>>(e->d, *rb, idx, eps);
+        sac_target_critic<T, false><<<e->nrt * e->h.xs, SAC_THREADS, lf, s>>>(e->d, *rb, idx, eps);
       break;
     case L_B:
       if (e->upd_ut_b == 512)
@@ -1516,21 +1209,12 @@ static void launch_kind(sac_engine* e, int kind, const sac_replay* rb, const int
       if (e->h.split)
         sac_actor_split<T><<<e->nrt * 3 * split_wc((int)sizeof(T)) + stg, SAC_THREADS, lf, s>>>(e->d, *rb);
       else if (e->h.roles)
-        sac_actor<T, true, false><<<e->nrt * 3 + stg, SAC_THREADS, lf, s>>>(e->d, *rb);
+        sac_actor<T, true><<<e->nrt * 3 + stg, SAC_THREADS, lf, s>>>(e->d, *rb);
       else
-        sac_actor<T, false, false><<<e->nrt * e->h.xs + stg, SAC_THREADS, lf, s>>>(e->d, *rb);
+        sac_actor<T, false><<<e->nrt * e->h.xs + stg, SAC_THREADS, lf, s>>>(e->d, *rb);
       break;
     case L_D:
-      if (e->upd_ut_d == 512)
-        sac_actor_update<T, 512><<<e->nD + 1, 512, e->upd_lds_d, s>>>(e->d, e->tilesD, e->nD);
-      else
-        sac_actor_update<T><<<e->nD + 1, SAC_UPD_THREADS, e->upd_lds, s>>>(e->d, e->tilesD, e->nD);
-      break;
-    case L_DA:
-      sac_target_critic<T, true, true><<<e->nD + 1 + e->nrt * 6, SAC_THREADS, lf, s>>>(e->d, *rb, idx, eps);
-      break;
-    case L_BC:
-      sac_actor<T, true, true><<<e->nB + e->nrt * 3 + stg, SAC_THREADS, lf, s>>>(e->d, *rb);
+      sac_actor_update<T><<<e->nD + 1, SAC_UPD_THREADS, e->upd_lds, s>>>(e->d, e->tilesD, e->nD);
       break;
   }
 }
@@ -1561,13 +1245,6 @@ static void launch_wide_stage(sac_engine* e, const sac_engine::WStage& st, const
     case 2:
       sac_wide_head<T><<<st.grid, WG_T, 0, s>>>(e->d, e->wdd, eps);
       break;
-    case 5: {
-      const bool relu = e->cfg.q_hidden_act == ACT_RELU && e->cfg.pi_hidden_act == ACT_RELU;
-      const int flags = st.last | (st.phase == 2 ? 2 : 0);
-      auto k = relu ? sac_wide_flow<T, true> : sac_wide_flow<T, false>;
-      k<<<st.G, WG_T, st.lds, s>>>(e->d, e->wdd, e->wjobs + st.j0, st.j1 - st.j0, st.grid, flags, *rb, idx, eps);
-      break;
-    }
     case 3:
       launch_kind<T>(e, L_B, rb, idx, eps, s);
       break;
@@ -1584,31 +1261,10 @@ static void launch_wide(sac_engine* e, const sac_engine::WStage& st, const sac_r
     launch_wide_stage<float>(e, st, rb, idx, eps, s, stage_next, next_idx);
 }
 
-// Fused-step launches of n consecutive steps (one step per launch, sac_persist.h).
-static void launch_persist(sac_engine* e, const sac_replay* rb, int n, const int32_t* indices, const float* eps,
-                           hipStream_t s) {
-  const size_t B = e->cfg.batch, A = e->cfg.act_dim;
-  const size_t lds = (size_t)e->h.o_pflag * 4 + 16;
-  for (int k = 0; k < n; ++k) {  // one step per launch (sac_persist.h)
-    const int32_t* ix = indices ? indices + (size_t)k * B : nullptr;
-    const float* ep = eps ? eps + (size_t)k * 2 * B * A : nullptr;
-    if (e->cfg.precision == SAC_PREC_BF16)
-      sac_persist<bf16><<<e->G, SAC_THREADS, lds, s>>>(e->d, *rb, ix, ep);
-    else
-      sac_persist<float><<<e->G, SAC_THREADS, lds, s>>>(e->d, *rb, ix, ep);
-  }
-}
-
 // The launches of n consecutive steps (and, per launch, its kind in *kinds).
-// persistent: one launch for the n steps (per-launch kinds / events: the four
-// phase launches, profiling only).
 static void launch_steps(sac_engine* e, const sac_replay* rb, int n, const int32_t* indices, const float* eps,
                          hipStream_t s, std::vector<int>* kinds = nullptr, std::vector<hipEvent_t>* ev = nullptr) {
   const size_t B = e->cfg.batch, A = e->cfg.act_dim;
-  if (e->persist && !kinds && !ev) {
-    if (n > 0) launch_persist(e, rb, n, indices, eps, s);
-    return;
-  }
   auto go = [&](int kind, int step) {
     const int32_t* ix = indices ? indices + (size_t)step * B : nullptr;
     const float* ep = eps ? eps + (size_t)step * 2 * B * A : nullptr;
@@ -1645,23 +1301,8 @@ static void launch_steps(sac_engine* e, const sac_replay* rb, int n, const int32
     }
     return;
   }
-  if (!e->fused) {
-    for (int i = 0; i < n; ++i)
-      for (int k = L_A; k <= L_D; ++k) go(k, i);
-    return;
-  }
-  if (n < 1) return;
-  go(L_A, 0);
-  for (int i = 0; i < n; ++i) {
-    if (e->fused == 2) {
-      go(L_BC, i);
-    } else {
-      go(L_B, i);
-      go(L_C, i);
-    }
-    if (i + 1 < n) go(L_DA, i + 1);
-  }
-  go(L_D, n - 1);
+  for (int i = 0; i < n; ++i)
+    for (int k = L_A; k <= L_D; ++k) go(k, i);
 }
 
 static int check_replay(sac_engine* e, const sac_replay* rb) {
@@ -1741,7 +1382,8 @@ int sac_engine_create(const sac_engine_config* cfg, const sac_engine_buffers* bu
     return fail(SAC_E_INVALID, "layer widths need " + std::to_string(lb) + " B of LDS per workgroup (max 163840)");
   }
   if (e->wide) {
-    size_t mx = 0;
+    // the stage launches' LDS, and the batch gather's [WGR][obs + act] rows + slots
+    size_t mx = (size_t)((WGR * (cfg->obs_dim + cfg->act_dim) + 1) & ~1) * 4 + WGR * 8;
     for (const sac_engine::WStage& st : e->wst) mx = std::max(mx, st.lds);
     if (e->hostW.size() > WIDE_MAX_JOBS || mx > 160 * 1024) {
       const std::string m = "internal: stage path plans " + std::to_string(e->hostW.size()) + " jobs, " +
@@ -1760,34 +1402,6 @@ int sac_engine_create(const sac_engine_config* cfg, const sac_engine_buffers* bu
     set_lds_attrs<bf16>(e->lds_bytes);
   else
     set_lds_attrs<float>(e->lds_bytes);
-  if (e->persist) {
-    // the fused step's G workgroups spin on each other's counters: every one of
-    // them must be resident at once (one per CU at its VGPR count and LDS size)
-    int nb = 0;
-    const size_t lds = (size_t)e->h.o_pflag * 4 + 16;
-    const hipError_t oe =
-        cfg->precision == SAC_PREC_BF16
-            ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, sac_persist<bf16>, SAC_THREADS, lds)
-            : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, sac_persist<float>, SAC_THREADS, lds);
-    if (oe != hipSuccess || nb < 1 || e->G > nb * e->ncu) e->persist = 0;
-  }
-  if (e->wide && e->wl.flow) {
-    // the flow launches' workgroups wait on each other: all of them resident at once
-    const bool relu = cfg->q_hidden_act == ACT_RELU && cfg->pi_hidden_act == ACT_RELU;
-    const bool bf = cfg->precision == SAC_PREC_BF16;
-    for (sac_engine::WStage& st : e->wst) {
-      if (st.kind != 5) continue;
-      int nb = 0;
-      const void* k = bf ? (relu ? (const void*)sac_wide_flow<bf16, true> : (const void*)sac_wide_flow<bf16, false>)
-                         : (relu ? (const void*)sac_wide_flow<float, true> : (const void*)sac_wide_flow<float, false>);
-      const hipError_t oe = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, WG_T, st.lds);
-      if (oe != hipSuccess || nb < 1) {
-        delete e;
-        return fail(SAC_E_HIP, "the flow kernel does not fit a CU");
-      }
-      st.G = std::min(st.grid, nb * e->ncu);
-    }
-  }
   hipStream_t s = (hipStream_t)stream;
   hipError_t err = hipMemsetAsync(buf->workspace, 0, buf->workspace_bytes, s);
   if (err == hipSuccess) err = hipMemcpyAsync(e->d, &e->h, sizeof(EngineDev), hipMemcpyHostToDevice, s);
@@ -1796,8 +1410,6 @@ int sac_engine_create(const sac_engine_config* cfg, const sac_engine_buffers* bu
   if (err == hipSuccess && e->wide) err = hipMemcpyAsync(e->wdd, &e->wdh, sizeof(WideDev), hipMemcpyHostToDevice, s);
   if (err == hipSuccess && e->wide)
     err = hipMemcpyAsync(e->wjobs, e->hostW.data(), e->hostW.size() * sizeof(WJob), hipMemcpyHostToDevice, s);
-  if (err == hipSuccess && e->persist)
-    err = hipMemcpyAsync((void*)e->h.ptasks, e->hostP.data(), e->hostP.size() * sizeof(PTask), hipMemcpyHostToDevice, s);
   if (err == hipSuccess) err = hipStreamSynchronize(s);
   if (err != hipSuccess) {
     delete e;
@@ -1915,15 +1527,10 @@ int sac_replay_push(const sac_replay* rb, const float* rows, int64_t n, int64_t 
 }
 
 // rows per wave of the records gather: 16 (4x the waves in flight of 64 rows per wave:
-// 65,536 rows 1.51 -> 2.42 TB/s, 1,048,576 rows 3.00 -> 3.17 TB/s); SAC_GATHER_RPW overrides
+// 65,536 rows 1.51 -> 2.42 TB/s, 1,048,576 rows 3.00 -> 3.17 TB/s)
 static int gather_rpw(int batch) {
-  static const int env = [] {
-    const char* v = getenv("SAC_GATHER_RPW");
-    const int x = v ? atoi(v) : 0;
-    return (x == 4 || x == 8 || x == 16 || x == 32 || x == 64) ? x : 0;
-  }();
   (void)batch;
-  return env ? env : 16;
+  return 16;
 }
 
 int sac_replay_gather(const sac_replay* rb, const int32_t* logical_idx, int32_t batch, float* s, float* a, float* r,
@@ -2030,8 +1637,6 @@ int sac_engine_uses_roles(const sac_engine* e) { return e && e->h.roles ? 1 : 0;
 
 int sac_engine_uses_split(const sac_engine* e) { return e && e->h.split ? 1 : 0; }
 
-int sac_engine_uses_fused_step(const sac_engine* e) { return e && e->persist ? e->G : 0; }
-
 int sac_engine_uses_wide(const sac_engine* e) { return e && e->wide ? (int)e->wst.size() : 0; }
 
 int sac_engine_phase_launches(const sac_engine* e, int32_t* out) {
@@ -2041,17 +1646,12 @@ int sac_engine_phase_launches(const sac_engine* e, int32_t* out) {
     for (int k = 0; k < 4; ++k) out[k] = 0;
     for (const sac_engine::WStage& st : e->wst)
       if (st.kind != 0 && st.phase >= 0 && st.phase < 4) ++out[st.phase];
-  } else if (e->fused) {
-    out[1] = e->fused == 2 ? 0 : 1;
-    out[3] = 0;
   }
   return SAC_OK;
 }
 
-int sac_engine_phase_layout(const sac_engine* e) { return e ? e->fused : 0; }
-
 int sac_engine_debug_launch(sac_engine* e, const sac_replay* rb, int32_t kind, void* stream) {
-  if (!e || !rb || kind < L_A || kind > L_BC) return fail(SAC_E_INVALID, "bad debug_launch arguments");
+  if (!e || !rb || kind < L_A || kind > L_D) return fail(SAC_E_INVALID, "bad debug_launch arguments");
   if (e->wide) {  // every launch of that phase
     for (const sac_engine::WStage& st : e->wst)
       if (st.phase == kind) launch_wide(e, st, rb, nullptr, nullptr, (hipStream_t)stream);
@@ -2080,8 +1680,7 @@ int sac_engine_time_phases(sac_engine* e, const sac_replay* rb, int32_t n_steps,
   if (rc) return rc;
   hipStream_t s = (hipStream_t)stream;
   // events after every launch of the step sequence; a launch's time = its event
-  // minus the previous one.  Fused: [0] = phase A launches with D inside (DA),
-  // [2] = phase C launches with B inside (BC), [1] = [3] = 0.
+  // minus the previous one
   std::vector<int> kinds;
   std::vector<hipEvent_t> ev;
   hipEvent_t start;
@@ -2093,8 +1692,8 @@ int sac_engine_time_phases(sac_engine* e, const sac_replay* rb, int32_t n_steps,
   HIPCHK(hipEventRecord(start, s));
   launch_steps(e, rb, n_steps, nullptr, nullptr, s, &kinds, &ev);
   HIPCHK(hipStreamSynchronize(s));
-  double sum[6] = {0, 0, 0, 0, 0, 0};
-  int cnt[6] = {0, 0, 0, 0, 0, 0};
+  double sum[4] = {0, 0, 0, 0};
+  int cnt[4] = {0, 0, 0, 0};
   for (size_t i = 0; i < ev.size(); ++i) {
     float ms = 0.f;
     HIPCHK(hipEventElapsedTime(&ms, i ? ev[i - 1] : start, ev[i]));
@@ -2103,14 +1702,7 @@ int sac_engine_time_phases(sac_engine* e, const sac_replay* rb, int32_t n_steps,
   }
   // per phase and step (the stage path has several launches per phase)
   auto avg = [&](int k) { return cnt[k] ? (float)(sum[k] / (e->wide ? n_steps : cnt[k])) : 0.f; };
-  if (e->fused) {
-    ms_host[0] = cnt[L_DA] ? avg(L_DA) : avg(L_A);
-    ms_host[1] = e->fused == 2 ? 0.f : avg(L_B);
-    ms_host[2] = e->fused == 2 ? avg(L_BC) : avg(L_C);
-    ms_host[3] = 0.f;
-  } else {
-    for (int p = 0; p < 4; ++p) ms_host[p] = avg(p);
-  }
+  for (int p = 0; p < 4; ++p) ms_host[p] = avg(p);
   // the same event pattern around empty launches: the per-launch gap
   {
     const int n = 64;

@@ -84,8 +84,7 @@ struct EngineDev {
   int gstride;     // granules per (kind, row tile): SAC_ROWS * (act_dim + 1)
   uint64_t* gran;  // [G_COUNT][nrt][gstride] data-tagged hand-off granules (gran_put)
   int upd_slots;  // update tiles: batch chunks staged per round (LDS slots, 1..4)
-  // update tiles, read by the fused launches (phase D inside phase A's launch,
-  // phase B inside phase C's launch)
+  // update tiles of phases B and D
   const TileDesc* tilesB;
   const TileDesc* tilesD;
   int nB, nD, nBq[2];
@@ -130,14 +129,6 @@ struct EngineDev {
   int gs2;
   int o_red;        // LDS: SAC_NW x 256 floats of k-split partial tiles
   int spin_limit;  // polls before a hand-off wait gives up and sets SYNC_TIMEOUT (~0.3 s at 1 << 22)
-  // persistent step (sac_persist.h): readiness counters [PC_COUNT][8 shards][16]
-  // + 1 exit word, the per-workgroup task table, producers per step of every
-  // counter, and an LDS word for the wait verdict (past every phase's layout)
-  int p_aqp;       // fused step: phase B's layers 0 / 1 start on the critics' pre-seed arrivals (PC_AQP)
-  uint32_t* pctr;
-  const void* ptasks;
-  uint32_t pc_n[8];
-  int o_pflag;
   // LDS layout (float offsets)
   int o_X, o_Y, o_P1[SAC_DEV_LAYERS], ldp1[SAC_DEV_LAYERS], o_P2[SAC_DEV_LAYERS], ldp2[SAC_DEV_LAYERS];
   int o_s, o_s2, o_a, o_a2, o_r, o_d, o_et, o_ea, o_out, o_outp, o_out2, o_outp2, o_lp, o_qt, o_y, o_g, o_g2,
@@ -146,8 +137,7 @@ struct EngineDev {
 
 // The gradient step a phase body works on: its device RNG step (indices, eps),
 // hand-off epoch (granule tags) and parity (double-buffered per-step state).
-// The per-phase kernels read them from memory at launch; the persistent step
-// (sac_persist.h) passes step k of its launch.
+// The phase kernels read them from memory at launch.
 struct StepCtx {
   uint64_t step;
   uint32_t ep;
@@ -171,9 +161,8 @@ struct TileDesc {
   float* tW;       // Polyak target master weight / bias / packed copy (critics)
   float* tb;
   void* tWc;
-  const float* dbp;
   long xt_par;     // element offset of the odd-step X^T copy (pi tiles), else 0
-  int K, N, Kp, Np, n0, k0, opt, nrt;
+  int K, N, Kp, Np, n0, k0, opt;
   int bp;          // batch columns this tile reduces over
   int ld, ldx;     // row strides of the GT / XT operands in elements (Bp; for a hidden-split
                    // layer 0 the parts' partial dY side by side, X duplicated)
@@ -192,12 +181,6 @@ struct TileDesc {
   // part order, and reduced once against X -- no batch parts, no hand-off
   long goff;
   int gsum;
-  int tile64;      // a 64 x 64 tile (dw_adam_tile64: large batches, no hidden split)
-  // the bias gradient is summed from the staged dY rows (every batch part its
-  // own columns, handed over like the seeded sums) instead of from the row
-  // tiles' partials, whose strided loads (256 row tiles at C3) made the
-  // k0 == 0 tiles the phase's tail (the default; SAC_BIAS_STAGED=0 clears it)
-  int bstage;
   // fp32 split critics (every layer): dY^T holds the unit-seed backward (phase
   // A's critic roles store it without waiting for y); every batch column b is
   // scaled by seed[b] (phase A's first target-critic half computes the seeds)
@@ -876,13 +859,6 @@ __device__ __forceinline__ float adam_elem(float& p, float& m, float& v, float g
   return pn;
 }
 
-// all threads: drain this workgroup's stores, then one lane counts the block done
-__device__ __forceinline__ void count_done(uint32_t* counter) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
 // One 32x32 weight tile of an update phase, UT threads:
 //   1. all threads stage the tile's 32 dY^T rows and 32 X^T rows (the dW GEMM's
 //      operands, K = batch) into LDS and fetch their elements' master weight,
@@ -905,33 +881,9 @@ __device__ __forceinline__ void count_done(uint32_t* counter) {
 // (>= the alpha block's 5 x 1024 floats)
 #define SAC_UPD_SLOT_BYTES (64 * 528)
 #define SAC_UPD_LDS_FOR(slots) ((slots) * SAC_UPD_SLOT_BYTES + 2 * 32 * 33 * 4 + 32 * 17 * 4)
-// Persistent mode (the whole step in one launch, sac_persist.h): the tile's
-// operands were written earlier in the same launch by other workgroups with
-// sc1 (write-through) stores, so every load of them is an sc1 buffer load
-// (MI355X_MICROARCH.md visibility, write-through form); its own element state
-// (masters, moments, targets: only this tile's workgroup writes them) is
-// loaded BEFORE waiting for the operands' producers; the step's Adam scalars
-// come from the caller (computed per step, no phase-A block); the biases and
-// the critics' W2 row (read by role workgroups) are stored sc1.
-struct UpdStep {
-  float neg_step, bc2s;  // this step's -lr / bias_correction1, sqrt(bias_correction2)
-  uint32_t ep;           // hand-off epoch of this step (batch-part granules)
-};
-struct NoWait {
-  template <typename... X>
-  __device__ __forceinline__ void operator()(X...) const {}
-};
-template <bool P>
-__device__ __forceinline__ u32x4 opnd16(const void* base, uint32_t byte_off) {
-  if constexpr (P)
-    return __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(coh_rsrc(base, 0xFFFFFFF0u), (int)byte_off,
-                                                                          0, 16));
-  return *(const AS_G u32x4*)((const AS_G char*)base + byte_off);
-}
-template <typename T, int UT, bool COH, int GS = 1, bool P = false, int MS = 4, typename Wait = NoWait>
+template <typename T, int UT, int GS = 1, int MS = 4>
 __device__ __forceinline__ void dw_adam_tile(const AS_C EngineDev& E, const TileDesc* tdp_, bool polyak, int par,
-                                             int par_x, lf* lds, const UpdStep* us = nullptr,
-                                             const Wait& wait = Wait()) {
+                                             int par_x, lf* lds) {
   constexpr int KC = MM<T>::KC, KL = MM<T>::KL;
   constexpr int EPR = 16 / sizeof(T);  // elements per 16-B piece (= KL)
   constexpr int EPT = 1024 / UT;       // elements per thread
@@ -952,9 +904,9 @@ __device__ __forceinline__ void dw_adam_tile(const AS_C EngineDev& E, const Tile
   lf* accs = lds + (ns * slot_el * (int)sizeof(T) + 15) / 16 * 4;
   lf* tgts = accs + 32 * 33;
   lf* red = tgts + 32 * 33;
-  // this step's Adam scalars (written by phase A; persistent: the caller's)
-  const float neg_step = P ? us->neg_step : GPC(float, E.adam_sc)[par * 6 + td.opt * 2];
-  const float bc2s = P ? us->bc2s : GPC(float, E.adam_sc)[par * 6 + td.opt * 2 + 1];
+  // this step's Adam scalars (written by phase A)
+  const float neg_step = GPC(float, E.adam_sc)[par * 6 + td.opt * 2];
+  const float bc2s = GPC(float, E.adam_sc)[par * 6 + td.opt * 2 + 1];
   // ---- 1. loads: the first round of staged operands, then element state + bias
   // state + bias partials, all before the first wait (one round trip; the bias
   // sums below wait for everything issued before them, in issue order)
@@ -972,7 +924,7 @@ __device__ __forceinline__ void dw_adam_tile(const AS_C EngineDev& E, const Tile
   const int ldg = td.ld, ldx = td.ldx;
   // round r0's slot sl -> rg[sl] (16-B pieces of the 32 dY^T rows of every part, then of the 32 X^T rows)
   // what: 1 operands, 2 seeds, 3 both
-  auto issue = [&](int r0, auto slc, int what = 3) {
+  auto issue = [&](int r0, auto slc) {
     constexpr int sl = decltype(slc)::value;
     const int b0 = r0 + sl * SAC_UPD_BCH;
     if (sl < ns && b0 < Bp) {  // uniform
@@ -985,23 +937,13 @@ __device__ __forceinline__ void dw_adam_tile(const AS_C EngineDev& E, const Tile
           const int i = threadIdx.x + pi * UT;
           const int row = i / per_row, pc = i % per_row;
           const AS_G T* src = op < GS ? gsrc + op * goff + (size_t)row * ldg : xsrc + (size_t)row * ldx;
-          if constexpr (P) {  // uniform bases, per-lane byte offsets: sc1 buffer loads
-            const AS_G T* base = op < GS ? gsrc : xsrc;
-            const uint32_t off = (uint32_t)((src - base + b0 + pc * EPR) * sizeof(T));
-            if ((what & 1) && i < 32 * per_row) rg[sl][op][pi] = opnd16<true>((const void*)base, off);
-            if constexpr (sizeof(T) == 4)
-              if ((what & 2) && op == 0 && seedp && i < 32 * per_row)
-                sdr[sl][pi] = __builtin_bit_cast(f32x4, opnd16<true>((const void*)seedp,
-                                                                      (uint32_t)((b0 + pc * EPR) * 4)));
-          } else {
-            if (i < 32 * per_row) rg[sl][op][pi] = *(const AS_G u32x4*)(src + b0 + pc * EPR);
-            if constexpr (sizeof(T) == 4)
-              if (op == 0 && seedp && i < 32 * per_row) sdr[sl][pi] = *(const AS_G f32x4*)(seedp + b0 + pc * EPR);
-          }
+          if (i < 32 * per_row) rg[sl][op][pi] = *(const AS_G u32x4*)(src + b0 + pc * EPR);
+          if constexpr (sizeof(T) == 4)
+            if (op == 0 && seedp && i < 32 * per_row) sdr[sl][pi] = *(const AS_G f32x4*)(seedp + b0 + pc * EPR);
         }
     }
   };
-  if (!P) static_for<MAXS>([&](auto sl) { issue(0, sl); });
+  static_for<MAXS>([&](auto sl) { issue(0, sl); });
   AS_G float* W = GP(float, td.W);
   AS_G float* Wm = GP(float, td.Wm);
   AS_G float* Wv = GP(float, td.Wv);
@@ -1016,7 +958,7 @@ __device__ __forceinline__ void dw_adam_tile(const AS_C EngineDev& E, const Tile
     ok[e] = n < td.N && k < td.K;
     idx[e] = ok[e] ? (size_t)n * td.K + k : 0;
     if (td.kpart < 2) {  // uniform: a producer part only computes its partial dW
-      p[e] = ldf<P>((const float*)(W + idx[e]));  // persistent: may have been stored sc1 (W2 row)
+      p[e] = W[idx[e]];
       m[e] = Wm[idx[e]];
       v[e] = Wv[idx[e]];
       tp[e] = polyak ? tW[idx[e]] : 0.f;
@@ -1025,51 +967,22 @@ __device__ __forceinline__ void dw_adam_tile(const AS_C EngineDev& E, const Tile
     }
   }
   const bool do_bias = td.k0 == 0 && td.kpart <= 1;
-  // seeded or TileDesc.bstage: the bias gradient is summed from the staged rows,
-  // every part its own columns
-  const bool bst = seedp || td.bstage;  // uniform
-  const bool bias_acc = td.k0 == 0 && (td.kpart <= 1 || bst);
+  // the bias gradient is summed from the staged (seed-scaled) dY rows, every
+  // batch part its own columns (handed over with the partial dW)
+  const bool bias_acc = td.k0 == 0;
   float pb = 0.f, mb = 0.f, vb = 0.f, tbv = 0.f;
   if (do_bias && tid < 32 && td.n0 + tid < td.N) {
-    pb = ldf<P>((const float*)td.b + td.n0 + tid);
+    pb = GPC(float, td.b)[td.n0 + tid];
     mb = GPC(float, td.bm)[td.n0 + tid];
     vb = GPC(float, td.bv)[td.n0 + tid];
-    if (polyak) tbv = ldf<P>((const float*)td.tb + td.n0 + tid);
+    if (polyak) tbv = GPC(float, td.tb)[td.n0 + tid];
   }
-  if constexpr (P) {  // the operands' producers, then the operands themselves
-    // wait(0): what the operands need (fp32 critics' layers 0 / 1: the
-    // unit-seed dY^T and X^T, stored before y is known); wait(1): everything
-    // (the seeds, the bias partials)
-    wait(0);
-    static_for<MAXS>([&](auto sl) { issue(0, sl, 1); });
-    wait(1);
-    static_for<MAXS>([&](auto sl) { issue(0, sl, 2); });
-  }
-  // bias gradient: the row tiles' partial sums, 16 partial lanes per column
-  // (512 lanes, BPT per thread: the same sums for 4-, 8- and 16-wave blocks);
-  // each lane's loads are issued 16 at a time (one round trip per 16 row tiles,
-  // not one per row tile: 256 row tiles at B = 4096) and added in row-tile order
-  constexpr int BPT = (512 + UT - 1) / UT, BU = 16;
+  // bias partial lanes: 16 per column (512 lanes, BPT per thread: the same sums
+  // for 8- and 16-wave blocks), summed in LDS in lane order below
+  constexpr int BPT = (512 + UT - 1) / UT;
   float bsum[BPT];
 #pragma unroll
-  for (int j = 0; j < BPT; ++j) {
-    const int t = tid + j * UT, bn = t >> 4, bs = t & 15;
-    bsum[j] = 0.f;
-    if (do_bias && !bst && t < 512 && td.n0 + bn < td.N) {
-      const AS_G float* dbp = GPC(float, td.dbp) + td.n0 + bn;
-      for (int rt0 = bs; rt0 < td.nrt; rt0 += 16 * BU) {
-        float pv[BU];
-#pragma unroll
-        for (int u = 0; u < BU; ++u) {
-          const int rt = rt0 + 16 * u;
-          pv[u] = rt < td.nrt ? ldf<P>((const float*)(dbp + (size_t)rt * td.N)) : 0.f;
-        }
-#pragma unroll
-        for (int u = 0; u < BU; ++u)
-          if (rt0 + 16 * u < td.nrt) bsum[j] += pv[u];
-      }
-    }
-  }
+  for (int j = 0; j < BPT; ++j) bsum[j] = 0.f;
   // ---- 2. dW = dY^T X over the batch, staged through LDS in 512-B row chunks,
   // nslot chunks per round; waves run (16x16 sub-tile, K-quarter) pairs, chunks
   // in batch order.  A slot's registers are re-issued for the next round as
@@ -1128,7 +1041,7 @@ __device__ __forceinline__ void dw_adam_tile(const AS_C EngineDev& E, const Tile
         issue(r0 + rstep, slc);
         __syncthreads();
         if (r0 == 0 && sl == 0) STAMP(polyak ? 51 : 55);
-        if (bst && bias_acc) {  // bias gradient: this lane's columns of the slot's (scaled) dY rows
+        if (bias_acc) {  // bias gradient: this lane's columns of the slot's (scaled) dY rows
 #pragma unroll
           for (int j = 0; j < BPT; ++j) {
             const int t = tid + j * UT, bn = t >> 4, bs = t & 15;
@@ -1202,14 +1115,14 @@ __device__ __forceinline__ void dw_adam_tile(const AS_C EngineDev& E, const Tile
 #pragma unroll
   for (int q = 0; q < MAXP; ++q) gbx[q] = 0.f;
   if (td.kpart) {  // hidden-split layer 0: the batch parts of this tile meet here
-    const uint32_t ep = P ? us->ep : *GPC(uint32_t, E.sync) + 1u;  // per launch (B and D have their own granules)
+    const uint32_t ep = *GPC(uint32_t, E.sync) + 1u;  // per launch (B and D have their own granules)
     if (td.kpart >= 2) {
       AS_G uint64_t* mine = GP(uint64_t, td.part) + (size_t)(td.kpart - 2) * SAC_PART_STRIDE;
       for (int el = tid; el < 1024; el += UT) {
         const uint64_t x = (uint64_t)__float_as_uint(accs[(el >> 5) * 33 + (el & 31)]) | ((uint64_t)ep << 32);
         __hip_atomic_store((uint64_t*)(mine + el), x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
-      if (bst && bias_acc && tid < 32) {
+      if (bias_acc && tid < 32) {
         float gb = 0.f;
         for (int q = 0; q < 16; ++q) gb += red[tid * 17 + q];
         const uint64_t x = (uint64_t)__float_as_uint(gb) | ((uint64_t)ep << 32);
@@ -1223,7 +1136,7 @@ __device__ __forceinline__ void dw_adam_tile(const AS_C EngineDev& E, const Tile
     constexpr int EL = 1024 / UT;
     static_assert(EL * UT == 1024 && EL <= 4, "granules per thread");
     const int np = td.nparts - 1;  // producer parts (1..MAXP)
-    const bool pb_here = bst && do_bias && tid < 32;
+    const bool pb_here = do_bias && tid < 32;
     float v[MAXP][EL];
     for (int it = 0;; ++it) {
       bool all = true;
@@ -1275,10 +1188,7 @@ __device__ __forceinline__ void dw_adam_tile(const AS_C EngineDev& E, const Tile
     tn[e] = 0.f;
     if (ok[e]) {
       pn[e] = adam_elem(p[e], m[e], v[e], accs[(el >> 5) * 33 + (el & 31)], w1, b2, w2, bc2s, eps, neg_step);
-      if (P && polyak && td.N == 1)  // a critic's W2 row: the role workgroups read the fp32 master
-        coh_storef((float*)(W + idx[e]), p[e]);
-      else
-        W[idx[e]] = p[e];
+      W[idx[e]] = p[e];
       Wm[idx[e]] = m[e];
       Wv[idx[e]] = v[e];
       if (polyak) {
@@ -1297,16 +1207,13 @@ __device__ __forceinline__ void dw_adam_tile(const AS_C EngineDev& E, const Tile
   if (do_bias && tid < 32 && td.n0 + tid < td.N) {
     float gb = 0.f;
     for (int q = 0; q < 16; ++q) gb += red[tid * 17 + q];
-    if (bst && td.kpart) {  // the other batch parts' sums, in part order
+    if (td.kpart) {  // the other batch parts' sums, in part order
 #pragma unroll
       for (int q = 0; q < MAXP; ++q)
         if (q < td.nparts - 1) gb += gbx[q];
     }
     const float pbn = adam_elem(pb, mb, vb, gb, w1, b2, w2, bc2s, eps, neg_step);
-    if (COH)
-      coh_storef((float*)td.b + td.n0 + tid, pb);
-    else
-      GP(float, td.b)[td.n0 + tid] = pb;
+    GP(float, td.b)[td.n0 + tid] = pb;
     GP(float, td.bm)[td.n0 + tid] = mb;
     GP(float, td.bv)[td.n0 + tid] = vb;
     if (polyak) GP(float, td.tb)[td.n0 + tid] = tau * pbn + omt * tbv;  // read by the next step's launch only
@@ -1316,19 +1223,6 @@ __device__ __forceinline__ void dw_adam_tile(const AS_C EngineDev& E, const Tile
   constexpr int PPR = 32 / EPR;  // pieces per 32-element tile row
   for (int mat = 0; mat < (polyak ? 3 : 2); ++mat) {  // uniform: one buffer descriptor per matrix
     const void* base = mat == 0 ? td.Wc : mat == 1 ? td.WTc : td.tWc;
-    // the fused step reads the online critics' copies in the same launch (phase
-    // C); the targets' only in the next launch: plain write-back stores for those
-    if (P && mat == 2) {
-      for (int i = tid; i < 32 * PPR; i += UT) {
-        const int row = i / PPR, pc = i % PPR;
-        T vv[EPR];
-#pragma unroll
-        for (int j = 0; j < EPR; ++j) vv[j] = MM<T>::cvt(tgts[row * 33 + pc * EPR + j]);
-        coh_store16<false>(base, (uint32_t)(packed_off<T>(td.n0 + row, td.k0 + pc * EPR, td.Kp) * sizeof(T)),
-                           *(const u32x4*)vv);
-      }
-      continue;
-    }
     for (int i = tid; i < 32 * PPR; i += UT) {
       const int row = i / PPR, pc = i % PPR;
       T vv[EPR];
@@ -1343,302 +1237,22 @@ __device__ __forceinline__ void dw_adam_tile(const AS_C EngineDev& E, const Tile
         for (int j = 0; j < EPR; ++j) vv[j] = MM<T>::cvt(srcm[row * 33 + pc * EPR + j]);
         off = packed_off<T>(td.n0 + row, td.k0 + pc * EPR, td.Kp);
       }
-      coh_store16<COH>(base, (uint32_t)(off * sizeof(T)), *(const u32x4*)vv);
-    }
-  }
-}
-
-// ---------------------------------------------------------------------------- 64 x 64 update tiles
-// Large batches (Bp > 1024, no hidden split; TileDesc.tile64): one workgroup
-// updates a 64 x 64 block of a weight matrix -- the 32 x 32 tile's three steps
-// (dw_adam_tile above) on four times the outputs per staged operand row, so
-// half the operand bytes per weight.  At C3 the update phases are bound by the
-// operand bytes each CU has in flight (profiles/r04_pmc_c3_fp32.json: B fetches
-// 78 MB in 38 us, ~30 GB/s per CU), not by the MFMAs.  Rows past the padded
-// widths (Np, Kp) are neither loaded nor stored; elements past (N, K) are not
-// updated.  Batch parts as the 32 x 32 tiles (granule hand-off to part 1), with
-// SAC_PART_STRIDE64 granules per producer part and no bias granules (the bias
-// gradient is the row tiles' partial sums, read whole by part 1).
-#define SAC_PART_STRIDE64 4096
-#define SAC_UPD64_SLOT_BYTES (128 * 528)
-#define SAC_UPD64_LDS (2 * SAC_UPD64_SLOT_BYTES + 64 * 17 * 4)
-template <typename T, int UT>
-__device__ __forceinline__ void dw_adam_tile64(const AS_C EngineDev& E, const TileDesc* tdp_, bool polyak, int par,
-                                               int par_x, lf* lds) {
-  static_assert(UT == 1024, "16 waves: one 16 x 16 sub-tile each");
-  constexpr int KC = MM<T>::KC, KL = MM<T>::KL;
-  constexpr int EPR = 16 / sizeof(T);            // elements per 16-B piece
-  constexpr int BCH = 512 / (int)sizeof(T);      // batch columns per staged chunk (512 B per row)
-  constexpr int EPT = 4096 / UT;                 // elements per thread
-  constexpr int NS = 2;                          // chunks (LDS slots) per round
-  constexpr int PPO = 64 * (BCH / EPR) / UT;     // pieces per thread per operand per chunk
-  static_assert(PPO >= 1 && 64 * (BCH / EPR) % UT == 0, "whole pieces per thread");
-  const AS_C TileDesc& td = *(const AS_C TileDesc*)tdp_;
-  const int tid = threadIdx.x, lane = tid & 63, wave = wave_id();
-  const int c = lane & 15, g = lane >> 4;
-  const int Bp = td.bp;
-  constexpr int LROW = BCH + 16 / (int)sizeof(T);  // T elements per staged row (+16 B: rows on different banks)
-  static_assert(LROW * (int)sizeof(T) * 128 == SAC_UPD64_SLOT_BYTES, "slot size");
-  AS_L T* stage = (AS_L T*)lds;
-  constexpr int SLOT = 128 * LROW;  // T elements per slot: dY^T rows 0..63, then X^T rows 64..127
-  lf* red = lds + NS * SAC_UPD64_SLOT_BYTES / 4;  // [64][17] bias partial lanes
-  const float neg_step = GPC(float, E.adam_sc)[par * 6 + td.opt * 2];
-  const float bc2s = GPC(float, E.adam_sc)[par * 6 + td.opt * 2 + 1];
-  const AS_G T* const gsrc = GPC(T, td.GT);
-  const AS_G T* const xsrc = GPC(T, td.XT) + par_x * td.xt_par;
-  const int ldg = td.ld, ldx = td.ldx;
-  const int gr = min(64, td.Np - td.n0), xr = min(64, td.Kp - td.k0);  // operand rows that exist
-  u32x4 rg[NS][2][PPO];
-  auto issue = [&](int r0, auto slc) {
-    constexpr int sl = decltype(slc)::value;
-    const int b0 = r0 + sl * BCH;
-    if (b0 < Bp) {  // uniform
-      const int per_row = min(Bp - b0, BCH) / EPR;
-#pragma unroll
-      for (int op = 0; op < 2; ++op)
-#pragma unroll
-        for (int pi = 0; pi < PPO; ++pi) {
-          // unconditional loads (a per-lane "load or not" makes hipcc wait for each
-          // load before the next): rows past the operand's end re-load its last row
-          const int i = tid + pi * UT, pc = i % per_row;
-          const int row = min(i / per_row, (op ? xr : gr) - 1);
-          const AS_G T* src = op ? xsrc + (size_t)row * ldx : gsrc + (size_t)row * ldg;
-          rg[sl][op][pi] = *(const AS_G u32x4*)(src + b0 + pc * EPR);
-        }
-    }
-  };
-  static_for<NS>([&](auto sl) { issue(0, sl); });
-  // element state (4 elements per thread), bias state, bias partials: one round trip with the operands
-  AS_G float* W = GP(float, td.W);
-  AS_G float* Wm = GP(float, td.Wm);
-  AS_G float* Wv = GP(float, td.Wv);
-  AS_G float* tW = GP(float, td.tW);
-  float p[EPT], m[EPT], v[EPT], tp[EPT];
-  size_t idx[EPT];
-  bool ok[EPT];
-#pragma unroll
-  for (int e = 0; e < EPT; ++e) {
-    const int el = tid + e * UT, en = el >> 6, ek = el & 63;
-    const int n = td.n0 + en, k = td.k0 + ek;
-    ok[e] = n < td.N && k < td.K;
-    idx[e] = ok[e] ? (size_t)n * td.K + k : 0;
-    if (td.kpart < 2) {
-      p[e] = W[idx[e]];
-      m[e] = Wm[idx[e]];
-      v[e] = Wv[idx[e]];
-      tp[e] = polyak ? tW[idx[e]] : 0.f;
-    } else {
-      p[e] = m[e] = v[e] = tp[e] = 0.f;
-    }
-  }
-  const bool do_bias = td.k0 == 0 && td.kpart <= 1;
-  float pb = 0.f, mb = 0.f, vb = 0.f, tbv = 0.f;
-  if (do_bias && tid < 64 && td.n0 + tid < td.N) {
-    pb = GPC(float, td.b)[td.n0 + tid];
-    mb = GPC(float, td.bm)[td.n0 + tid];
-    vb = GPC(float, td.bv)[td.n0 + tid];
-    if (polyak) tbv = GPC(float, td.tb)[td.n0 + tid];
-  }
-  // bias gradient: the row tiles' partial sums, 16 lanes per column (64 x 16 = 1024 lanes),
-  // 16 loads in flight per lane, added in row-tile order
-  float bsum = 0.f;
-  {
-    const int bn = tid >> 4, bs = tid & 15;
-    if (do_bias && td.n0 + bn < td.N) {
-      const AS_G float* dbp = GPC(float, td.dbp) + td.n0 + bn;
-      constexpr int BU = 16;
-      for (int rt0 = bs; rt0 < td.nrt; rt0 += 16 * BU) {
-        float pv[BU];
-#pragma unroll
-        for (int u = 0; u < BU; ++u) {
-          const int rt = rt0 + 16 * u;
-          pv[u] = rt < td.nrt ? dbp[(size_t)rt * td.N] : 0.f;
-        }
-#pragma unroll
-        for (int u = 0; u < BU; ++u)
-          if (rt0 + 16 * u < td.nrt) bsum += pv[u];
-      }
-    }
-  }
-  // ---- dW = dY^T X over the batch: chunk by chunk through LDS, NS chunks per
-  // round, the next round's loads issued as soon as a chunk is in LDS; wave w
-  // owns the 16 x 16 sub-tile (rows 16 (w >> 2), columns 16 (w & 3)) over every chunk
-  const int sn = (wave >> 2) * 16, sk = (wave & 3) * 16;
-  f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
-  for (int r0 = 0; r0 < Bp; r0 += NS * BCH) {
-    static_for<NS>([&](auto slc) {
-      constexpr int sl = decltype(slc)::value;
-      const int b0 = r0 + sl * BCH;
-      if (b0 < Bp) {  // uniform
-        const int bch = min(Bp - b0, BCH);
-        const int per_row = bch / EPR;
-#pragma unroll
-        for (int op = 0; op < 2; ++op)
-#pragma unroll
-          for (int pi = 0; pi < PPO; ++pi) {
-            const int i = tid + pi * UT, pc = i % per_row;
-            const int row = min(i / per_row, (op ? xr : gr) - 1);  // (same clamp: duplicates write equal data)
-            *(AS_L u32x4*)(stage + sl * SLOT + (row + 64 * op) * LROW + pc * EPR) = rg[sl][op][pi];
-          }
-        issue(r0 + NS * BCH, slc);
-        __syncthreads();
-        const AS_L T* arow = stage + sl * SLOT + (sn + c) * LROW + g * KL;
-        const AS_L T* brow = stage + sl * SLOT + (64 + sk + c) * LROW + g * KL;
-        const int nchk = bch / KC;
-        auto frag = [&](const AS_L T* r, int ch) __attribute__((always_inline)) {
-          if constexpr (sizeof(T) == 2) return *(const AS_L bf16x8*)(r + ch * KC);
-          else return *(const AS_L f32x4*)(r + ch * KC);
-        };
-        for (int ch = 0; ch < nchk; ch += 2) {  // two accumulators: even / odd chunks
-          MM<T>::mma(acc0, frag(arow, ch), frag(brow, ch));
-          if (ch + 1 < nchk) MM<T>::mma(acc1, frag(arow, ch + 1), frag(brow, ch + 1));
-        }
-      }
-    });
-    __syncthreads();  // the slots are refilled by the next round
-  }
-  // ---- partial dW -> LDS [64][65] (the free stage), bias lanes -> red
-  lf* accs = (lf*)stage;
-  lf* tgts = accs + 64 * 65;
-  {
-    const f32x4 a = acc0 + acc1;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) accs[(sn + g * 4 + i) * 65 + sk + c] = a[i];
-  }
-  red[(tid >> 4) * 17 + (tid & 15)] = bsum;
-  __syncthreads();
-  if (td.kpart) {  // batch parts of this tile meet at part 1
-    const uint32_t ep = *GPC(uint32_t, E.sync) + 1u;
-    if (td.kpart >= 2) {
-      AS_G uint64_t* mine = GP(uint64_t, td.part) + (size_t)(td.kpart - 2) * SAC_PART_STRIDE64;
-#pragma unroll
-      for (int e = 0; e < EPT; ++e) {
-        const int el = tid + e * UT;
-        const uint64_t x = (uint64_t)__float_as_uint(accs[(el >> 6) * 65 + (el & 63)]) | ((uint64_t)ep << 32);
-        __hip_atomic_store((uint64_t*)(mine + el), x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-      return;  // uniform: part 1 runs Adam on the sum
-    }
-    const int np = td.nparts - 1;  // producer parts (1..7)
-    float sum[EPT];
-#pragma unroll
-    for (int e = 0; e < EPT; ++e) {
-      const int el = tid + e * UT;
-      sum[e] = accs[(el >> 6) * 65 + (el & 63)];
-    }
-    // every producer part's granules of this thread in one batch of loads per
-    // attempt (one round trip, not one per part); parts added in order
-    constexpr int MAXP = 7;
-    float vq[MAXP][EPT];
-    for (int it = 0;; ++it) {
-      bool all = true;
-#pragma unroll
-      for (int q = 0; q < MAXP; ++q)
-        if (q < np)
-#pragma unroll
-          for (int e = 0; e < EPT; ++e) {
-            const uint64_t x = __hip_atomic_load(td.part + (size_t)q * SAC_PART_STRIDE64 + tid + e * UT,
-                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            all = all && (uint32_t)(x >> 32) == ep;
-            vq[q][e] = __uint_as_float((uint32_t)x);
-          }
-      if (all) break;
-      if (it > E.spin_limit) {  // a producer part never ran: flag the error, do not hang
-        __hip_atomic_store((uint32_t*)GP(uint32_t, E.sync) + 1 /* SYNC_TIMEOUT */, 1u, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-        break;
-      }
-      __builtin_amdgcn_s_sleep(1);
-    }
-#pragma unroll
-    for (int q = 0; q < MAXP; ++q)
-      if (q < np)
-#pragma unroll
-        for (int e = 0; e < EPT; ++e) sum[e] += vq[q][e];
-    __syncthreads();  // every read of accs done
-#pragma unroll
-    for (int e = 0; e < EPT; ++e) {
-      const int el = tid + e * UT;
-      accs[(el >> 6) * 65 + (el & 63)] = sum[e];
-    }
-    __syncthreads();
-  }
-  // ---- elements: Adam + Polyak on the masters; new values -> LDS
-  const float w1 = (float)(1.0 - (double)E.beta1), b2 = E.beta2, w2 = (float)(1.0 - (double)E.beta2);
-  const float eps = E.adam_eps, tau = E.tau, omt = (float)(1.0 - (double)E.tau);
-  float pn[EPT], tn[EPT];
-#pragma unroll
-  for (int e = 0; e < EPT; ++e) {
-    const int el = tid + e * UT;
-    pn[e] = 0.f;
-    tn[e] = 0.f;
-    if (ok[e]) {
-      pn[e] = adam_elem(p[e], m[e], v[e], accs[(el >> 6) * 65 + (el & 63)], w1, b2, w2, bc2s, eps, neg_step);
-      W[idx[e]] = p[e];
-      Wm[idx[e]] = m[e];
-      Wv[idx[e]] = v[e];
-      if (polyak) {
-        tn[e] = tau * pn[e] + omt * tp[e];
-        tW[idx[e]] = tn[e];
-      }
-    }
-  }
-  __syncthreads();
-#pragma unroll
-  for (int e = 0; e < EPT; ++e) {
-    const int el = tid + e * UT;
-    accs[(el >> 6) * 65 + (el & 63)] = pn[e];  // padding elements: 0, as packed
-    if (polyak) tgts[(el >> 6) * 65 + (el & 63)] = tn[e];
-  }
-  if (do_bias && tid < 64 && td.n0 + tid < td.N) {
-    float gb = 0.f;
-    for (int q = 0; q < 16; ++q) gb += red[tid * 17 + q];
-    const float pbn = adam_elem(pb, mb, vb, gb, w1, b2, w2, bc2s, eps, neg_step);
-    GP(float, td.b)[td.n0 + tid] = pb;
-    GP(float, td.bm)[td.n0 + tid] = mb;
-    GP(float, td.bv)[td.n0 + tid] = vb;
-    if (polyak) GP(float, td.tb)[td.n0 + tid] = tau * pbn + omt * tbv;
-  }
-  __syncthreads();
-  // ---- packed copies as 16-B pieces (rows past Np / Kp do not exist)
-  constexpr int PPR = 64 / EPR;  // pieces per 64-element row
-  for (int mat = 0; mat < (polyak ? 3 : 2); ++mat) {
-    const void* base = mat == 0 ? td.Wc : mat == 1 ? td.WTc : td.tWc;
-    for (int i = tid; i < 64 * PPR; i += UT) {
-      const int row = i / PPR, pc = i % PPR;
-      T vv[EPR];
-      size_t off;
-      if (mat == 1) {  // W^T: row k = k0 + row, columns n = n0 + pc * EPR + j
-        if (row >= xr || pc * EPR >= gr) continue;
-#pragma unroll
-        for (int j = 0; j < EPR; ++j) vv[j] = MM<T>::cvt(accs[(pc * EPR + j) * 65 + row]);
-        off = packed_off<T>(td.k0 + row, td.n0 + pc * EPR, td.Np);
-      } else {  // W or target W: row n = n0 + row, columns k = k0 + pc * EPR + j
-        if (row >= gr || pc * EPR >= xr) continue;
-        const lf* srcm = mat == 0 ? accs : tgts;
-#pragma unroll
-        for (int j = 0; j < EPR; ++j) vv[j] = MM<T>::cvt(srcm[row * 65 + pc * EPR + j]);
-        off = packed_off<T>(td.n0 + row, td.k0 + pc * EPR, td.Kp);
-      }
-      *(AS_G u32x4*)((AS_G char*)base + off * sizeof(T)) = *(const u32x4*)vv;
+      coh_store16<false>(base, (uint32_t)(off * sizeof(T)), *(const u32x4*)vv);
     }
   }
 }
 
 // a tile with summed dY parts (hidden-split layer 0) runs its own instance
-template <typename T, int UT, bool COH, bool P = false, int MS = 4, typename Wait = NoWait>
+template <typename T, int UT, int MS = 4>
 __device__ __forceinline__ void dw_adam_tile_any(const AS_C EngineDev& E, const TileDesc* tdp_, bool polyak, int par,
-                                                 int par_x, lf* lds, const UpdStep* us = nullptr,
-                                                 const Wait& wait = Wait()) {
-  if constexpr (!P && UT == 1024)
-    if (((const AS_C TileDesc*)tdp_)->tile64) return dw_adam_tile64<T, UT>(E, tdp_, polyak, par, par_x, lds);
+                                                 int par_x, lf* lds) {
   if constexpr (MS >= 4) {  // (MS 2: the 512-thread phase B, never with the hidden split's summed tiles)
     const int gs = ((const AS_C TileDesc*)tdp_)->gsum;  // uniform
     if constexpr (sizeof(T) == 4)
-      if (gs == 4) return dw_adam_tile<T, UT, COH, 4, P, MS>(E, tdp_, polyak, par, par_x, lds, us, wait);
-    if (gs == 2) return dw_adam_tile<T, UT, COH, 2, P, MS>(E, tdp_, polyak, par, par_x, lds, us, wait);
+      if (gs == 4) return dw_adam_tile<T, UT, 4, MS>(E, tdp_, polyak, par, par_x, lds);
+    if (gs == 2) return dw_adam_tile<T, UT, 2, MS>(E, tdp_, polyak, par, par_x, lds);
   }
-  dw_adam_tile<T, UT, COH, 1, P, MS>(E, tdp_, polyak, par, par_x, lds, us, wait);
+  dw_adam_tile<T, UT, 1, MS>(E, tdp_, polyak, par, par_x, lds);
 }
 
 // One block: reduces the step's loss partials into stats[0..3] and runs the
@@ -1646,32 +1260,25 @@ __device__ __forceinline__ void dw_adam_tile_any(const AS_C EngineDev& E, const 
 // (no early exit: the caller's completion barrier follows).  alpha_state is
 // stored sc1: the critics of a phase A sharing the launch read alpha after the
 // completion counter.
-// P (persistent step): log pi, the loss partials and the alpha state were
-// stored sc1 earlier in the launch: sc1 loads; bc[2] = this step's alpha Adam
-// bias corrections (else read from E.alpha_sc, written by phase A).
-__device__ __forceinline__ double ldd_coh(const double* p) {
-  return __hip_atomic_load((double*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-template <bool P = false>
-__device__ __forceinline__ void alpha_and_losses(const AS_C EngineDev& E, int par, lf* red, const double* bc = nullptr) {
+__device__ __forceinline__ void alpha_and_losses(const AS_C EngineDev& E, int par, lf* red) {
   const int tid = threadIdx.x, NT = blockDim.x, B = E.B;
   const float H = E.target_entropy;
   AS_G double* st = GP(double, E.alpha_state);
-  const double st0 = P ? ldd_coh((const double*)st) : st[0];
+  const double st0 = st[0];
   const float la32 = (float)st0;
   const float mB = -1.0f / (float)B;
   const AS_G float* lp = GPC(float, E.lp_st) + par * E.Br;
   const AS_G float* lossp = GPC(float, E.lossp) + par * E.nrt * 4;
   float sg = 0.f, sl = 0.f, l0 = 0.f, l1 = 0.f, l2 = 0.f;
   for (int b = tid; b < B; b += NT) {
-    const float term = ldf<P>((const float*)(lp + b)) + H;
+    const float term = lp[b] + H;
     sg += mB * term;
     sl += la32 * term;
   }
   for (int rt = tid; rt < E.nrt; rt += NT) {
-    l0 += ldf<P>((const float*)(lossp + rt * 4 + 0));
-    l1 += ldf<P>((const float*)(lossp + rt * 4 + 1));
-    l2 += ldf<P>((const float*)(lossp + rt * 4 + 2));
+    l0 += lossp[rt * 4 + 0];
+    l1 += lossp[rt * 4 + 1];
+    l2 += lossp[rt * 4 + 2];
   }
   red[0 * NT + tid] = sg;
   red[1 * NT + tid] = sl;
@@ -1693,11 +1300,11 @@ __device__ __forceinline__ void alpha_and_losses(const AS_C EngineDev& E, int pa
     if (E.auto_entropy && E.alpha_update) {
       const double gr = (double)red[0];
       const double b1 = (double)E.beta1, b2 = (double)E.beta2;
-      const double st2 = P ? ldd_coh((const double*)st + 2) : st[2], st3 = P ? ldd_coh((const double*)st + 3) : st[3];
+      const double st2 = st[2], st3 = st[3];
       const double m = st2 + (1.0 - b1) * (gr - st2);
       const double v = st3 * b2 + (1.0 - b2) * gr * gr;
-      const double bc1 = P ? bc[0] : GPC(double, E.alpha_sc)[par * 2];
-      const double bc2 = P ? bc[1] : GPC(double, E.alpha_sc)[par * 2 + 1];
+      const double bc1 = GPC(double, E.alpha_sc)[par * 2];
+      const double bc2 = GPC(double, E.alpha_sc)[par * 2 + 1];
       const double denom = sqrt(v) / sqrt(bc2) + (double)E.adam_eps;
       const double la = st0 + (-(E.alpha_lr / bc1)) * m / denom;
       double* sd = (double*)E.alpha_state;
@@ -1719,13 +1326,13 @@ __device__ __forceinline__ void alpha_and_losses(const AS_C EngineDev& E, int pa
 // joins the others at a barrier.  Flags carry a per-launch epoch (E.sync[0] + 1,
 // advanced by phase C), so they are never reset.  Producers have lower block
 // indices than their consumers in every layout (phase A: pi(s') -> target
-// critics -> critics; phase C: critics -> pi; fused: update tiles first), so
+// critics -> critics; phase C: critics -> pi), so
 // in-order dispatch gives every spinning consumer resident producers; spins are
 // still bounded (E.spin_limit) and set E.sync[1] on a timeout, which the host
 // API turns into an error (sac_engine_read_status, SacEngine._poll_status).
 enum HandKind { HK_PI = 0, HK_T1 = 1, HK_T2 = 2, HK_C1 = 3, HK_C2 = 4, HK_COUNT = 5 };
 // SYNC_STAGED (u64 at words 4-5): step whose phase A last used a staged batch record
-enum SyncWord { SYNC_EPOCH = 0, SYNC_TIMEOUT = 1, SYNC_STAGED = 4, SYNC_DDONE = 16, SYNC_BDONE = 32, SYNC_CDONE = 64, SYNC_FLAGS = 128 };
+enum SyncWord { SYNC_EPOCH = 0, SYNC_TIMEOUT = 1, SYNC_STAGED = 4, SYNC_CDONE = 64, SYNC_FLAGS = 128 };
 #define SAC_HAND_STRIDE 576  // floats per (kind, row tile) payload: >= SAC_ROWS * (act_dim + 1)
 
 __device__ __forceinline__ AS_G uint32_t* hand_flag(const AS_C EngineDev& E, int kind, int rbi) {
@@ -1773,22 +1380,6 @@ __device__ __forceinline__ void hand_wait2(const AS_C EngineDev& E, int k1, int 
       if (a == ep && b == ep) break;
       if (it > E.spin_limit) {
         __hip_atomic_store((uint32_t*)GP(uint32_t, E.sync) + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        break;
-      }
-      __builtin_amdgcn_s_sleep(2);
-    }
-  }
-  __syncthreads();
-}
-
-// all threads: returns once *counter >= target (one polling lane, one barrier)
-__device__ __forceinline__ void count_wait(const AS_C EngineDev& E, int word, uint32_t target) {
-  if (threadIdx.x == 0) {
-    uint32_t* c = (uint32_t*)E.sync + word;
-    for (int it = 0; __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target; ++it) {
-      if (it > E.spin_limit) {
-        __hip_atomic_store((uint32_t*)GP(uint32_t, E.sync) + SYNC_TIMEOUT, 1u, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
         break;
       }
       __builtin_amdgcn_s_sleep(2);
@@ -2007,11 +1598,7 @@ __device__ __forceinline__ void stage_next_batch(const AS_C EngineDev& E, const 
 // sample + gather, pi on [s'; s], target twin-Q -> y, critics forward + backward.
 // ROLES: block = role * nrt + row tile; role 0 pi on s' (target sample), 1/2
 // target critics, 3/4 critics, 5 pi on s (actor sample, stashed for phase C).
-// WITH_D (role split only): blocks [0, nD] first run the PREVIOUS step's phase
-// D (pi tiles, then the alpha block) and count themselves done; the pi roles
-// wait for that count before streaming pi's weights, everything else of phase
-// A (sampling, gathers, the critics' forward) overlaps it.
-template <typename T, bool ROLES, bool WITH_D>
+template <typename T, bool ROLES>
 __device__ __forceinline__ void target_critic_body(const EngineDev* __restrict__ Ep, const sac_replay& rb,
                                                    const int32_t* __restrict__ inj_idx_,
                                                    const float* __restrict__ inj_eps_) {
@@ -2021,21 +1608,7 @@ __device__ __forceinline__ void target_critic_body(const EngineDev* __restrict__
   lf* lds = (lf*)lds_raw;
   constexpr int R = SAC_ROWS;
   const int tid = threadIdx.x;
-  int bid = blockIdx.x;
-  if (WITH_D) {
-    // grid order = dispatch order: the phase D blocks (producers of pi's new
-    // weights) first, then the roles; the pi roles wait for D's count
-    if (bid <= E.nD) {
-      const int parD = (int)((*GPC(uint64_t, E.rng_step) - 1) & 1);  // the step phase C just closed
-      if (bid < E.nD)
-        dw_adam_tile_any<T, SAC_THREADS, true>(E, E.tilesD + bid, false, parD, parD, lds);
-      else
-        alpha_and_losses(E, parD, lds);
-      count_done((uint32_t*)E.sync + SYNC_DDONE);
-      return;
-    }
-    bid -= E.nD + 1;
-  }
+  const int bid = blockIdx.x;
   int rbi, role;
   if (ROLES) {
     rbi = bid % E.nrt;
@@ -2085,9 +1658,9 @@ __device__ __forceinline__ void target_critic_body(const EngineDev* __restrict__
   // order) does not also wait for ~72 KB of cold weights (they land under the
   // eps draw and the X build)
   constexpr int MXS = 4;  // staged floats of s / s' per thread, at most
-  const bool late_ph1 = !WITH_D && ROLES && role == 0 && E.stage && !inj_idx_ &&
+  const bool late_ph1 = ROLES && role == 0 && E.stage && !inj_idx_ &&
                         SAC_ROWS * E.O <= MXS * SAC_THREADS && SAC_ROWS * E.A <= SAC_THREADS;
-  if (!WITH_D && ROLES && role == 0 && !late_ph1) {
+  if (ROLES && role == 0 && !late_ph1) {
     held_issue<T, 1>(ph0, gw_fwd(pi.l[0]));
     held_issue<T, 8>(ph1, gw_fwd(pi.l[1]));
   }
@@ -2099,10 +1672,6 @@ __device__ __forceinline__ void target_critic_body(const EngineDev* __restrict__
   // draws the same indices from (seed, step), so no role waits for another's gather
   const uint64_t step = *GPC(uint64_t, E.rng_step);
   const int par = (int)(step & 1);  // step parity: selects the double-buffered per-step state
-  if ((!ROLES || role == 0) && rbi == 0 && tid == 0) {  // phase B of this step counts from 0
-    GP(uint32_t, E.sync)[SYNC_BDONE] = 0u;
-    GP(uint32_t, E.sync)[SYNC_BDONE + 16] = 0u;
-  }
   if ((!ROLES || role == 0) && rbi == 0 && tid < 4 && (tid < 3 || (E.auto_entropy && E.alpha_update))) {
     const double t = GP(double, E.opt_steps)[tid] + 1.0;
     GP(double, E.opt_steps)[tid] = t;
@@ -2230,11 +1799,11 @@ __device__ __forceinline__ void target_critic_body(const EngineDev* __restrict__
       const int ldl = out ? ldo : ld;
       const GemmW nx = out ? gw_fwd(E.net[NET_Q1T].l[0]) : gw_fwd(pi.l[l + 1]);
       if (l == 0)
-        layer_fwd<T, ROWS, WITH_D, 1>(X, ld, Ly, pi.P + Ly.b_off, act_l, Pl, ldl, Yl, ldl, stash, a0, pf, nx, &ph0);
+        layer_fwd<T, ROWS, false, 1>(X, ld, Ly, pi.P + Ly.b_off, act_l, Pl, ldl, Yl, ldl, stash, a0, pf, nx, &ph0);
       else if (l == 1)
-        layer_fwd<T, ROWS, WITH_D, 8>(X, ld, Ly, pi.P + Ly.b_off, act_l, Pl, ldl, Yl, ldl, stash, a0, pf, nx, &ph1);
+        layer_fwd<T, ROWS, false, 8>(X, ld, Ly, pi.P + Ly.b_off, act_l, Pl, ldl, Yl, ldl, stash, a0, pf, nx, &ph1);
       else
-        layer_fwd<T, ROWS, WITH_D>(X, ld, Ly, pi.P + Ly.b_off, act_l, Pl, ldl, Yl, ldl, stash, a0, pf, nx);
+        layer_fwd<T, ROWS, false>(X, ld, Ly, pi.P + Ly.b_off, act_l, Pl, ldl, Yl, ldl, stash, a0, pf, nx);
       __syncthreads();
       STAMP(2 + l);
       lf* t = X;
@@ -2297,13 +1866,6 @@ __device__ __forceinline__ void target_critic_body(const EngineDev* __restrict__
   if (!ROLES) {
     pi_forward_head(std::integral_constant<int, 2 * R>(), true, true);
   } else if (role == 0 || role == 5) {
-    if (WITH_D) {
-      count_wait(E, SYNC_DDONE, (uint32_t)E.nD + 1u);  // pi updated by the previous step's phase D
-      if (role == 0) {
-        held_issue<T, 1, true>(ph0, gw_fwd(pi.l[0]));
-        held_issue<T, 8, true>(ph1, gw_fwd(pi.l[1]));
-      }
-    }
     STAMP(59);
     pi_forward_head(std::integral_constant<int, R>(), role == 0, role == 5);
   }
@@ -2435,11 +1997,11 @@ __device__ __forceinline__ void target_critic_body(const EngineDev* __restrict__
   }
 }
 
-template <typename T, bool ROLES, bool WITH_D>
+template <typename T, bool ROLES>
 __global__ void __launch_bounds__(SAC_THREADS) sac_target_critic(const EngineDev* __restrict__ Ep, sac_replay rb,
                                                                   const int32_t* __restrict__ inj_idx_,
                                                                   const float* __restrict__ inj_eps_) {
-  target_critic_body<T, ROLES, WITH_D>(Ep, rb, inj_idx_, inj_eps_);
+  target_critic_body<T, ROLES>(Ep, rb, inj_idx_, inj_eps_);
   const AS_C EngineDev& E = *(const AS_C EngineDev*)Ep;
   (void)E;
   END_STAMP(60);
@@ -2452,7 +2014,7 @@ __global__ void __launch_bounds__(SAC_THREADS) sac_target_critic(const EngineDev
 // A critic role back-propagates a UNIT seed (d Q_i / d a~) and hands (q_i,
 // dQ_i/da~) to the pi role, which applies the min-Q weights -1/B, -1/2B or 0
 // (powers of two for power-of-two batches: bit-identical to seeding them).
-template <typename T, bool ROLES, bool WITH_B>
+template <typename T, bool ROLES>
 __device__ __forceinline__ void actor_body(const EngineDev* __restrict__ Ep, int bid) {
   const AS_C EngineDev& E = *(const AS_C EngineDev*)Ep;
   extern __shared__ float lds_raw[];
@@ -2510,12 +2072,11 @@ __device__ __forceinline__ void actor_body(const EngineDev* __restrict__ Ep, int
 
   if (!ROLES || role >= 1) {
     const int q_lo = ROLES ? role - 1 : 0, q_hi = ROLES ? role : 2;
-    if (WITH_B) count_wait(E, SYNC_BDONE + 16 * q_lo, (uint32_t)E.nBq[q_lo]);  // this critic updated
     Held<T, 1> ch0;
     Held<T, 8> ch1;
     if (ROLES) {  // one critic per role: its layers 0 and 1 held under the input loads
-      held_issue<T, 1, WITH_B>(ch0, gw_fwd(E.net[NET_Q1 + q_lo].l[0]));
-      held_issue<T, 8, WITH_B>(ch1, gw_fwd(E.net[NET_Q1 + q_lo].l[1]));
+      held_issue<T, 1, false>(ch0, gw_fwd(E.net[NET_Q1 + q_lo].l[0]));
+      held_issue<T, 8, false>(ch1, gw_fwd(E.net[NET_Q1 + q_lo].l[1]));
     }
     STAMP(33);
     // ---- Q1, Q2 on (s, a~) with the updated critics (agent.py:244-248)
@@ -2527,7 +2088,7 @@ __device__ __forceinline__ void actor_body(const EngineDev* __restrict__ Ep, int
         Xb[r * ld + k] = k < O ? sB[r * O + k] : (k < O + A ? aB[r * A + (k - O)] : 0.f);
       }
       __syncthreads();
-      mlp_forward<T, R, WITH_B, ROLES>(q, Xb, Yb, ld, qi ? outP2 : outP1, qi ? out2 : out1, ldo,
+      mlp_forward<T, R, false, ROLES>(q, Xb, Yb, ld, qi ? outP2 : outP1, qi ? out2 : out1, ldo,
                                        qi ? E.o_P2 : E.o_P1, qi ? E.ldp2 : E.ldp1, lds, true, false, Bp, r0, nvalid, pf,
                                        ROLES ? gw_bwd(q.l[q.L - 1])
                                        : qi ? gw_bwd(E.net[NET_Q1].l[E.net[NET_Q1].L - 1]) : gw_fwd(E.net[NET_Q2].l[0]),
@@ -2570,10 +2131,10 @@ __device__ __forceinline__ void actor_body(const EngineDev* __restrict__ Ep, int
     // ---- d a~ through the critics: dX of layer 0, action columns
     for (int qi = q_lo; qi < q_hi; ++qi) {
       const AS_C NetDev& q = E.net[NET_Q1 + qi];
-      lf* G0 = mlp_backward<T, R, WITH_B>(q, qi ? g2B : g1B, ldo, Xb, Yb, ld, qi ? E.o_P2 : E.o_P1, qi ? E.ldp2 : E.ldp1,
+      lf* G0 = mlp_backward<T, R, false>(q, qi ? g2B : g1B, ldo, Xb, Yb, ld, qi ? E.o_P2 : E.o_P1, qi ? E.ldp2 : E.ldp1,
                                   lds, false, Bp, r0, nvalid, pf, gw_bwd(q.l[0]));
       lf* Gx = (G0 == Xb) ? Yb : Xb;
-      layer_bwd<T, R, WITH_B>(G0, ld, q.l[0], nullptr, 0, -1, Gx, ld, pf,
+      layer_bwd<T, R, false>(G0, ld, q.l[0], nullptr, 0, -1, Gx, ld, pf,
                       qi ? gw_bwd(pi.l[pi.L - 1]) : gw_bwd(E.net[NET_Q2].l[E.net[NET_Q2].L - 1]));
       __syncthreads();
       if (ROLES) {
@@ -2686,30 +2247,21 @@ __device__ __forceinline__ void phase_c_done(const AS_C EngineDev& E) {
     *GP(uint64_t, E.rng_step) += 1;
     sync[SYNC_EPOCH] += 1u;
     sync[SYNC_CDONE] = 0u;
-    sync[SYNC_DDONE] = 0u;
   }
 }
 
-// WITH_B (role split only): blocks [0, nB) first run this step's phase B (critic
-// tiles, Polyak) and count themselves done per critic; each critic role waits
-// for its critic's count before streaming its weights.
 // After the role blocks: E.stage ? nrt stager blocks (next step's batch).
-template <typename T, bool ROLES, bool WITH_B>
+template <typename T, bool ROLES>
 __global__ void __launch_bounds__(SAC_THREADS) sac_actor(const EngineDev* __restrict__ Ep, sac_replay rb) {
   PREFETCH_ARG(Ep);
   const AS_C EngineDev& E = *(const AS_C EngineDev*)Ep;
   extern __shared__ float lds_raw[];
-  const int bid = (int)blockIdx.x - (WITH_B ? E.nB : 0);
+  const int bid = (int)blockIdx.x;
   const int nrole = ROLES ? 3 * E.nrt : E.nrt * E.xs;
-  if (WITH_B && (int)blockIdx.x < E.nB) {
-    const AS_C TileDesc& td = *((const AS_C TileDesc*)E.tilesB + blockIdx.x);
-    dw_adam_tile_any<T, SAC_THREADS, true>(E, E.tilesB + blockIdx.x, true, (int)(*GPC(uint64_t, E.rng_step) & 1), 0,
-                                       (lf*)lds_raw);
-    count_done((uint32_t*)E.sync + SYNC_BDONE + 16 * (td.opt - 1));
-  } else if (bid >= nrole) {
+  if (bid >= nrole) {
     stage_next_batch(E, rb, bid - nrole, (lf*)lds_raw, *GPC(uint64_t, E.rng_step));
   } else {
-    actor_body<T, ROLES, WITH_B>(Ep, bid);
+    actor_body<T, ROLES>(Ep, bid);
   }
   phase_c_done(E);
   END_STAMP(61);
@@ -2724,19 +2276,19 @@ __global__ void __launch_bounds__(UT, UT == 512 ? 4 : 1) sac_critic_update(const
   const AS_C EngineDev& E = *(const AS_C EngineDev*)Ep;
   extern __shared__ float upd_lds[];
   // critic tiles: one X^T copy (xt_par = 0), so their operand loads need not wait for the step's parity
-  dw_adam_tile_any<T, UT, false, false, UT == 512 ? 2 : 4>(E, tiles + blockIdx.x, true,
+  dw_adam_tile_any<T, UT, UT == 512 ? 2 : 4>(E, tiles + blockIdx.x, true,
                                                           (int)(*GPC(uint64_t, E.rng_step) & 1), 0, (lf*)upd_lds);
   END_STAMP(62);  // standalone: the launch boundary publishes (no counter)
 }
 
-template <typename T, int UT = SAC_UPD_THREADS>
-__global__ void __launch_bounds__(UT, UT == 512 ? 4 : 1) sac_actor_update(const EngineDev* __restrict__ Ep,
-                                                                         const TileDesc* __restrict__ tiles, int ntiles) {
+template <typename T>
+__global__ void __launch_bounds__(SAC_UPD_THREADS) sac_actor_update(const EngineDev* __restrict__ Ep,
+                                                                   const TileDesc* __restrict__ tiles, int ntiles) {
   const AS_C EngineDev& E = *(const AS_C EngineDev*)Ep;
   const int par = (int)((*GPC(uint64_t, E.rng_step) - 1) & 1);  // phase C already advanced the step
   extern __shared__ float upd_lds[];
   if ((int)blockIdx.x < ntiles)
-    dw_adam_tile_any<T, UT, false, false, UT == 512 ? 2 : 4>(E, tiles + blockIdx.x, false, par, par, (lf*)upd_lds);
+    dw_adam_tile_any<T, SAC_UPD_THREADS>(E, tiles + blockIdx.x, false, par, par, (lf*)upd_lds);
   else
     alpha_and_losses(E, par, (lf*)upd_lds);
   END_STAMP(63);  // standalone: the launch boundary publishes (no counter)

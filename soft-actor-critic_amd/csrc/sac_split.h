@@ -283,17 +283,11 @@ __device__ __forceinline__ void gemm_ksplit(const lf* __restrict__ A, int lda, c
 }
 
 // ---------------------------------------------------------------------------- phase A
-// P (fused step, sac_persist.h): bidA and the step context come from the
-// fused launch, and everything the role hands to workgroups of the launch's
-// later phases is stored sc1 (their loads are sc1).  Phase A opens the launch,
-// so its inputs (the previous launch's weights, the batch staged for it) need
-// no wait, and its weight and bias loads stay plain (L2-cached): nothing in the
-// launch writes them before phase A's last reader has arrived.
-template <typename T, bool P = false, typename RoleWait = NoWait>
+template <typename T>
 __device__ __forceinline__ void target_critic_split_body(const EngineDev* __restrict__ Ep, const sac_replay& rb,
                                                          const int32_t* __restrict__ inj_idx_,
                                                          const float* __restrict__ inj_eps_, int bidA,
-                                                         const StepCtx& sc, const RoleWait& role_wait = RoleWait()) {
+                                                         const StepCtx& sc) {
   const AS_C EngineDev& E = *(const AS_C EngineDev*)Ep;
   extern __shared__ float lds_raw[];
   lf* lds = (lf*)lds_raw;
@@ -360,7 +354,7 @@ __device__ __forceinline__ void target_critic_split_body(const EngineDev* __rest
 #ifndef SAC_ADAM_LAST
 #define SAC_ADAM_LAST 1
 #endif
-  const bool adam_blk = !P && (SAC_ADAM_LAST ? (role == 5 && rbi == E.nrt - 1 && h == 1) : (role == 0 && rbi == 0 && h == 0));
+  const bool adam_blk = (SAC_ADAM_LAST ? (role == 5 && rbi == E.nrt - 1 && h == 1) : (role == 0 && rbi == 0 && h == 0));
   if (adam_blk && tid < 4 && (tid < 3 || (E.auto_entropy && E.alpha_update))) {
     // optimizer step counters and this step's Adam bias corrections (torch adam.py), read
     // by phases B and D only: done by the last pi(s) workgroup, off the y chain (a load
@@ -463,7 +457,6 @@ __device__ __forceinline__ void target_critic_split_body(const EngineDev* __rest
     }
   }
   __syncthreads();
-  if constexpr (P) role_wait(role);  // the fused step's hook (phase A waits for nothing: it opens the launch)
   STAMP(1);
 
   // pi's squashed-Gaussian head (models.py:79-87) from two layer-2 partials:
@@ -525,11 +518,11 @@ __device__ __forceinline__ void target_critic_split_body(const EngineDev* __rest
         if (stash) {
           const int b = r0 + r;
           float* hs = E.head_st + (size_t)b * 4 * A;
-          st_f<P>(hs + j, mu);
-          st_f<P>(hs + A + j, lsr);
-          st_f<P>(hs + 2 * A + j, z);
-          st_f<P>(hs + 3 * A + j, e);
-          st_f<P>(E.a_st + (size_t)b * A + j, act_v);
+          st_f<false>(hs + j, mu);
+          st_f<false>(hs + A + j, lsr);
+          st_f<false>(hs + 2 * A + j, z);
+          st_f<false>(hs + 3 * A + j, e);
+          st_f<false>(E.a_st + (size_t)b * A + j, act_v);
         }
       }
       for (int o = 1; o < AP; o <<= 1) {
@@ -561,10 +554,10 @@ __device__ __forceinline__ void target_critic_split_body(const EngineDev* __rest
     __syncthreads();
     if (pi_actor && h == 0) {  // pi's layer-0 pre-activations for phase C's relu masks
       float* ps = L0.pstash + (size_t)r0 * L0.Np;
-      for (int i = tid; i < R * L0.Np; i += SAC_THREADS) st_f<P>(ps + i, P0[(i / L0.Np) * ldp0 + i % L0.Np]);
+      for (int i = tid; i < R * L0.Np; i += SAC_THREADS) st_f<false>(ps + i, P0[(i / L0.Np) * ldp0 + i % L0.Np]);
     }
     if (stXT && h == 0)
-      store_T<T, R, P>(H0, ld, L1.Kp, L1.K, (T*)L1.XT + (pi_actor ? par * L1.xt_par : 0), Bp, r0, nvalid, nullptr);
+      store_T<T, R>(H0, ld, L1.Kp, L1.K, (T*)L1.XT + (pi_actor ? par * L1.xt_par : 0), Bp, r0, nvalid, nullptr);
     STAMP(2);
     if (sizeof(T) == 4 && !kh2.ok) ks_issue<T, KsHeld<T>::MAXC, false>(kh2, w2n);  // fp32: under layer 1 (target critics: before the poll)
     // layer 1, this half: H0 -> P1 / H1 [R][HH]
@@ -583,10 +576,10 @@ __device__ __forceinline__ void target_critic_split_body(const EngineDev* __rest
     __syncthreads();
     if (pi_actor) {  // this half's layer-1 pre-activations
       float* ps = L1.pstash + (size_t)r0 * L1.Np + h * HH;
-      for (int i = tid; i < R * HH; i += SAC_THREADS) st_f<P>(ps + (i / HH) * L1.Np + i % HH, P1[(i / HH) * ldp1 + i % HH]);
+      for (int i = tid; i < R * HH; i += SAC_THREADS) st_f<false>(ps + (i / HH) * L1.Np + i % HH, P1[(i / HH) * ldp1 + i % HH]);
     }
     if (stXT)  // layer 2's input, this half's rows of X^T
-      store_T<T, R, P>(H1, ldh1, HH, HH, (T*)L2.XT + (pi_actor ? par * L2.xt_par : 0) + (size_t)h * HH * Bp, Bp, r0,
+      store_T<T, R>(H1, ldh1, HH, HH, (T*)L2.XT + (pi_actor ? par * L2.xt_par : 0) + (size_t)h * HH * Bp, Bp, r0,
                        nvalid, nullptr);
     STAMP(3);
     // layer 2, this half's partial sum: outB [R][Np2]
@@ -604,8 +597,7 @@ __device__ __forceinline__ void target_critic_split_body(const EngineDev* __rest
     __syncthreads();
   };
 
-  // alpha (agent.py:203): the previous step's phase D wrote it (the previous
-  // launch, also in the fused step)
+  // alpha (agent.py:203): the previous step's phase D wrote it (the previous launch)
   const float alpha32 = (float)*GPC(double, E.alpha_state + 1);
   if (role == 0) {
     // ---- pi(s'): the critical path's head
@@ -617,17 +609,17 @@ __device__ __forceinline__ void target_critic_split_body(const EngineDev* __rest
   } else if (role == 5) {
     // ---- pi(s): the actor sample for phase C (stashes), X^T of pi's layers
     if (h == 0)
-      for (int i = tid; i < R * O; i += SAC_THREADS) st_f<P>(E.s_st + (size_t)r0 * O + i, sB[i]);
+      for (int i = tid; i < R * O; i += SAC_THREADS) st_f<false>(E.s_st + (size_t)r0 * O + i, sB[i]);
     build_x(sB, aB, 0);
     // layer-0 input X^T: both halves store it (columns h Bp + r0: the partial dW layout)
-    store_T<T, R, P>(Xb, ld, L0.Kp, L0.K, (T*)L0.XT + par * L0.xt_par, 2 * Bp, h * Bp + r0, nvalid, nullptr);
+    store_T<T, R>(Xb, ld, L0.Kp, L0.K, (T*)L0.XT + par * L0.xt_par, 2 * Bp, h * Bp + r0, nvalid, nullptr);
     forward01(true, true, true, no_hook);
     AS_G uint64_t* g = gs_at(E, GS_PS, rbi, h);
     for (int i = tid; i < R * 2 * A; i += SAC_THREADS) gran_put(g + i, outB[(i / (2 * A)) * ldo + i % (2 * A)], ep);
     head(nullptr, gs_at(E, GS_PS, rbi, 1 - h), false, a2B, lpB, h == 0);
     if (h == 0 && tid < nvalid) {
       const int b = r0 + tid;
-      st_f<P>(E.lp_st + par * E.Br + b, lpB[tid]);
+      st_f<false>(E.lp_st + par * E.Br + b, lpB[tid]);
       stats[4 + B + b] = lpB[tid];
     }
     STAMP(6);
@@ -676,13 +668,13 @@ __device__ __forceinline__ void target_critic_split_body(const EngineDev* __rest
           sq[qi] = v ? d * d : 0.f;
           float seed = v ? (2.0f / (float)B) * d : 0.f;
           if (qn.out_act != ACT_ID) seed = act_bwd(qn.out_act, qpre, seed);
-          st_f<P>(E.seedq + qi * Bp + b, seed);
+          st_f<false>(E.seedq + qi * Bp + b, seed);
         }
       }
 #pragma unroll
       for (int qi = 0; qi < 2; ++qi) {
         const float s2 = wave_sum(sq[qi]);
-        if (tid == 0) st_f<P>(E.lossp + (par * E.nrt + rbi) * 4 + qi, s2);
+        if (tid == 0) st_f<false>(E.lossp + (par * E.nrt + rbi) * 4 + qi, s2);
       }
     }
   } else {
@@ -699,7 +691,7 @@ __device__ __forceinline__ void target_critic_split_body(const EngineDev* __rest
     const float w2n = ldf<false>(net.P + L2.w_off + h * HH + tid % HH);  // W2 [1][H] fp32 master
     build_x(sB, aB, A);
     // layer-0 input X^T is shared by Q1 and Q2: Q1's halves store it (columns h Bp + r0)
-    if (qi == 0) store_T<T, R, P>(Xb, ld, L0.Kp, L0.K, L0.XT, 2 * Bp, h * Bp + r0, nvalid, nullptr);
+    if (qi == 0) store_T<T, R>(Xb, ld, L0.Kp, L0.K, L0.XT, 2 * Bp, h * Bp + r0, nvalid, nullptr);
     forward01(true, true, false, [&] {
       if constexpr (sizeof(T) == 4) ht_issue<T, 2, NCH_HH, false>(ht1, wt1);
     });
@@ -732,18 +724,16 @@ __device__ __forceinline__ void target_critic_split_body(const EngineDev* __rest
       // dY^T (layer 2's: the indicator row); phase B scales each batch column
       // by the seed the first target-critic half computed (E.seedq) and sums
       // the bias gradients from the scaled rows.
-      store_T<T, R, P>(U1, ldu1, HH, HH, (T*)L1.GT + (size_t)h * HH * Bp, Bp, r0, nvalid, nullptr);
-      store_T<T, R, P>(Xb, ld, L0.Np, L0.N, L0.GT, 2 * Bp, h * Bp + r0, nvalid, nullptr);
+      store_T<T, R>(U1, ldu1, HH, HH, (T*)L1.GT + (size_t)h * HH * Bp, Bp, r0, nvalid, nullptr);
+      store_T<T, R>(Xb, ld, L0.Np, L0.N, L0.GT, 2 * Bp, h * Bp + r0, nvalid, nullptr);
       if (h == 0) {
         lf* g2 = outB;  // this half's q partial went out as a granule above
         for (int i = tid; i < R * 32; i += SAC_THREADS) g2[(i / 32) * ldo + i % 32] = (i % 32) == 0 ? 1.f : 0.f;
         __syncthreads();
-        store_T<T, R, P>(g2, ldo, L2.Np, L2.N, L2.GT, Bp, r0, nvalid, nullptr);
+        store_T<T, R>(g2, ldo, L2.Np, L2.N, L2.GT, Bp, r0, nvalid, nullptr);
       }
-      if constexpr (P) role_wait(-1);
       STAMP(15);
     } else {
-      if constexpr (P) role_wait(-1);
       if (tid < 64) {  // wave 0: q, y, loss partial, seed dL/dq = 2(q - y)/B  (mse_loss backward)
         float sq = 0.f;
         if (tid < R) {
@@ -779,7 +769,7 @@ __device__ __forceinline__ void target_critic_split_body(const EngineDev* __rest
           qtB[tid] = seed;
         }
         sq = wave_sum(sq);
-        if (tid == 0 && h == 0) st_f<P>(E.lossp + (par * E.nrt + rbi) * 4 + qi, sq);
+        if (tid == 0 && h == 0) st_f<false>(E.lossp + (par * E.nrt + rbi) * 4 + qi, sq);
       }
       __syncthreads();
       STAMP(15);
@@ -788,10 +778,10 @@ __device__ __forceinline__ void target_critic_split_body(const EngineDev* __rest
         lf* g2 = outB;
         for (int i = tid; i < R * 32; i += SAC_THREADS) g2[(i / 32) * ldo + i % 32] = (i % 32) == 0 ? 1.f : 0.f;
         __syncthreads();
-        store_T<T, R, P>(g2, ldo, L2.Np, L2.N, L2.GT, Bp, r0, nvalid, L2.dbp, qtB);
+        store_T<T, R>(g2, ldo, L2.Np, L2.N, L2.GT, Bp, r0, nvalid, L2.dbp, qtB);
       }
-      store_T<T, R, P>(U1, ldu1, HH, HH, (T*)L1.GT + (size_t)h * HH * Bp, Bp, r0, nvalid, L1.dbp ? L1.dbp + h * HH : nullptr, qtB, L1.N);
-      store_T<T, R, P>(Xb, ld, L0.Np, L0.N, L0.GT, 2 * Bp, h * Bp + r0, nvalid, L0.dbp, qtB);
+      store_T<T, R>(U1, ldu1, HH, HH, (T*)L1.GT + (size_t)h * HH * Bp, Bp, r0, nvalid, L1.dbp ? L1.dbp + h * HH : nullptr, qtB, L1.N);
+      store_T<T, R>(Xb, ld, L0.Np, L0.N, L0.GT, 2 * Bp, h * Bp + r0, nvalid, L0.dbp, qtB);
     }
     STAMP(11 + 2 * qi);
   }
@@ -828,15 +818,9 @@ __global__ void __launch_bounds__(SAC_THREADS) sac_target_critic_split(const Eng
 }
 
 // ---------------------------------------------------------------------------- phase C
-// pi's weights are read with plain loads in either mode (the previous launch's
-// phase D wrote them; this launch's D waits for every pi role).
-// P (persistent step): wait(0) = pi(s) of this step done (the stashes), wait(1 +
-// qi) = critic qi updated by this step's phase B, wait(3) = both critics
-// updated; every load of data written earlier in the launch is sc1, and what
-// phase D reads is stored sc1.
-template <typename T, bool P = false, typename CWait = NoWait>
-__device__ __forceinline__ void actor_split_body(const EngineDev* __restrict__ Ep, int bid, const StepCtx& sc,
-                                                 const CWait& wait = CWait()) {
+// pi's weights are read with plain loads (the previous launch's phase D wrote them).
+template <typename T>
+__device__ __forceinline__ void actor_split_body(const EngineDev* __restrict__ Ep, int bid, const StepCtx& sc) {
   const AS_C EngineDev& E = *(const AS_C EngineDev*)Ep;
   extern __shared__ float lds_raw[];
   lf* lds = (lf*)lds_raw;
@@ -891,11 +875,9 @@ __device__ __forceinline__ void actor_split_body(const EngineDev* __restrict__ E
     // would otherwise sit between the forward pass and the backward GEMM)
     const GemmW wt1 = gw_sub<T>(L1.WTc, L1.Np, 0, L1.Kp, h * HH, HH, nullptr, 0);
     HTiles<T, 2, NCH_HH> ht1;
-    if constexpr (!P) {
-      ht_issue<T, 2, HC0>(h0, w0);
-      ht_issue<T, 1, NCH_H>(h1, w1);
-      ht_issue<T, 2, NCH_HH>(ht1, wt1);
-    }
+    ht_issue<T, 2, HC0>(h0, w0);
+    ht_issue<T, 1, NCH_H>(h1, w1);
+    ht_issue<T, 2, NCH_HH>(ht1, wt1);
     // the two k-split steps of the critic's chain (layer 2's partial q, then
     // layer 0's dX for the action columns) read weights phase B has just
     // written: held (issued behind the inputs), not a cold round trip each
@@ -909,24 +891,12 @@ __device__ __forceinline__ void actor_split_body(const EngineDev* __restrict__ E
     kc2.ok = kc0.ok = false;
     // the W2 (fp32 master) element of this thread's column n = tid % HH of the unit-seed backward
     static_assert(SAC_THREADS % HH == 0, "one W2 column per thread in the unit-seed loop");
-    float w2n = 0.f;
-    if constexpr (P) {  // the stashes of pi(s), then (once phase B has updated this critic) its weights
-      wait(0);
-      for (int i = tid; i < R * O; i += SAC_THREADS) sB[i] = ldf<true>(E.s_st + (size_t)r0 * O + i);
-      for (int i = tid; i < R * A; i += SAC_THREADS) aB[i] = ldf<true>(E.a_st + (size_t)r0 * A + i);
-      wait(1 + qi);
-      ht_issue<T, 2, HC0, true>(h0, w0);
-      ht_issue<T, 1, NCH_H, true>(h1, w1);
-      ht_issue<T, 2, NCH_HH, true>(ht1, wt1);
-      w2n = ldf<true>(net.P + L2.w_off + h * HH + tid % HH);
-    } else {
-      w2n = GPC(float, net.P + L2.w_off)[h * HH + tid % HH];
-      for (int i = tid; i < R * O; i += SAC_THREADS) sB[i] = GPC(float, E.s_st)[(size_t)r0 * O + i];
-      for (int i = tid; i < R * A; i += SAC_THREADS) aB[i] = GPC(float, E.a_st)[(size_t)r0 * A + i];
-    }
+    const float w2n = GPC(float, net.P + L2.w_off)[h * HH + tid % HH];
+    for (int i = tid; i < R * O; i += SAC_THREADS) sB[i] = GPC(float, E.s_st)[(size_t)r0 * O + i];
+    for (int i = tid; i < R * A; i += SAC_THREADS) aB[i] = GPC(float, E.a_st)[(size_t)r0 * A + i];
     if (SAC_KS_C) {  // behind the inputs: waiting for s / a~ must not wait for these (loads retire in order)
-      ks_issue<T, decltype(kc2)::MAXC, P>(kc2, w2);
-      if (sizeof(T) == 2) ks_issue<T, decltype(kc0)::MAXC, P>(kc0, wt0);  // fp32: after layer 1 (its held W1 part is dead then; from here it spilled)
+      ks_issue<T, decltype(kc2)::MAXC>(kc2, w2);
+      if (sizeof(T) == 2) ks_issue<T, decltype(kc0)::MAXC>(kc0, wt0);  // fp32: after layer 1 (its held W1 part is dead then; from here it spilled)
     }
     __syncthreads();
     const int Kp0 = L0.Kp;
@@ -937,7 +907,7 @@ __device__ __forceinline__ void actor_split_body(const EngineDev* __restrict__ E
     __syncthreads();
     STAMP(33);
     const int act = net.hid_act;
-    gemm_hs<T, 2, HC0, P>(Xb, ld, w0, &h0, [&](int j, int col, const f32x4& acc) {
+    gemm_hs<T, 2, HC0, false>(Xb, ld, w0, &h0, [&](int j, int col, const f32x4& acc) {
       const bool nv = col < L0.N;
       const float bn = h0.b[j];
 #pragma unroll
@@ -950,7 +920,7 @@ __device__ __forceinline__ void actor_split_body(const EngineDev* __restrict__ E
     });
     if (act != ACT_RELU && act != ACT_ID) act_pass_fwd<R>(H0, ld, L0.Np >> 4, act);
     __syncthreads();
-    gemm_hs<T, 1, NCH_H, P>(H0, ld, w1, &h1, [&](int j, int col, const f32x4& acc) {
+    gemm_hs<T, 1, NCH_H, false>(H0, ld, w1, &h1, [&](int j, int col, const f32x4& acc) {
       const float bn = h1.b[j];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
@@ -960,10 +930,10 @@ __device__ __forceinline__ void actor_split_body(const EngineDev* __restrict__ E
         H1[r * ldh1 + col] = act == ACT_RELU ? (p > 0.f ? p : 0.f) : p;
       }
     });
-    if (SAC_KS_C && sizeof(T) == 4) ks_issue<T, decltype(kc0)::MAXC, P>(kc0, wt0);
+    if (SAC_KS_C && sizeof(T) == 4) ks_issue<T, decltype(kc0)::MAXC>(kc0, wt0);
     if (act != ACT_RELU && act != ACT_ID) act_pass_fwd<R>(H1, ldh1, HH >> 4, act);
     __syncthreads();
-    gemm_ksplit<T, P, decltype(kc2)::MAXC>(H1, ldh1, w2, red, outB, ldo, &kc2);  // partial q
+    gemm_ksplit<T, false, decltype(kc2)::MAXC>(H1, ldh1, w2, red, outB, ldo, &kc2);  // partial q
     STAMP(36 + qi);
     // unit-seed backward down to a~ (the pi role applies the min-Q weights and act'(q))
     {
@@ -972,7 +942,7 @@ __device__ __forceinline__ void actor_split_body(const EngineDev* __restrict__ E
         U1[r * ldu1 + n] = act_bwd(act, P1[r * ldp1 + n], w2n);
       }
       __syncthreads();
-      gemm_hs<T, 2, NCH_HH, P>(U1, ldu1, wt1, &ht1, [&](int j, int col, const f32x4& acc) {
+      gemm_hs<T, 2, NCH_HH, false>(U1, ldu1, wt1, &ht1, [&](int j, int col, const f32x4& acc) {
         const bool kv = col < L1.K;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
@@ -985,7 +955,7 @@ __device__ __forceinline__ void actor_split_body(const EngineDev* __restrict__ E
       if (act != ACT_RELU && act != ACT_ID) act_pass_bwd<R>(Xb, ld, P0, ldp0, L1.Kp >> 4, L1.K, act);
       __syncthreads();
       // dX of layer 0 for the action columns: the 16-row tiles of W0^T holding [O, O + A)
-      gemm_ksplit<T, P, decltype(kc0)::MAXC>(Xb, ld, wt0, red, H0, ld, &kc0);  // H0 [R][k1 - k0]: partial dX0
+      gemm_ksplit<T, false, decltype(kc0)::MAXC>(Xb, ld, wt0, red, H0, ld, &kc0);  // H0 [R][k1 - k0]: partial dX0
       AS_G uint64_t* g = gs_at(E, GS_C1 + qi, rbi, h);
       for (int i = tid; i < R * A; i += SAC_THREADS) gran_put(g + i, H0[(i / A) * ld + (O - k0) + i % A], ep);
       if (tid < R) gran_put(g + R * A + tid, outB[tid * ldo], ep);
@@ -1005,16 +975,15 @@ __device__ __forceinline__ void actor_split_body(const EngineDev* __restrict__ E
   const GemmW wt1 = gw_sub<T>(L1.WTc, L1.Np, 0, L1.Kp, h * HH, HH, nullptr, 0);
   HTiles<T, 1, NCH_32> ht2;
   HTiles<T, 2, NCH_HH> ht1;
-  if (P) wait(0);  // pi(s) of this step: its stashes (and, before it, the phase D that wrote pi's weights)
   ht_issue<T, 1, NCH_32, false>(ht2, wt2);
   ht_issue<T, 2, NCH_HH, false>(ht1, wt1);
   {  // relu masks: pi's pre-activations stashed by phase A's pi(s) role
     const float* p0 = L0.pstash + (size_t)r0 * L0.Np;
-    for (int i = tid; i < R * L0.Np; i += SAC_THREADS) P0[(i / L0.Np) * ldp0 + i % L0.Np] = ldf<P>(p0 + i);
+    for (int i = tid; i < R * L0.Np; i += SAC_THREADS) P0[(i / L0.Np) * ldp0 + i % L0.Np] = ldf<false>(p0 + i);
     const float* p1 = L1.pstash + (size_t)r0 * L1.Np + h * HH;
     for (int i = tid; i < R * HH; i += SAC_THREADS)
-      P1[(i / HH) * ldp1 + i % HH] = ldf<P>(p1 + (i / HH) * L1.Np + i % HH);
-    if (tid < R) lpB[tid] = ldf<P>(E.lp_st + par * E.Br + r0 + tid);
+      P1[(i / HH) * ldp1 + i % HH] = ldf<false>(p1 + (i / HH) * L1.Np + i % HH);
+    if (tid < R) lpB[tid] = ldf<false>(E.lp_st + par * E.Br + r0 + tid);
   }
   // the head stash of this thread's (row, dim) and the critics' output biases,
   // loaded now: after the critics' hand-off they would be one more round trip
@@ -1022,11 +991,9 @@ __device__ __forceinline__ void actor_split_body(const EngineDev* __restrict__ E
   if (tid < R * A && r0 + tid / A < E.Br) {
     const float* hs = E.head_st + (size_t)(r0 + tid / A) * 4 * A;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) hsv[q] = ldf<P>(hs + q * A + tid % A);
+    for (int q = 0; q < 4; ++q) hsv[q] = ldf<false>(hs + q * A + tid % A);
   }
-  // fused step: the critics' output biases once this step's phase B has written them
-  if (P) wait(3);
-  const float bq1 = ldf<P>(E.net[NET_Q1].l[2].bias), bq2 = ldf<P>(E.net[NET_Q2].l[2].bias);
+  const float bq1 = ldf<false>(E.net[NET_Q1].l[2].bias), bq2 = ldf<false>(E.net[NET_Q2].l[2].bias);
   __syncthreads();
   STAMP(34);
   // combine the critics' unit-seed partials with the min-Q weights (L_pi = mean(alpha logpi - min Q))
@@ -1081,7 +1048,7 @@ __device__ __forceinline__ void actor_split_body(const EngineDev* __restrict__ E
         if (q2n.out_act != ACT_ID) w2 = act_bwd(q2n.out_act, q2p, w2);
       }
       term = wave_sum(term);
-      if (tid == 0 && h == 0) st_f<P>(E.lossp + (par * E.nrt + rbi) * 4 + 2, term);
+      if (tid == 0 && h == 0) st_f<false>(E.lossp + (par * E.nrt + rbi) * 4 + 2, term);
       const float w1r = __shfl(w1, r, 64), w2r = __shfl(w2, r, 64);
       if (live) {
         float da1 = gv[0], da2 = gv[W];
@@ -1130,7 +1097,7 @@ __device__ __forceinline__ void actor_split_body(const EngineDev* __restrict__ E
       g2B[tid] = w2;
     }
     term = wave_sum(term);
-    if (tid == 0 && h == 0) st_f<P>(E.lossp + (par * E.nrt + rbi) * 4 + 2, term);
+    if (tid == 0 && h == 0) st_f<false>(E.lossp + (par * E.nrt + rbi) * 4 + 2, term);
   }
   __syncthreads();
   for (int i = tid; i < R * A; i += SAC_THREADS) {
@@ -1189,7 +1156,7 @@ __device__ __forceinline__ void actor_split_body(const EngineDev* __restrict__ E
   }
   __syncthreads();
   // layer 2 dY^T (= dOut) + bias partials: half 0
-  if (h == 0) store_T<T, R, P>(goutB, ldo, L2.Np, L2.N, L2.GT, Bp, r0, nvalid, L2.dbp);
+  if (h == 0) store_T<T, R>(goutB, ldo, L2.Np, L2.N, L2.GT, Bp, r0, nvalid, L2.dbp);
   // dY1 (this half) = act'(P1) * (dOut W2[:, half])
   const int act = pi.hid_act;
   gemm_hs<T, 1, NCH_32, false>(goutB, ldo, wt2, &ht2, [&](int j, int col, const f32x4& acc) {
@@ -1203,7 +1170,7 @@ __device__ __forceinline__ void actor_split_body(const EngineDev* __restrict__ E
   });
   if (act != ACT_RELU && act != ACT_ID) act_pass_bwd<R>(U1, ldu1, P1, ldp1, HH >> 4, HH, act);
   __syncthreads();
-  store_T<T, R, P>(U1, ldu1, HH, HH, (T*)L1.GT + (size_t)h * HH * Bp, Bp, r0, nvalid, L1.dbp ? L1.dbp + h * HH : nullptr, nullptr, L1.N);
+  store_T<T, R>(U1, ldu1, HH, HH, (T*)L1.GT + (size_t)h * HH * Bp, Bp, r0, nvalid, L1.dbp ? L1.dbp + h * HH : nullptr, nullptr, L1.N);
   // dY0 partial = act'(P0) * (dY1 W1[half])
   gemm_hs<T, 2, NCH_HH, false>(U1, ldu1, wt1, &ht1, [&](int j, int col, const f32x4& acc) {
     const bool kv = col < L1.K;
@@ -1217,7 +1184,7 @@ __device__ __forceinline__ void actor_split_body(const EngineDev* __restrict__ E
   });
   if (act != ACT_RELU && act != ACT_ID) act_pass_bwd<R>(Xb, ld, P0, ldp0, L1.Kp >> 4, L1.K, act);
   __syncthreads();
-  store_T<T, R, P>(Xb, ld, L0.Np, L0.N, L0.GT, W * Bp, h * Bp + r0, nvalid, L0.dbp);
+  store_T<T, R>(Xb, ld, L0.Np, L0.N, L0.GT, W * Bp, h * Bp + r0, nvalid, L0.dbp);
   STAMP(35);
 }
 

@@ -41,7 +41,7 @@
 #define WJMAX 16
 #define WWS 1088   // floats of the epilogue weight slices (OUTP: Nout x 64; DA: A x 64)
 
-enum WAMode { WA_PLAIN = 0, WA_ACT = 1, WA_OUTBWD = 2, WA_HEAD = 3, WA_GATHER = 4 };  // 3, 4: flow items
+enum WAMode { WA_PLAIN = 0, WA_ACT = 1, WA_OUTBWD = 2 };
 enum WEMode { WE_FWD = 0, WE_BWD = 1 };
 enum WRowPro { WR_NONE = 0, WR_YSEED = 1, WR_MINQ = 2, WR_PIHEAD = 3 };
 
@@ -74,7 +74,6 @@ struct WideDev {
   float* dbppi_out;
   int stamp_stage;  // stamps builds: the stage index that writes stamps (SAC_WIDE_STAMP_STAGE)
   const uint64_t* rng_step;  // = EngineDev::rng_step (read through the prefetched WideDev lines)
-  uint32_t* cnt;             // flow kernel: per (job, row block) completion counters
 };
 
 // One GEMM of a stage: output tiles (row block rb, column block cb), items
@@ -124,10 +123,6 @@ struct WJob {
   int adbp_ld;
   int p_row0;  // forward: P is stored for rows >= p_row0 only
   int nbuf;    // K-block buffers in LDS (2..4): nbuf - 1 blocks in flight ahead of the MFMAs
-  // flow kernel: this job's counters (one per row block) and the jobs of the
-  // launch whose items of the same row block (rb mod their nrb) it reads
-  int cnt_off, ndep;
-  int dep_job[4], dep_need[4];
 };
 
 static_assert(sizeof(WJob) <= 448, "extend wide_prefetch");
@@ -173,36 +168,17 @@ __device__ __forceinline__ void st4(void* base, size_t off, const f32x4& v) {
   }
 }
 
-// Data handed between workgroups of one flow launch (FL) is stored write-through
-// (sc1: a plain store would sit dirty in the producer XCD's L2) and read with
-// plain (L2-cached) loads: every line of it is first read in the launch after
-// its producer's counter says it is in memory, and the kernel-start acquire
-// invalidated what the reader's L2 held from earlier launches -- so the column
-// blocks of a row block re-read their A operand from their XCD's L2.
-// SAC_FLOW_SC1_LOADS builds read it with sc1 loads instead (A/B).
-#ifndef SAC_FLOW_SC1_LOADS
-#define SAC_FLOW_SC1_LOADS 0
-#endif
-template <bool FL>
-__device__ __forceinline__ float ldh(const float* p) { return ldf<FL && SAC_FLOW_SC1_LOADS>(p); }
-template <bool FL>
-__device__ __forceinline__ void sth(float* p, float v) { st_f<FL>(p, v); }
-template <bool FL>
-__device__ __forceinline__ void st16h(float* base, size_t off, f32x4 v) {
-  if constexpr (FL) coh_store16<true>(base, (uint32_t)(off * 4), __builtin_bit_cast(u32x4, v));
-  else *(AS_G f32x4*)(GP(float, base) + off) = v;
-}
-template <bool FL>
-__device__ __forceinline__ f32x4 ld16h(const float* base, size_t off) {
-  if constexpr (FL && SAC_FLOW_SC1_LOADS)
-    return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(coh_rsrc(base, 0xFFFFFFF0u), (int)(off * 4), 0, 16));
-  else return *(const AS_G f32x4*)(GPC(float, base) + off);
-}
+// plain loads / stores of the buffers the stages hand to each other (every
+// hand-off crosses a launch boundary)
+__device__ __forceinline__ float ldh(const float* p) { return *GPC(float, p); }
+__device__ __forceinline__ void sth(float* p, float v) { *GP(float, p) = v; }
+__device__ __forceinline__ void st16h(float* base, size_t off, f32x4 v) { *(AS_G f32x4*)(GP(float, base) + off) = v; }
+__device__ __forceinline__ f32x4 ld16h(const float* base, size_t off) { return *(const AS_G f32x4*)(GPC(float, base) + off); }
 
 // ---------------------------------------------------------------------------- row prologues
 // D[r][0..J) of the item's rows into Dl (LDS), plus the side outputs of the
 // output layer (cb == 0 items only: losses, y, the output layer's dY^T / bias).
-template <typename T, bool FL>
+template <typename T>
 __device__ __forceinline__ void wide_rowpro(const AS_C EngineDev& E, const AS_C WideDev& W, const AS_C WJob& jb,
                                             int row0, int cb, int par, lf* Dl) {
   const int tid = threadIdx.x, B = W.B, A = W.A;
@@ -224,9 +200,9 @@ __device__ __forceinline__ void wide_rowpro(const AS_C EngineDev& E, const AS_C 
 #pragma unroll
           for (int u = 0; u < 4; ++u) {
             const int c = c0 + u < W.ncb_q ? c0 + u : W.ncb_q - 1;
-            x1[u] = ldh<FL>(W.OUTPqt[0] + c * W.cbs_q + lr);
-            x2[u] = ldh<FL>(W.OUTPqt[1] + c * W.cbs_q + lr);
-            xq[u] = ldh<FL>(W.OUTPq[qi] + c * W.cbs_q + lr);
+            x1[u] = ldh(W.OUTPqt[0] + c * W.cbs_q + lr);
+            x2[u] = ldh(W.OUTPqt[1] + c * W.cbs_q + lr);
+            xq[u] = ldh(W.OUTPq[qi] + c * W.cbs_q + lr);
           }
 #pragma unroll
           for (int u = 0; u < 4; ++u)
@@ -239,7 +215,7 @@ __device__ __forceinline__ void wide_rowpro(const AS_C EngineDev& E, const AS_C 
         const float t1 = act_fwd(qt1.out_act, a1 + GPC(float, qt1.l[qt1.L - 1].bias)[0]);
         const float t2 = act_fwd(qt2.out_act, a2 + GPC(float, qt2.l[qt2.L - 1].bias)[0]);
         const float qp = aq + GPC(float, q.l[q.L - 1].bias)[0];
-        y = ldh<FL>(W.R + lr) + (E.gamma * (1.f - ldh<FL>(W.Dn + lr))) * (fmin_nan(t1, t2) - alpha32 * ldh<FL>(W.LP2 + lr));
+        y = ldh(W.R + lr) + (E.gamma * (1.f - ldh(W.Dn + lr))) * (fmin_nan(t1, t2) - alpha32 * ldh(W.LP2 + lr));
         const float d = act_fwd(q.out_act, qp) - y;
         sq = d * d;
         seed = (2.0f / (float)B) * d;
@@ -260,7 +236,7 @@ __device__ __forceinline__ void wide_rowpro(const AS_C EngineDev& E, const AS_C 
         }
         const int rt = lr >> 4;
         if ((tid & 15) == 0 && rt < W.nrt) {
-          GP(float, W.dbpq_out[qi])[rt] = s;
+          if (W.dbpq_out[qi]) GP(float, W.dbpq_out[qi])[rt] = s;
           GP(float, E.lossp)[(par * E.nrt + rt) * 4 + qi] = sq;
         }
       }
@@ -279,8 +255,8 @@ __device__ __forceinline__ void wide_rowpro(const AS_C EngineDev& E, const AS_C 
 #pragma unroll
           for (int u = 0; u < 4; ++u) {
             const int c = c0 + u < W.ncb_q ? c0 + u : W.ncb_q - 1;
-            x1[u] = ldh<FL>(W.OUTPc[0] + c * W.cbs_q + lr);
-            x2[u] = ldh<FL>(W.OUTPc[1] + c * W.cbs_q + lr);
+            x1[u] = ldh(W.OUTPc[0] + c * W.cbs_q + lr);
+            x2[u] = ldh(W.OUTPc[1] + c * W.cbs_q + lr);
           }
 #pragma unroll
           for (int u = 0; u < 4; ++u)
@@ -321,8 +297,8 @@ __device__ __forceinline__ void wide_rowpro(const AS_C EngineDev& E, const AS_C 
 #pragma unroll
           for (int u = 0; u < 4; ++u) {
             const int c = c0 + u < W.ncb_da ? c0 + u : W.ncb_da - 1;
-            x1[u] = ldh<FL>(W.DA[0] + c * W.cbs_da + (size_t)lr * A + j);
-            x2[u] = ldh<FL>(W.DA[1] + c * W.cbs_da + (size_t)lr * A + j);
+            x1[u] = ldh(W.DA[0] + c * W.cbs_da + (size_t)lr * A + j);
+            x2[u] = ldh(W.DA[1] + c * W.cbs_da + (size_t)lr * A + j);
           }
 #pragma unroll
           for (int u = 0; u < 4; ++u)
@@ -372,7 +348,7 @@ __device__ __forceinline__ void wide_rowpro(const AS_C EngineDev& E, const AS_C 
         }
       }
     }
-    if (cb == 0) {  // bias partials of the output layer: per 16-row tile, column j < 2A
+    if (cb == 0 && W.dbppi_out) {  // bias partials of the output layer: per 16-row tile, column j < 2A
       __syncthreads();
       for (int i = tid; i < 4 * 2 * A; i += WG_T) {
         const int rt = i / (2 * A), j = i % (2 * A);
@@ -443,7 +419,7 @@ __device__ __forceinline__ float hactb(int a, float p, float g) {
 // 64 rows x 64 columns of Et dotted with No weight rows Ws[j][0..64): four
 // threads per row, 16 columns each, reduced by two shuffles; act: apply the
 // hidden activation to Et first (output-layer partials of a forward stage)
-template <bool HR, bool ACTX, bool FL>
+template <bool HR, bool ACTX>
 __device__ __forceinline__ void wide_rowdot(const lf* Et, const lf* Ws, int No, int aact, float* dst) {
   const int tid = threadIdx.x, r = tid >> 2, kq = tid & 3;
   float x[16];
@@ -463,7 +439,7 @@ __device__ __forceinline__ void wide_rowdot(const lf* Et, const lf* Ws, int No, 
     }
     s += __shfl_xor(s, 1, 64);
     s += __shfl_xor(s, 2, 64);
-    if (kq == (j & 3)) sth<FL>(dst + (size_t)r * No + j, s);
+    if (kq == (j & 3)) sth(dst + (size_t)r * No + j, s);
   }
 }
 
@@ -481,7 +457,7 @@ __device__ __forceinline__ void wide_rbcb(const AS_C WJob& jb, int it, int& rb, 
   }
 }
 
-template <typename T, int AM, bool HR, bool FL = false>
+template <typename T, int AM, bool HR>
 __device__ __forceinline__ void wide_item(const AS_C EngineDev& E, const AS_C WideDev& W, const AS_C WJob& jb, int it,
                                           lf* lds, int par, bool wst) {
   typedef WK<T> K_;
@@ -526,7 +502,7 @@ __device__ __forceinline__ void wide_item(const AS_C EngineDev& E, const AS_C Wi
     for (int i = 0; i < PR; ++i) {
       const int pa = wave + 4 * i, h = pa % PR;
       const bool v = k0 + K_::chunk(h) * KC < Kp;
-      glds16<FL && SAC_FLOW_SC1_LOADS ? 16 : 0>(xa[i] + (v ? k0 : -K_::koff(h, g)), Aq + pa * 256);  // past Kp: the row's first 4 k
+      glds16(xa[i] + (v ? k0 : -K_::koff(h, g)), Aq + pa * 256);  // past Kp: the row's first 4 k
     }
 #pragma unroll
     for (int i = 0; i < NCH; ++i) {
@@ -585,7 +561,7 @@ __device__ __forceinline__ void wide_item(const AS_C EngineDev& E, const AS_C Wi
   const int J = jb.J;
   const int rA = prt * 16 + (pL & 15);  // the pass's two rows rA, rA + 1
   if constexpr (AM == WA_OUTBWD) {
-    wide_rowpro<T, FL>(E, W, jb, row0, cb, par, Dl);
+    wide_rowpro<T>(E, W, jb, row0, cb, par, Dl);
     for (int i = tid; i < J * Kp; i += WG_T) {
       const int j = i / Kp, k = i % Kp;
       Wol[i] = k < jb.ldwo ? GPC(float, jb.Wo)[(size_t)j * jb.ldwo + k] : 0.f;
@@ -691,7 +667,7 @@ __device__ __forceinline__ void wide_item(const AS_C EngineDev& E, const AS_C Wi
         st4<T>(jb.AGT, (size_t)(k0 + k) * W.Bp + b0, v);
       }
     }
-    if (tid < 4 * KB) {
+    if (jb.Adbp && tid < 4 * KB) {
       const int rt = tid / KB, k = tid % KB, grt = row0 / 16 + rt;
       float s = 0.f;
       for (int r = 0; r < 16; ++r) s += Aq[K_::aloc(rt * 16 + r, k)];
@@ -744,12 +720,12 @@ __device__ __forceinline__ void wide_item(const AS_C EngineDev& E, const AS_C Wi
       if (k < jb.Np) {
         f32x4 v = *(AS_L f32x4*)(Et + r * WLDE + 4 * q);
         if (jb.pact >= 0) {
-          const f32x4 pp = ld16h<FL>(jb.Pprev, (size_t)(row0 + r) * jb.ldpp + k);
+          const f32x4 pp = ld16h(jb.Pprev, (size_t)(row0 + r) * jb.ldpp + k);
 #pragma unroll
           for (int e = 0; e < 4; ++e) v[e] = hactb<HR>(jb.pact, pp[e], v[e]);
           *(AS_L f32x4*)(Et + r * WLDE + 4 * q) = v;
         }
-        if (jb.DY) st16h<FL>(jb.DY, (size_t)(row0 + r) * jb.lddy + k, v);
+        if (jb.DY) st16h(jb.DY, (size_t)(row0 + r) * jb.lddy + k, v);
       }
     }
     __syncthreads();
@@ -773,7 +749,7 @@ __device__ __forceinline__ void wide_item(const AS_C EngineDev& E, const AS_C Wi
       if (grt < W.nrt && col0 + k < jb.N) GP(float, jb.dbp)[(size_t)grt * jb.dbp_ld + col0 + k] = s;
     }
     // d a~ partials: sum over this block's hidden units of dY0[r][n] W0[n][O + j]
-    if (jb.DA) wide_rowdot<HR, false, FL>(Et, Ws, W.A, 0, jb.DA + cb * jb.da_cb + (size_t)row0 * W.A);
+    if (jb.DA) wide_rowdot<HR, false>(Et, Ws, W.A, 0, jb.DA + cb * jb.da_cb + (size_t)row0 * W.A);
     return;
   }
   // forward: pre-activation rows (rows >= p_row0), act(P)^T stash, output-layer partials
@@ -782,7 +758,7 @@ __device__ __forceinline__ void wide_item(const AS_C EngineDev& E, const AS_C Wi
     for (int u = 0; u < 4; ++u) {
       const int p = tid + WG_T * u, r = p >> 4, q = p & 15;
       if (col0 + 4 * q < jb.Np)
-        st16h<FL>(jb.P, (size_t)(row0 + r) * jb.ldp + col0 + 4 * q, *(AS_L f32x4*)(Et + r * WLDE + 4 * q));
+        st16h(jb.P, (size_t)(row0 + r) * jb.ldp + col0 + 4 * q, *(AS_L f32x4*)(Et + r * WLDE + 4 * q));
     }
   }
   if (jb.XT && row0 >= jb.xt_row0) {
@@ -798,7 +774,7 @@ __device__ __forceinline__ void wide_item(const AS_C EngineDev& E, const AS_C Wi
     }
   }
   if (jb.OUTP)
-    wide_rowdot<HR, true, FL>(Et, Ws, jb.Nout, jb.oact, jb.OUTP + cb * jb.outp_cb + (size_t)row0 * jb.Nout);
+    wide_rowdot<HR, true>(Et, Ws, jb.Nout, jb.oact, jb.OUTP + cb * jb.outp_cb + (size_t)row0 * jb.Nout);
 }
 
 // ---------------------------------------------------------------------------- gather
@@ -813,7 +789,7 @@ __device__ __forceinline__ void wide_item(const AS_C EngineDev& E, const AS_C Wi
 // first stage, the critics' X^T by phase B, and pi's X^T is the other step
 // parity's copy from the one phase D of step t reads).
 #define WGR 16
-template <typename T, bool FL = false>
+template <typename T>
 __device__ __forceinline__ void wide_gather_rows(const AS_C EngineDev& E, const AS_C WideDev& W, const sac_replay& rb,
                                                  const int32_t* __restrict__ inj_idx_, uint64_t step, int blk,
                                                  lf* gl) {
@@ -866,20 +842,20 @@ __device__ __forceinline__ void wide_gather_rows(const AS_C EngineDev& E, const 
       if (slot[r] < 0) continue;
       const float x = v[u];
       if (f < O) {
-        sth<FL>(W.Xpi0 + (size_t)(W.Brw + b) * W.ldpi0 + f, x);
-        sth<FL>(W.Xq0 + (size_t)b * W.ldq0 + f, x);
+        sth(W.Xpi0 + (size_t)(W.Brw + b) * W.ldpi0 + f, x);
+        sth(W.Xq0 + (size_t)b * W.ldq0 + f, x);
         GP(float, W.Xc0)[(size_t)b * W.ldq0 + f] = x;
         gl[r * OA + f] = x;
       } else if (f < 2 * O) {
-        sth<FL>(W.Xpi0 + (size_t)b * W.ldpi0 + (f - O), x);
-        sth<FL>(W.Xqt0 + (size_t)b * W.ldq0 + (f - O), x);
+        sth(W.Xpi0 + (size_t)b * W.ldpi0 + (f - O), x);
+        sth(W.Xqt0 + (size_t)b * W.ldq0 + (f - O), x);
       } else if (f < 2 * O + A) {
-        sth<FL>(W.Xq0 + (size_t)b * W.ldq0 + O + (f - 2 * O), x);
+        sth(W.Xq0 + (size_t)b * W.ldq0 + O + (f - 2 * O), x);
         gl[r * OA + O + (f - 2 * O)] = x;
       } else if (f == 2 * O + A) {
-        sth<FL>(W.R + b, x);
+        sth(W.R + b, x);
       } else {
-        sth<FL>(W.Dn + b, x);
+        sth(W.Dn + b, x);
       }
     }
   }
@@ -932,7 +908,7 @@ __global__ void __launch_bounds__(WG_T) sac_wide_gather(const EngineDev* __restr
 // rows (s, draw 1) -> a~ into phase C's critic input, the head stash, log pi.
 // pi rows [rbase, rbase + nrows) (of the 2 Brw rows: s' then s), WG_T / AP
 // rows per pass, one lane per (row, action dim)
-template <typename T, bool FL = false>
+template <typename T>
 __device__ __forceinline__ void wide_head_rows(const AS_C EngineDev& E, const AS_C WideDev& W, int rbase, int nrows,
                                                const float* __restrict__ inj_eps_, uint64_t step) {
   const AS_C NetDev& pi = E.net[NET_PI];
@@ -953,8 +929,8 @@ __device__ __forceinline__ void wide_head_rows(const AS_C EngineDev& E, const AS
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
           const int c = c0 + u < W.ncb_pi ? c0 + u : W.ncb_pi - 1;
-          xm[u] = ldh<FL>(W.OUTPpi + c * W.cbs_pi + (size_t)r * 2 * A + j);
-          xs[u] = ldh<FL>(W.OUTPpi + c * W.cbs_pi + (size_t)r * 2 * A + A + j);
+          xm[u] = ldh(W.OUTPpi + c * W.cbs_pi + (size_t)r * 2 * A + j);
+          xs[u] = ldh(W.OUTPpi + c * W.cbs_pi + (size_t)r * 2 * A + A + j);
         }
 #pragma unroll
         for (int u = 0; u < 8; ++u)
@@ -996,7 +972,7 @@ __device__ __forceinline__ void wide_head_rows(const AS_C EngineDev& E, const AS
           GP(float, W.PIOP)[(size_t)b * 2 * A + A + j] = ps;
         }
       } else {
-        sth<FL>(W.Xqt0 + (size_t)b * W.ldq0 + W.O + j, act_v);
+        sth(W.Xqt0 + (size_t)b * W.ldq0 + W.O + j, act_v);
       }
     }
     for (int o = 1; o < AP; o <<= 1) {
@@ -1009,7 +985,7 @@ __device__ __forceinline__ void wide_head_rows(const AS_C EngineDev& E, const AS
         GP(float, E.lp_st)[par * E.Br + b] = v;
         GP(float, E.stats)[4 + B + b] = v;
       } else {
-        sth<FL>(W.LP2 + b, v);
+        sth(W.LP2 + b, v);
       }
     }
   }
@@ -1067,88 +1043,4 @@ __global__ void __launch_bounds__(WG_T, 4) sac_wide_stage(const EngineDev* __res
   }
 #endif
   if (flags & 1) phase_c_done(E);  // the step's last launch before phase D advances the step
-}
-
-
-// ---------------------------------------------------------------------------- the flow kernel
-// One launch per phase (A, then C): every gather row block, GEMM item and pi
-// head row block of the phase's stages, on a persistent grid of resident
-// workgroups.  Item i runs on workgroup i mod gridDim in stage order, once the
-// items of its row block that it reads are done: per (job, row block)
-// completion counters, advanced with the sc1 hand-off (data stored write-
-// through, each wave's stores retired, one relaxed agent-scope increment;
-// consumers poll relaxed and read with sc1 loads).  Counters run across
-// launches: the target is (this phase's launch epoch + 1) x the producer's
-// items per row block, and the last workgroup out advances the epoch.
-// Deadlock-free: items wait only for lower-numbered items and every workgroup
-// runs its items in increasing order, so the lowest unfinished item can always
-// proceed.  flags: bit 0 = the step's last launch before phase D (advances the
-// step), bit 1 = phase C (its own epoch words).
-#define SYNC_FLOW_EP 80  // sync words: [80] phase A launch epoch, [88] its exit count; [96] / [104] phase C
-template <typename T, bool HR>
-__global__ void __launch_bounds__(WG_T, 4) sac_wide_flow(const EngineDev* __restrict__ Ep, const WideDev* __restrict__ Wd,
-                                                      const WJob* __restrict__ jobs, int njobs, int nitems, int flags,
-                                                      sac_replay rbuf, const int32_t* __restrict__ inj_idx_,
-                                                      const float* __restrict__ inj_eps_) {
-  const AS_C EngineDev& E = *(const AS_C EngineDev*)Ep;
-  const AS_C WideDev& W = *(const AS_C WideDev*)Wd;
-  extern __shared__ float lds_raw[];
-  lf* lds = (lf*)lds_raw;
-  const AS_C WJob* J = (const AS_C WJob*)jobs;
-  const int ph = (flags & 2) ? 1 : 0;
-  uint32_t* sync = (uint32_t*)E.sync;
-  const uint32_t ep = __hip_atomic_load(sync + SYNC_FLOW_EP + 16 * ph, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
-  const uint64_t step = *GPC(uint64_t, E.rng_step);
-  const int par = (int)(step & 1);
-  if (ph == 0 && blockIdx.x == 0) wide_step_scalars(E, par);
-  uint32_t* cnt = W.cnt;
-  for (int i = blockIdx.x; i < nitems; i += gridDim.x) {
-    int j = 0;
-    while (j + 1 < njobs && i >= J[j + 1].item0) ++j;
-    const AS_C WJob& jb = J[j];
-    const int it = i - jb.item0;
-    int rbk, cbk;
-    wide_rbcb(jb, it, rbk, cbk);
-    if (threadIdx.x == 0) {  // the producers of this row block
-      for (int d = 0; d < jb.ndep; ++d) {
-        const AS_C WJob& pj = J[jb.dep_job[d]];
-        const uint32_t* c = cnt + pj.cnt_off + rbk % pj.nrb;
-        const uint32_t tgt = ep * (uint32_t)jb.dep_need[d];
-        for (int sp = 0; (int)(__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - tgt) < 0; ++sp) {
-          if (sp > E.spin_limit) {  // a producer never ran: flag the error, do not hang
-            __hip_atomic_store(sync + SYNC_TIMEOUT, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            break;
-          }
-          __builtin_amdgcn_s_sleep(2);
-        }
-      }
-    }
-    __syncthreads();
-    if (jb.amode == WA_PLAIN) {
-      wide_item<T, WA_PLAIN, HR, true>(E, W, jb, it, lds, par, false);
-    } else if (jb.amode == WA_ACT) {
-      wide_item<T, WA_ACT, HR, true>(E, W, jb, it, lds, par, false);
-    } else if (jb.amode == WA_OUTBWD) {
-      wide_item<T, WA_OUTBWD, HR, true>(E, W, jb, it, lds, par, false);
-    } else if (jb.amode == WA_HEAD) {
-      wide_head_rows<T, true>(E, W, rbk * 64, 64, inj_eps_, step);
-    } else {  // WA_GATHER: 64 batch rows
-      for (int q = 0; q < 64 / WGR; ++q) {
-        wide_gather_rows<T, true>(E, W, rbuf, inj_idx_, step, rbk * (64 / WGR) + q, lds);
-        __syncthreads();
-      }
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's (write-through) stores are done
-    __syncthreads();
-    if (threadIdx.x == 0) __hip_atomic_fetch_add(cnt + jb.cnt_off + rbk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  if (threadIdx.x == 0) {  // the last workgroup out advances this phase's launch epoch
-    const uint32_t old =
-        __hip_atomic_fetch_add(sync + SYNC_FLOW_EP + 8 + 16 * ph, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (old == gridDim.x - 1) {
-      __hip_atomic_store(sync + SYNC_FLOW_EP + 8 + 16 * ph, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(sync + SYNC_FLOW_EP + 16 * ph, ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
-  if (flags & 1) phase_c_done(E);
 }

@@ -49,7 +49,16 @@ class EngineConfig(ctypes.Structure):
         ("beta1", ctypes.c_float), ("beta2", ctypes.c_float), ("adam_eps", ctypes.c_float),
         ("auto_entropy", ctypes.c_int32), ("target_entropy", ctypes.c_float),
         ("precision", ctypes.c_int32), ("seed", ctypes.c_uint64),
+        # kernel layout overrides (0 = the engine's choice; tests and A/B runs only)
+        ("layout", ctypes.c_int32), ("stage_path", ctypes.c_int32), ("stage_batch", ctypes.c_int32),
+        ("upd_parts", ctypes.c_int32), ("upd_threads", ctypes.c_int32),
     ]
+
+
+# sac_engine_config.layout (include/sac_engine.h enum sac_layout)
+LAYOUTS = {"auto": 0, "roles": 1, "rows": 2}
+# the overrides a caller may pass to SacEngine(layout={...}), with their C field
+LAYOUT_KEYS = ("layout", "stage_path", "stage_batch", "upd_parts", "upd_threads")
 
 
 class EngineBuffers(ctypes.Structure):
@@ -96,7 +105,6 @@ SIGNATURES = {
     "sac_phase_kernel_name": (ctypes.c_char_p, [ctypes.c_int32]),
     "sac_engine_check": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
     "sac_engine_set_alpha_update": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p]),
-    "sac_engine_phase_layout": (ctypes.c_int, [ctypes.c_void_p]),
 }
 
 _lib: Optional[ctypes.CDLL] = None

@@ -59,7 +59,13 @@ class SacEngine:
     def __init__(self, policy_net, q_net1, q_net2, q_net1_target, q_net2_target, *, batch_size: int,
                  gamma: float, tau: float, actor_lr: float, critic_lr: float, alpha_lr: float,
                  alpha: float, auto_entropy_tuning: bool, device, precision: str = "fp32",
-                 seed: int = 0, betas=(0.9, 0.999), eps: float = 1e-8):
+                 seed: int = 0, betas=(0.9, 0.999), eps: float = 1e-8, layout: Optional[dict] = None):
+        """``layout`` (tests and A/B runs only; None = the engine's choice, which
+        every measured number uses): kernel layout overrides, the fields of
+        sac_engine_config named in sac._engine.LAYOUT_KEYS -- layout ("auto" |
+        "roles" | "rows"), stage_path (1 force / -1 refuse the stage path),
+        stage_batch (-1: phase A gathers its own batch), upd_parts (batch parts
+        of the large-batch update tiles), upd_threads (512 / 1024)."""
         self.device = torch.device(device)
         E.require_gpu(self.device)
         self.lib = E.load_library()
@@ -111,6 +117,10 @@ class SacEngine:
         cfg.target_entropy = -float(pi.action_size)
         cfg.precision = PRECISIONS[precision]
         cfg.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
+        for k, v in (layout or {}).items():
+            if k not in E.LAYOUT_KEYS:
+                raise ValueError(f"unknown layout override {k!r} (one of {E.LAYOUT_KEYS})")
+            setattr(cfg, k, E.LAYOUTS[v] if k == "layout" else int(v))
         self.cfg = cfg
         ws = self.lib.sac_engine_workspace_bytes(ctypes.byref(cfg))
         if ws == 0:
@@ -142,7 +152,6 @@ class SacEngine:
         self._calls = 0
         self.lib.sac_engine_uses_roles.argtypes = [ctypes.c_void_p]
         self.roles = bool(self.lib.sac_engine_uses_roles(h))
-        self.fused = int(self.lib.sac_engine_phase_layout(h))  # 1: D in the next A's launch, 2: + B in C's
         # large-batch stage path (csrc/sac_wide.h): launches per step, 0 when the phase kernels run
         self.lib.sac_engine_uses_wide.argtypes = [ctypes.c_void_p]
         self.wide = int(self.lib.sac_engine_uses_wide(h))

@@ -53,7 +53,8 @@ def _c_layout(tmp_path):
         "sac_engine_config": ["obs_dim", "act_dim", "batch", "q_layers", "q_dims", "q_hidden_act", "q_out_act",
                               "pi_layers", "pi_dims", "pi_hidden_act", "pi_out_act", "gamma", "tau", "log_std_min",
                               "log_std_max", "action_scale", "actor_lr", "critic_lr", "alpha_lr", "beta1", "beta2",
-                              "adam_eps", "auto_entropy", "target_entropy", "precision", "seed"],
+                              "adam_eps", "auto_entropy", "target_entropy", "precision", "seed", "layout",
+                              "stage_path", "stage_batch", "upd_parts", "upd_threads"],
         "sac_engine_buffers": ["pi", "q1", "q2", "q1t", "q2t", "pi_m", "pi_v", "q1_m", "q1_v", "q2_m", "q2_v",
                                "alpha_state", "opt_steps", "rng_step", "stats", "workspace", "workspace_bytes"],
         "sac_replay": ["obs", "act", "rew", "next_obs", "done", "capacity", "obs_dim", "act_dim", "state",

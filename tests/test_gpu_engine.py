@@ -21,14 +21,16 @@ def lib():
     return E.load_library()
 
 
-def _engine(cfgname="c1", precision="fp32", seed=0, capacity=None):
+def _engine(cfgname="c1", precision="fp32", seed=0, capacity=None, **layout):
+    """bench.build_engine with kernel layout overrides (sac_engine_config.layout
+    and friends, sac.engine.SacEngine(layout=...)) as keyword arguments."""
     import bench
 
     c = dict(bench.CONFIGS[cfgname])
     if capacity:
         bench.CONFIGS[cfgname] = dict(c, capacity=capacity)
     try:
-        return bench.build_engine(cfgname, precision, seed, DEV)
+        return bench.build_engine(cfgname, precision, seed, DEV, layout=layout or None)
     finally:
         bench.CONFIGS[cfgname] = c
 
@@ -110,7 +112,7 @@ def test_device_sampler_equals_host(lib, size, batch):
 
 def test_in_step_sampler_is_the_exported_sampler(lib):
     """A device-sampled step equals the same step fed the host sampler's
-    indices for (seed, rng_step): the fused kernel gathers exactly those rows."""
+    indices for (seed, rng_step): the step kernels gather exactly those rows."""
     eng, rb, c = _engine("c1", "fp32")
     f = lib.sac_debug_sample_indices_host
     f.argtypes = [ctypes.c_int64, ctypes.c_int32, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_void_p]
@@ -226,17 +228,16 @@ def test_save_load_roundtrip_continues_identically(tmp_path):
     assert torch.equal(agent.engine.stats[:4], other.engine.stats[:4])
 
 
-# ---------------------------------------------------------------- role-split vs fused phase kernels
+# ---------------------------------------------------------------- role-split vs row-tile phase kernels
 @pytest.mark.parametrize("precision", ["fp32", "bf16"])
-def test_role_split_equals_fused(precision, monkeypatch):
+def test_role_split_equals_row_tiles(precision):
     """Phases A/C split into per-network workgroups with in-launch hand-offs give
     the same bits as the one-workgroup-per-row-tile kernels (power-of-two batch:
-    the min-Q weights are applied after a unit-seed backward, exactly)."""
-    monkeypatch.setenv("SAC_SPLIT", "0")  # the hidden-split kernels sum in another order (tested vs the oracle)
+    the min-Q weights are applied after a unit-seed backward, exactly).  Both
+    without the hidden split, which sums in another order (tested vs the oracle)."""
     out = {}
     for roles in ("1", "0"):
-        monkeypatch.setenv("SAC_ROLES", roles)
-        eng, rb, c = _engine("c2", precision, capacity=5000)
+        eng, rb, c = _engine("c2", precision, capacity=5000, layout="roles" if roles == "1" else "rows")
         assert bool(eng.roles) == (roles == "1")
         eng.train(rb, 4)
         eng.train_graph(rb, 6, chunk=3)
@@ -247,19 +248,19 @@ def test_role_split_equals_fused(precision, monkeypatch):
         assert torch.equal(out["1"][k], out["0"][k]), k
 
 
-def test_large_batch_uses_fused_kernels_and_runs(monkeypatch):
+def test_large_batch_uses_row_tile_kernels_and_runs():
     """C3 (B=4096): 256 row tiles do not fit the role split; the one-block-per-
-    row-tile kernels run (C3's default; SAC_WIDE=0 also refuses the stage path)."""
-    monkeypatch.setenv("SAC_WIDE", "0")
-    eng, rb, c = _engine("c3", "bf16", capacity=20_000)
+    row-tile kernels run (C3's default; stage_path=-1 also refuses the stage path)."""
+    eng, rb, c = _engine("c3", "bf16", capacity=20_000, stage_path=-1)
     assert not eng.roles and not eng.wide
     eng.train_graph(rb, 20, chunk=10)
     eng.check()
     assert all(np.isfinite(eng.losses()))
 
 
-@pytest.mark.parametrize("cfg,precision,fuse", [("c2", "bf16", "0"), ("c2", "fp32", "2"), ("c3", "bf16", "0")])
-def test_staged_batch_equals_in_step_gather(cfg, precision, fuse, monkeypatch):
+@pytest.mark.parametrize("cfg,precision,layout", [("c2", "bf16", "auto"), ("c2", "fp32", "roles"),
+                                                  ("c3", "bf16", "auto")])
+def test_staged_batch_equals_in_step_gather(cfg, precision, layout):
     """Phase C staging step t+1's batch (sampled and gathered one launch early)
     gives the same bits as phase A gathering it, across graph replays, a replay
     push between calls (the staged record goes stale and phase A gathers), and
@@ -268,15 +269,11 @@ def test_staged_batch_equals_in_step_gather(cfg, precision, fuse, monkeypatch):
 
     from sac import _engine as E
 
-    monkeypatch.setenv("SAC_FUSE", fuse)
-    if cfg == "c3":
-        monkeypatch.setenv("SAC_WIDE", "0")  # batch staging is a feature of the row-tile kernels
-    if fuse != "0":
-        monkeypatch.setenv("SAC_SPLIT", "0")  # fused layouts run the one-workgroup-per-role kernels
     out = {}
     for stage in ("1", "0"):
-        monkeypatch.setenv("SAC_STAGE", stage)
-        eng, rb, c = _engine(cfg, precision, capacity=5000)
+        # stage_path=-1 at C3: batch staging is a feature of the row-tile kernels
+        eng, rb, c = _engine(cfg, precision, capacity=5000, layout=layout, stage_batch=0 if stage == "1" else -1,
+                             stage_path=-1 if cfg == "c3" else 0)
         eng.train(rb, 3)
         eng.train_graph(rb, 5, chunk=2)
         if stage == "1":
@@ -298,27 +295,6 @@ def test_staged_batch_equals_in_step_gather(cfg, precision, fuse, monkeypatch):
         out[stage]["stats"] = eng.stats.clone()
     for k in out["1"]:
         assert torch.equal(out["1"][k], out["0"][k]), k
-
-
-@pytest.mark.parametrize("precision,layout", [("fp32", "1"), ("bf16", "1"), ("fp32", "2"), ("bf16", "2")])
-def test_fused_launches_equal_four_launches(precision, layout, monkeypatch):
-    """Two launches per step (phase D inside the next phase A launch, phase B
-    inside the phase C launch, in-launch completion counters) give the same
-    bits as four launches per step."""
-    monkeypatch.setenv("SAC_SPLIT", "0")  # fused layouts run the one-workgroup-per-role kernels
-    out = {}
-    for fuse in (layout, "0"):
-        monkeypatch.setenv("SAC_FUSE", fuse)
-        eng, rb, c = _engine("c2", precision, capacity=5000)
-        assert eng.fused == int(fuse)
-        eng.train(rb, 3)
-        eng.train_graph(rb, 7, chunk=3)
-        eng.train(rb, 1)
-        eng.check()
-        out[fuse] = {k: v.clone() for k, v in eng.state_tensors().items()}
-        out[fuse]["stats"] = eng.stats.clone()
-    for k in out[layout]:
-        assert torch.equal(out[layout][k], out["0"][k]), k
 
 
 # ---------------------------------------------------------------- hand-off status (round 2)
@@ -381,15 +357,14 @@ def test_concurrent_engines_on_streams_match_serial():
             assert torch.equal(runs["serial"][i][k], runs["concurrent"][i][k]), (i, k)
 
 
-def test_clear_and_refill_invalidates_the_staged_batch(monkeypatch):
+def test_clear_and_refill_invalidates_the_staged_batch():
     """ReplayBuffer.clear() followed by a refill to the same (size, write slot)
     must not let phase A use the batch phase C staged from the old rows: the
     push generation in the replay state differs, so phase A gathers the new
     rows (same bits as a run with staging off)."""
     out = {}
     for stage in ("1", "0"):
-        monkeypatch.setenv("SAC_STAGE", stage)
-        eng, rb, c = _engine("c2", "fp32", capacity=4096)
+        eng, rb, c = _engine("c2", "fp32", capacity=4096, stage_batch=0 if stage == "1" else -1)
         eng.train(rb, 2)  # phase C of step 2 staged step 3's batch from the old rows
         g = np.random.default_rng(9)
         rb.clear()
@@ -480,7 +455,7 @@ def test_c3_full_size_properties():
 
 @pytest.mark.parametrize("precision", ["fp32", "bf16"])
 def test_training_is_layout_independent(precision):
-    """The fused step reads the replay through its field strides: the same rows
+    """The step reads the replay through its field strides: the same rows
     in transition records and in struct-of-arrays give the same bits (device
     sampler, staged next-step batches and graph replay included)."""
     import bench
@@ -501,7 +476,7 @@ def test_training_is_layout_independent(precision):
 
 
 @pytest.mark.parametrize("precision", ["fp32", "bf16"])
-def test_hidden_split_is_used_and_close_to_unsplit(lib, precision, monkeypatch):
+def test_hidden_split_is_used_and_close_to_unsplit(lib, precision):
     """C2 runs the hidden-split role kernels (two workgroups per role and row
     tile); 5 device-sampled steps agree with the unsplit role kernels to
     rounding (the split only changes the summation order of layers 1-2 and of
@@ -509,8 +484,7 @@ def test_hidden_split_is_used_and_close_to_unsplit(lib, precision, monkeypatch):
     lib.sac_engine_uses_split.argtypes = [ctypes.c_void_p]
     out = {}
     for split in ("1", "0"):
-        monkeypatch.setenv("SAC_SPLIT", split)
-        eng, rb, c = _engine("c2", precision, capacity=5000)
+        eng, rb, c = _engine("c2", precision, capacity=5000, layout="auto" if split == "1" else "roles")
         assert lib.sac_engine_uses_split(eng.handle) == int(split)
         eng.train(rb, 2)
         eng.train_graph(rb, 3, chunk=3)
@@ -523,53 +497,16 @@ def test_hidden_split_is_used_and_close_to_unsplit(lib, precision, monkeypatch):
         assert torch.allclose(a, b, rtol=tol, atol=tol), (k, (a - b).abs().max().item())
 
 
-# ---------------------------------------------------------------- fused step (round 3)
-@pytest.mark.parametrize("cfg,precision", [("c2", "fp32"), ("c2", "bf16"), ("c4", "fp32"), ("c4", "bf16")])
-def test_fused_step_equals_four_launches(lib, cfg, precision, monkeypatch):
-    """The fused step (sac_persist.h: the four phases of a step in one launch
-    of one workgroup per CU, readiness counters in place of the kernel
-    boundaries, every cross-workgroup byte stored and loaded sc1) runs the
-    phase kernels' own device code: device-sampled steps, graph-replayed
-    steps, injected indices + eps, a replay push in between -- the same bits
-    as four launches per step."""
-    lib.sac_engine_uses_fused_step.argtypes = [ctypes.c_void_p]
-    out = {}
-    for fused in ("1", "0"):
-        monkeypatch.setenv("SAC_PERSIST", fused)
-        eng, rb, c = _engine(cfg, precision, capacity=5000)
-        g_ = lib.sac_engine_uses_fused_step(eng.handle)
-        assert (g_ > 0) == (fused == "1"), g_
-        eng.train(rb, 3)
-        eng.train_graph(rb, 6, chunk=3)
-        g = np.random.default_rng(3)
-        B, A = c["batch"], c["act"]
-        idx = torch.from_numpy(g.choice(len(rb), size=(2, B), replace=False).astype(np.int32))
-        eps = torch.from_numpy(g.standard_normal((2, 2, B, A)).astype(np.float32))
-        eng.train(rb, 2, indices=idx, eps=eps)
-        n = 5
-        rb.push_batch(g.standard_normal((n, c["obs"]), dtype=np.float32), g.uniform(-1, 1, (n, A)),
-                      g.standard_normal(n), g.standard_normal((n, c["obs"]), dtype=np.float32), g.random(n) < 0.1)
-        eng.train(rb, 2)
-        eng.check()
-        out[fused] = {k: v.clone() for k, v in eng.state_tensors().items()}
-        out[fused]["stats"] = eng.stats.clone()
-    for k in out["1"]:
-        assert torch.equal(out["1"][k], out["0"][k]), (k, (out["1"][k].double() - out["0"][k].double()).abs().max())
-
-
-@pytest.mark.parametrize("precision,flow", [("fp32", "0"), ("bf16", "0"), ("fp32", "1"), ("bf16", "1")])
-def test_stage_path_staged_batches_equal_fresh_gathers(precision, flow, monkeypatch):
-    """The stage path (csrc/sac_wide.h, forced at C3 by SAC_WIDE=1) gathers step
-    t+1's batch inside step t's last phase-C launch; the first step of every
-    call gathers its own (the flow kernel, SAC_WIDE_FLOW=1, gathers every step
-    inside its phase-A launch).  So one call of 5 steps (device RNG) must equal
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_stage_path_staged_batches_equal_fresh_gathers(precision):
+    """The stage path (csrc/sac_wide.h, forced at C3 by stage_path=1) gathers
+    step t+1's batch inside step t's last phase-C launch; the first step of
+    every call gathers its own.  So one call of 5 steps (device RNG) must equal
     5 calls of one step, bit for bit, and the same with injected indices; graph
     replay equals eager launches."""
-    monkeypatch.setenv("SAC_WIDE", "1")
-    monkeypatch.setenv("SAC_WIDE_FLOW", flow)
     out = {}
     for mode in ("one_call", "per_step", "graph"):
-        eng, rb, c = _engine("c3", precision, capacity=12_000)
+        eng, rb, c = _engine("c3", precision, capacity=12_000, stage_path=1)
         assert eng.wide > 0
         if mode == "one_call":
             eng.train(rb, 5)

@@ -78,99 +78,33 @@ def test_engine_matches_oracle(name, precision):
             assert abs(la - st.log_alpha) <= (1e-7 if precision == "fp32" else 1e-5), (la, st.log_alpha)
 
 
-@pytest.mark.parametrize("precision,parts", [("fp32", "4"), ("bf16", "2")])
-def test_c3_batch_part_counts_match_oracle(precision, parts, monkeypatch):
+@pytest.mark.parametrize("precision,parts", [("fp32", 4), ("bf16", 2)])
+def test_c3_batch_part_counts_match_oracle(precision, parts):
     """C3's update tiles with a batch-part count other than the cost model's
-    choice (3; SAC_BPARTS overrides it): 4 parts (the round-2 layout before the
-    model) and 2, against the oracle like test_baseline_config_matches_oracle."""
-    monkeypatch.setenv("SAC_BPARTS", parts)
-    test_baseline_config_matches_oracle("c3", 12_288, 2, precision)
+    choice (3; config.upd_parts overrides it): 4 parts (the round-2 layout
+    before the model) and 2, against the oracle like
+    test_baseline_config_matches_oracle."""
+    test_baseline_config_matches_oracle("c3", 12_288, 2, precision, layout={"upd_parts": parts})
 
 
-@pytest.mark.parametrize("name,batch,steps", [("c3", 12_288, 2), ("c2", 4096, 3)])
-@pytest.mark.parametrize("precision", ["fp32", "bf16"])
-def test_bias_gradient_sources_match_oracle(name, batch, steps, precision, monkeypatch):
-    """The update tiles' bias gradient from the row tiles' partial sums
-    (SAC_BIAS_STAGED=0; the default sums the staged dY rows) at C3 and C2,
-    against the oracle like test_baseline_config_matches_oracle."""
-    import bench
-
-    monkeypatch.setenv("SAC_BIAS_STAGED", "0")
-    _check_config_against_oracle(dict(bench.CONFIGS[name], capacity=batch), precision, steps, roles=name != "c3")
-
-
-@pytest.mark.parametrize("precision,parts", [("fp32", None), ("bf16", None), ("fp32", "4")])
-def test_c3_update_block_sizes_match_oracle(precision, parts, monkeypatch):
-    """C3's phase B with the 1024-thread update tiles (SAC_UPD_UT=1024; C3's
-    default runs its 480 B blocks as 512-thread tiles, two per CU), default
-    batch parts, and the 512-thread tiles at 4 parts (640 blocks, two rounds),
-    against the oracle like test_baseline_config_matches_oracle."""
-    monkeypatch.setenv("SAC_UPD_UT", "512" if parts else "1024")
+@pytest.mark.parametrize("precision,parts", [("fp32", None), ("bf16", None), ("fp32", 4)])
+def test_c3_update_block_sizes_match_oracle(precision, parts):
+    """C3's phase B with the 1024-thread update tiles (config.upd_threads =
+    1024; C3's default runs its 480 B blocks as 512-thread tiles, two per CU),
+    default batch parts, and the 512-thread tiles at 4 parts (640 blocks, two
+    rounds), against the oracle like test_baseline_config_matches_oracle."""
+    lay = {"upd_threads": 512 if parts else 1024}
     if parts:
-        monkeypatch.setenv("SAC_BPARTS", parts)
-    test_baseline_config_matches_oracle("c3", 12_288, 2, precision)
-
-
-@pytest.mark.parametrize("precision,parts", [("fp32", None), ("bf16", None), ("fp32", "8")])
-def test_c3_half_size_policy_update_blocks_match_oracle(precision, parts, monkeypatch):
-    """C3's phase D as 512-thread update tiles (SAC_UPD_UT_D=512: up to 8 batch
-    parts, 7 producer parts per consumer; default 6 and 8 parts), against the
-    oracle like test_baseline_config_matches_oracle."""
-    monkeypatch.setenv("SAC_UPD_UT_D", "512")
-    if parts:
-        monkeypatch.setenv("SAC_BPARTS_D", parts)
-    test_baseline_config_matches_oracle("c3", 12_288, 2, precision)
+        lay["upd_parts"] = parts
+    test_baseline_config_matches_oracle("c3", 12_288, 2, precision, layout=lay)
 
 
 @pytest.mark.parametrize("precision", ["fp32", "bf16"])
-def test_c3_forced_role_kernels_match_oracle(precision, monkeypatch):
-    """C3 through the per-network role kernels past co-residency (SAC_ROLES=2:
-    6 x 256 phase-A blocks, progress by in-order dispatch), against the oracle
-    like test_baseline_config_matches_oracle."""
-    import bench
-
-    monkeypatch.setenv("SAC_ROLES", "2")
-    _check_config_against_oracle(dict(bench.CONFIGS["c3"], capacity=12_288), precision, 2, roles=True)
-
-
-@pytest.mark.parametrize("precision", ["fp32", "bf16"])
-def test_c3_stage_path_matches_oracle(precision, monkeypatch):
-    """C3 through the layer-synchronous stage path (SAC_WIDE=1; the row-tile
+def test_c3_stage_path_matches_oracle(precision):
+    """C3 through the layer-synchronous stage path (stage_path=1; the row-tile
     kernels are C3's default), against the oracle like
     test_baseline_config_matches_oracle."""
-    monkeypatch.setenv("SAC_WIDE", "1")
-    test_baseline_config_matches_oracle("c3", 12_288, 2, precision)
-
-
-@pytest.mark.parametrize("precision,parts", [("fp32", None), ("bf16", None), ("fp32", "2")])
-def test_c3_tile64_matches_oracle(precision, parts, monkeypatch):
-    """C3 with the 64 x 64 update tiles (SAC_TILE64=1, dw_adam_tile64; default
-    part count and 2 parts), against the oracle like
-    test_baseline_config_matches_oracle."""
-    monkeypatch.setenv("SAC_TILE64", "1")
-    if parts:
-        monkeypatch.setenv("SAC_BPARTS", parts)
-    test_baseline_config_matches_oracle("c3", 12_288, 2, precision)
-
-
-@pytest.mark.parametrize("precision", ["fp32", "bf16"])
-def test_c3_flow_path_matches_oracle(precision, monkeypatch):
-    """C3 through the flow kernel (SAC_WIDE=1 SAC_WIDE_FLOW=1: phases A and C
-    as one persistent launch each, row-block counters between the stage
-    items), against the oracle like test_baseline_config_matches_oracle."""
-    monkeypatch.setenv("SAC_WIDE", "1")
-    monkeypatch.setenv("SAC_WIDE_FLOW", "1")
-    test_baseline_config_matches_oracle("c3", 12_288, 2, precision)
-
-
-@pytest.mark.parametrize("shape", ["wide_deep_b1100", "wide512_b384", "wide400_300"])
-def test_flow_path_edge_shapes_match_oracle(shape, monkeypatch):
-    """The flow kernel at ragged column blocks, three hidden layers and the
-    widths past the phase kernels' LDS, fp32, tolerances as the edge shapes."""
-    monkeypatch.setenv("SAC_WIDE", "1")
-    monkeypatch.setenv("SAC_WIDE_FLOW", "1")
-    c = dict(EDGE_SHAPES[shape], name=shape)
-    _check_config_against_oracle(c, "fp32", 2 if c["batch"] > 1024 else 3, traj_tol=2e-3)
+    test_baseline_config_matches_oracle("c3", 12_288, 2, precision, layout={"stage_path": 1})
 
 
 @pytest.mark.parametrize("name", ["c1_auto", "c2"])
@@ -203,7 +137,7 @@ BENCH_NETS = {"policy": "pi", "q1": "q1", "q2": "q2", "q1t": "q1t", "q2t": "q2t"
 
 @pytest.mark.parametrize("precision", ["fp32", "bf16"])
 @pytest.mark.parametrize("cfg,capacity,steps", [("c4", 4096, 3), ("c4w", 2048, 3), ("c3", 12_288, 2)])
-def test_baseline_config_matches_oracle(cfg, capacity, steps, precision):
+def test_baseline_config_matches_oracle(cfg, capacity, steps, precision, layout=None):
     """The BASELINE.json configs the fixtures do not cover, against the
     fixture-pinned oracle on seeded batches with injected indices and eps:
       c4  DonkeyVae as BASELINE.json states it: obs 32, act 2, [256,256], B 256;
@@ -218,7 +152,7 @@ def test_baseline_config_matches_oracle(cfg, capacity, steps, precision):
     import bench
 
     _check_config_against_oracle(dict(bench.CONFIGS[cfg], capacity=capacity), precision, steps,
-                                 roles=cfg != "c3")
+                                 roles=cfg != "c3", layout=layout)
 
 
 # Shapes at the edges of the kernels' tiling, none of them a BASELINE config:
@@ -244,36 +178,33 @@ EDGE_SHAPES = {
 
 @pytest.mark.parametrize("precision", ["fp32", "bf16"])
 @pytest.mark.parametrize("shape", sorted(EDGE_SHAPES))
-def test_edge_shapes_match_oracle(shape, precision, monkeypatch):
+def test_edge_shapes_match_oracle(shape, precision):
     """Ragged and extreme shapes against the oracle, with the same checks and
     tolerances as the BASELINE configs (parity unpinned by the reference at
     these shapes; the oracle is pinned by the 8 reference fixtures).
     wide_deep_b1100 runs the stage path (forced: the row-tile kernels fit it)."""
-    if shape == "wide_deep_b1100":
-        monkeypatch.setenv("SAC_WIDE", "1")
     c = dict(EDGE_SHAPES[shape], name=shape)
     # y / log pi against the oracle's trajectory after step 1: 2e-3 at these
     # shapes (measured 6.1e-4 at obs 256, step 3: Adam sign flips of ~0 gradients)
-    _check_config_against_oracle(c, precision, 2 if c["batch"] > 1024 else 3, traj_tol=2e-3)
+    _check_config_against_oracle(c, precision, 2 if c["batch"] > 1024 else 3, traj_tol=2e-3,
+                                 layout={"stage_path": 1} if shape == "wide_deep_b1100" else None)
 
 
-# shapes the phase kernels fit: the stage path runs them only when forced (SAC_WIDE=1)
+# shapes the phase kernels fit: the stage path runs them only when forced (stage_path=1)
 STAGE_FORCED = {"wide_deep_b1100", "rowtile_b4001"}
 
 
 @pytest.mark.parametrize("shape", ["obs300", "wide400_300", "wide512_b384", "wide_deep_b1100", "rowtile_b4001"])
-def test_stage_path_is_used_where_the_phase_kernels_do_not_fit(shape, monkeypatch):
+def test_stage_path_is_used_where_the_phase_kernels_do_not_fit(shape):
     """Shapes past the phase kernels' LDS layout run the layer-synchronous stage
     path (no fallback, no refusal); batches past the role split run it when
-    SAC_WIDE=1 forces it."""
+    stage_path=1 forces it."""
     import bench
-
-    if shape in STAGE_FORCED:
-        monkeypatch.setenv("SAC_WIDE", "1")
 
     bench.CONFIGS["_stage"] = dict(EDGE_SHAPES[shape])
     try:
-        eng, rb, cc = bench.build_engine("_stage", "fp32", 3, torch.device("cuda", 0))
+        eng, rb, cc = bench.build_engine("_stage", "fp32", 3, torch.device("cuda", 0),
+                                         layout={"stage_path": 1} if shape in STAGE_FORCED else None)
     finally:
         del bench.CONFIGS["_stage"]
     assert eng.wide > 0 and not eng.roles
@@ -288,7 +219,7 @@ def _engine_mlp(eng, key):
                                  "relu")
 
 
-def _check_config_against_oracle(c, precision, steps, roles=None, traj_tol=1e-4):
+def _check_config_against_oracle(c, precision, steps, roles=None, traj_tol=1e-4, layout=None):
     """`steps` engine steps of config c against two oracles, with injected
     indices and eps:
       the trajectory oracle, started from the engine's initial state and run
@@ -308,7 +239,7 @@ def _check_config_against_oracle(c, precision, steps, roles=None, traj_tol=1e-4)
     ckey = "_parity_" + c.get("name", "cfg")
     bench.CONFIGS[ckey] = c
     try:
-        eng, rb, cc = bench.build_engine(ckey, precision, 3, torch.device("cuda", 0))
+        eng, rb, cc = bench.build_engine(ckey, precision, 3, torch.device("cuda", 0), layout=layout)
     finally:
         del bench.CONFIGS[ckey]
     if roles is not None:
@@ -412,7 +343,7 @@ def _oracle_state_from_engine(eng, act):
 
 @pytest.mark.parametrize("shape", ["c2_split", "c4", "roles_b384", "rowtile_b2000", "stage_b2000",
                                    "wide512_b384", "wide400_300"])
-def test_one_step_from_the_engine_state(shape, monkeypatch):
+def test_one_step_from_the_engine_state(shape):
     """Per-step parity without trajectory drift (fp32): before every step the
     oracle is loaded with the engine's FULL state (parameters, Adam moments and
     step counts, alpha), runs the same step, and every post-step parameter of
@@ -430,13 +361,12 @@ def test_one_step_from_the_engine_state(shape, monkeypatch):
          "stage_b2000": dict(obs=17, act=6, hidden=[128, 128], batch=2000, capacity=4096),
          "wide512_b384": dict(obs=24, act=4, hidden=[512, 512], batch=384, capacity=2048),
          "wide400_300": dict(obs=17, act=6, hidden=[400, 300], batch=256, capacity=2048)}[shape]
-    if shape == "roles_b384":
-        monkeypatch.setenv("SAC_SPLIT", "0")
-    if shape == "stage_b2000":
-        monkeypatch.setenv("SAC_WIDE", "1")  # the stage path (the row-tile kernels fit B = 2000)
+    # roles_b384: the role kernels without the hidden split; stage_b2000: the
+    # stage path (the row-tile kernels fit B = 2000)
+    lay = {"roles_b384": {"layout": "roles"}, "stage_b2000": {"stage_path": 1}}.get(shape)
     bench.CONFIGS["_local"] = c
     try:
-        eng, rb, cc = bench.build_engine("_local", "fp32", 3, torch.device("cuda", 0))
+        eng, rb, cc = bench.build_engine("_local", "fp32", 3, torch.device("cuda", 0), layout=lay)
     finally:
         del bench.CONFIGS["_local"]
     B, A = cc["batch"], cc["act"]

@@ -1,12 +1,13 @@
 """The engine's launch plan on the CPU (no GPU needed): sac_engine_create runs
 the whole planner -- phase layouts, update tiles with their batch parts and
-bias blocks, the fused step's task table -- before its first HIP call.  On a
+bias blocks, the stage path's job list -- before its first HIP call.  On a
 machine without a GPU it must therefore stop at that first HIP call
 (SAC_E_HIP), never at the planner's own consistency check ("internal: ...",
 SAC_E_INVALID): a mismatch between the tiles the planner counts (the grids of
 phases B and D) and the tiles it builds would make the update kernels read
 descriptors that do not exist.  Every bench config, both precisions, and the
-diagnostic layouts the env switches select."""
+diagnostic layouts sac_engine_config's override fields select (the library
+reads no environment: tested on its dynamic symbol table)."""
 import ctypes
 import os
 import sys
@@ -46,16 +47,16 @@ def _cfg(name, precision):
     return cfg
 
 
-@pytest.mark.parametrize("env", ["", "SAC_PERSIST=1", "SAC_STAGE=0", "SAC_PI0_PARTS=1", "SAC_ROLE_XCD=0",
-                                 "SAC_SPLIT=0", "SAC_BPARTS=4"])
+@pytest.mark.parametrize("override", ["", "stage_batch=-1", "layout=1", "layout=2", "upd_parts=4",
+                                      "upd_threads=1024", "stage_path=1", "stage_path=-1"])
 @pytest.mark.parametrize("precision", ["fp32", "bf16"])
 @pytest.mark.parametrize("name", sorted(bench.CONFIGS))
-def test_plan_is_consistent(name, precision, env, monkeypatch):
-    if env:
-        k, v = env.split("=")
-        monkeypatch.setenv(k, v)
+def test_plan_is_consistent(name, precision, override):
     lib = E.load_library()
     cfg = _cfg(name, precision)
+    if override:
+        k, v = override.split("=")
+        setattr(cfg, k, int(v))
     ws = lib.sac_engine_workspace_bytes(ctypes.byref(cfg))
     assert ws > 0, lib.sac_last_error()
     bufs = E.EngineBuffers(*([0x1000] * 15), 0x100000, ws)  # never dereferenced before the first HIP call
@@ -104,3 +105,29 @@ def test_one_wide_hidden_layer_is_refused():
     the byte count, before any HIP call."""
     rc, msg = _create_rc(24, 4, [1024])
     assert rc == SAC_E_INVALID and "B of LDS per workgroup (max 163840)" in msg, (rc, msg)
+
+
+@pytest.mark.parametrize("field,value", [("layout", 3), ("stage_path", 2), ("stage_batch", 1), ("upd_parts", 5),
+                                         ("upd_threads", 256)])
+def test_bad_layout_override_is_refused(field, value):
+    """Out-of-range override fields fail validation (SAC_E_INVALID) in both the
+    workspace query and create, before any HIP call."""
+    lib = E.load_library()
+    cfg = _cfg("c2", "fp32")
+    setattr(cfg, field, value)
+    assert lib.sac_engine_workspace_bytes(ctypes.byref(cfg)) == 0
+    bufs = E.EngineBuffers(*([0x1000] * 15), 0x100000, 1 << 30)
+    out = ctypes.c_void_p()
+    rc = lib.sac_engine_create(ctypes.byref(cfg), ctypes.byref(bufs), None, ctypes.byref(out))
+    assert rc == SAC_E_INVALID and "layout override" in lib.sac_last_error().decode()
+
+
+def test_engine_library_reads_no_environment():
+    """the product library takes every layout choice from
+    sac_engine_config; no getenv / secure_getenv import in its dynamic symbols
+    (the SAC_STAMPS diagnostic build may read one)."""
+    import subprocess
+
+    syms = subprocess.run(["nm", "-D", "--undefined-only", E.library_path()], capture_output=True, text=True,
+                          check=True).stdout
+    assert "getenv" not in syms, [ln for ln in syms.splitlines() if "getenv" in ln]

@@ -35,8 +35,7 @@ def _tiles(dims):
 O_, A_, H_ = c["obs"], c["act"], c["hidden"]
 n_b = 2 * _tiles([O_ + A_] + H_ + [1])
 n_d = _tiles([O_] + H_ + [2 * A_])
-# role blocks start after the update tiles in the fused launches
-OFF = {"A": n_d + 1, "C": n_b} if eng.fused else {"A": 0, "C": 0}
+OFF = {"A": 0, "C": 0}  # role blocks are the launches' first blocks
 lib.sac_engine_uses_split.argtypes = [ctypes.c_void_p]
 SPLIT = bool(lib.sac_engine_uses_split(eng.handle))
 GROUP = 2 * nrt if SPLIT else nrt  # blocks per role group (hidden split: two halves per row tile in A)
@@ -83,7 +82,7 @@ WPI = (4 if prec == "fp32" else 2) if SPLIT else 1  # phase A: pi(s') parts (spl
 
 # phase A's split kernel places each weight part's workgroups on one or two XCDs
 # (EngineDev::role_xcd, default on): hardware block -> the body's block id
-ROLE_XCD = SPLIT and os.environ.get("SAC_ROLE_XCD", "1") != "0" and (10 + WPI) * nrt % 8 == 0
+ROLE_XCD = SPLIT and (10 + WPI) * nrt % 8 == 0
 
 
 def _role_xcd_bid(b):
