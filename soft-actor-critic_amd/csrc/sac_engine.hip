@@ -1053,7 +1053,7 @@ static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
             t.gsum = 1;
             t.goff = 0;
             t.seed = nullptr;
-            if (split && esz == 4 && ni != NET_PI) t.seed = h.seedq + (size_t)(ni - NET_Q1) * Bp;
+            if (split && ni != NET_PI) t.seed = h.seedq + (size_t)(ni - NET_Q1) * Bp;
             if (l == 0 && split) {  // one block: dY parts [p Bp, (p+1) Bp) summed, X^T [0, Bp)
               t.gsum = ni == NET_PI ? wc : 2;
               t.goff = Bp;

@@ -410,7 +410,7 @@ __device__ __forceinline__ void mma_batch(const lf* __restrict__ arow, int lda, 
 // whose loads are all issued before the batch's first MFMA.  A short last batch
 // loads its last chunk again for the missing slots (unconditional, so the loads
 // stay back to back) and skips their MFMAs.
-template <typename T, int RT, int BM, bool COH>
+template <typename T, int RT, int BM>
 __device__ __forceinline__ void mma_pair_from(const lf* __restrict__ arow, int lda, __amdgpu_buffer_rsrc_t rs,
                                               uint32_t o0, uint32_t o1, bool has1, int ch0, int nch,
                                               f32x4 (&acc0)[RT], f32x4 (&acc1)[RT]) {
@@ -423,8 +423,8 @@ __device__ __forceinline__ void mma_pair_from(const lf* __restrict__ arow, int l
 #pragma unroll
     for (int u = 0; u < BM; ++u) {
       const uint32_t cu = ch + (u < rem ? u : rem - 1);
-      f0[u] = coh_frag<T, COH>(rs, o0 + cu * FSB);
-      f1[u] = coh_frag<T, COH>(rs, o1 + cu * FSB);
+      f0[u] = coh_frag<T, false>(rs, o0 + cu * FSB);
+      f1[u] = coh_frag<T, false>(rs, o1 + cu * FSB);
     }
     if (rem == BM) {  // full batch: every A fragment read from LDS up front, then the MFMAs
       mma_batch<T, RT, BM>(arow, lda, ch, has1, f0, f1, acc0, acc1);
@@ -500,7 +500,7 @@ __device__ __forceinline__ void gemm_pair_fixed(const lf* __restrict__ arow, int
 // acc = sum_k A[r][k] B[col][k]; epi(h, col, acc[RT]) consumes each tile pair.
 // Batch 0 of the first pair comes from pf; the next step's batch 0 is issued
 // into pf right after those MFMAs.
-template <typename T, int ROWS, bool COH, int HC, typename Epi>
+template <typename T, int ROWS, int HC, typename Epi>
 __device__ __forceinline__ void gemm_step(const lf* __restrict__ A, int lda, const GemmW& w, Pf<T>& pf,
                                           const GemmW& next, Epi epi, const Held<T, HC ? HC : 1>* held) {
   constexpr int RT = ROWS / 16;
@@ -512,11 +512,11 @@ __device__ __forceinline__ void gemm_step(const lf* __restrict__ A, int lda, con
 #if !SAC_PF
   if (w.NT == 2 * SAC_NW) {  // one pair per wave (uniform branches)
     if (nch == 8) {
-      gemm_pair_fixed<T, RT, 8, COH, HC>(arow, lda, w, lane, wave, c, epi, held);
+      gemm_pair_fixed<T, RT, 8, false, HC>(arow, lda, w, lane, wave, c, epi, held);
       return;
     }
     if (nch == 1) {
-      gemm_pair_fixed<T, RT, 1, COH, HC>(arow, lda, w, lane, wave, c, epi, held);
+      gemm_pair_fixed<T, RT, 1, false, HC>(arow, lda, w, lane, wave, c, epi, held);
       return;
     }
   }
@@ -552,7 +552,7 @@ __device__ __forceinline__ void gemm_step(const lf* __restrict__ A, int lda, con
       pf_issue<T>(pf, next);
       __builtin_amdgcn_sched_barrier(0);
     }
-    mma_pair_from<T, RT, 8, COH>(arow, lda, rs, o0, o1, has1, ch0, nch, acc0, acc1);
+    mma_pair_from<T, RT, 8>(arow, lda, rs, o0, o1, has1, ch0, nch, acc0, acc1);
 #else
     if (HC > 0 && first && held && held->tag == w.p) {  // resident fragments (uniform branch)
       const int hn = nch < HC ? nch : HC;
@@ -570,9 +570,9 @@ __device__ __forceinline__ void gemm_step(const lf* __restrict__ A, int lda, con
             }
         });
       }
-      if (hn < nch) mma_pair_from<T, RT, 8, COH>(arow, lda, rs, o0, o1, has1, hn, nch, acc0, acc1);
+      if (hn < nch) mma_pair_from<T, RT, 8>(arow, lda, rs, o0, o1, has1, hn, nch, acc0, acc1);
     } else {
-      mma_pair_from<T, RT, 8, COH>(arow, lda, rs, o0, o1, has1, 0, nch, acc0, acc1);
+      mma_pair_from<T, RT, 8>(arow, lda, rs, o0, o1, has1, 0, nch, acc0, acc1);
     }
 #endif
     epi(0, nt0 * 16 + c, acc0, first);
@@ -624,7 +624,7 @@ __device__ __forceinline__ void act_pass_bwd(lf* G, int ldg, const lf* P, int ld
 
 // Forward: Y[r][n] = act(sum_k X[r][k] W[n][k] + b[n]) for n < Np (padded -> 0).
 // P (optional) keeps the pre-activation; Pg (optional) stashes rows >= pg_row0.
-template <typename T, int ROWS, bool COH = false, int HC = 0>
+template <typename T, int ROWS, int HC = 0>
 __device__ __forceinline__ void layer_fwd(const lf* X, int ldx, const AS_C LayerDev& L, const float* bias_, int act, lf* P,
                                           int ldp, lf* Y, int ldy, float* Pg_, int pg_row0, Pf<T>& pf,
                                           const GemmW& next, const Held<T, HC ? HC : 1>* held = nullptr) {
@@ -642,13 +642,13 @@ __device__ __forceinline__ void layer_fwd(const lf* X, int ldx, const AS_C Layer
   const float bpre0 = pf.b0, bpre1 = pf.b1;
 #else
   const bool hb = HC > 0 && held && held->tag == w.p;  // bias held with the fragments
-  const float bpre0 = hb ? held->b0 : ldf<COH>((const float*)bias + (n0 < N ? n0 : N - 1));
-  const float bpre1 = hb ? held->b1 : ldf<COH>((const float*)bias + (n1 < N ? n1 : N - 1));
+  const float bpre0 = hb ? held->b0 : ldf<false>((const float*)bias + (n0 < N ? n0 : N - 1));
+  const float bpre1 = hb ? held->b1 : ldf<false>((const float*)bias + (n1 < N ? n1 : N - 1));
 #endif
   // first: the wave's first tile pair, whose columns are n0 / n1 (bias preloaded)
-  gemm_step<T, ROWS, COH, HC>(X, ldx, w, pf, next, [&](int h, int n, const f32x4* acc, bool first) {
+  gemm_step<T, ROWS, HC>(X, ldx, w, pf, next, [&](int h, int n, const f32x4* acc, bool first) {
     const bool nv = n < N;
-    const float bn = first ? (h ? bpre1 : bpre0) : ldf<COH>((const float*)bias + (nv ? n : N - 1));
+    const float bn = first ? (h ? bpre1 : bpre0) : ldf<false>((const float*)bias + (nv ? n : N - 1));
 #pragma unroll
     for (int rt = 0; rt < ROWS / 16; ++rt)
 #pragma unroll
@@ -664,13 +664,13 @@ __device__ __forceinline__ void layer_fwd(const lf* X, int ldx, const AS_C Layer
 }
 
 // dX: Gout[r][k] = act'(Pprev[r][k]) * sum_n G[r][n] W[n][k]   (act_prev < 0: no act')
-template <typename T, int ROWS, bool COH = false, int HC = 0>
+template <typename T, int ROWS, int HC = 0>
 __device__ __forceinline__ void layer_bwd(const lf* G, int ldg, const AS_C LayerDev& L, const lf* Pprev, int ldp,
                                           int act_prev, lf* Gout, int ldo, Pf<T>& pf, const GemmW& next,
                                           const Held<T, HC ? HC : 1>* held = nullptr) {
   const int g = (threadIdx.x & 63) >> 4;
   const int K = L.K;
-  gemm_step<T, ROWS, COH, HC>(G, ldg, gw_bwd(L), pf, next, [&](int, int k, const f32x4* acc, bool) {
+  gemm_step<T, ROWS, HC>(G, ldg, gw_bwd(L), pf, next, [&](int, int k, const f32x4* acc, bool) {
     const bool kv = k < K;
 #pragma unroll
     for (int rt = 0; rt < ROWS / 16; ++rt)
@@ -689,9 +689,7 @@ __device__ __forceinline__ void layer_bwd(const lf* G, int ldg, const AS_C Layer
 // dst[k][col0 + r] = x[r][k] (0 for k >= K or r >= nvalid), k < Kp, where
 // x[r][k] = src[r][k] * rowscale[r] (rowscale == null: 1); with dbp != null also
 // dbp[col0 / SAC_ROWS][k] = sum_{r<nvalid} x[r][k] (k < K).
-// COH (persistent step): sc1 (write-through) stores, for consumers in other
-// workgroups of the same launch (they load with sc1 loads after a counter).
-template <typename T, int ROWS, bool COH = false>
+template <typename T, int ROWS>
 __device__ __forceinline__ void store_T(const lf* __restrict__ src, int lds_ld, int Kp, int K, void* dst_,
                                                  int Bp, int col0, int nvalid, float* dbp_,
                                                  const lf* __restrict__ rowscale = nullptr, int dbp_ld = 0) {
@@ -723,11 +721,7 @@ __device__ __forceinline__ void store_T(const lf* __restrict__ src, int lds_ld, 
     }
     if (live) {
       AS_G T* d = dst + (size_t)k * Bp + col0 + ch * 8;
-      if constexpr (COH) {
-        const uint32_t off = (uint32_t)(((size_t)k * Bp + col0 + ch * 8) * sizeof(T));
-        coh_store16<true>(dst_, off, *(const u32x4*)v);
-        if constexpr (sizeof(T) == 4) coh_store16<true>(dst_, off + 16, *(const u32x4*)(v + 4));
-      } else if constexpr (sizeof(T) == 2) {
+      if constexpr (sizeof(T) == 2) {
         *(AS_G u32x4*)d = *(const u32x4*)v;
       } else {
         *(AS_G u32x4*)d = *(const u32x4*)v;
@@ -739,10 +733,7 @@ __device__ __forceinline__ void store_T(const lf* __restrict__ src, int lds_ld, 
       for (int o = 1; o < CH; o <<= 1) s += __shfl_xor(s, o, 64);
       if (live && ch == 0 && k < K) {
         AS_G float* bp = dbp + (size_t)(col0 / SAC_ROWS) * (dbp_ld ? dbp_ld : K) + k;
-        if constexpr (COH)
-          coh_storef((float*)bp, s);
-        else
-          *bp = s;
+        *bp = s;
       }
     }
   }
@@ -753,7 +744,7 @@ __device__ __forceinline__ void store_T(const lf* __restrict__ src, int lds_ld, 
 // pre-activations into lds[o_P[l]] (stride ldp[l]).  storeXT: each layer's input
 // transposed into L.XT (ROWS must be SAC_ROWS).  after: the GEMM step that follows.
 // HELD: layers 0 and 1 start on fragments held in h0 / h1 (see Held).
-template <typename T, int ROWS, bool COH = false, bool HELD = false>
+template <typename T, int ROWS, bool HELD = false>
 __device__ __forceinline__ void mlp_forward(const AS_C NetDev& net, lf* Xb, lf* Yb, int ld, lf* Pout, lf* Yout, int ldo,
                                             const AS_C int* o_P, const AS_C int* ldp, lf* lds, bool keepP, bool storeXT, int Bp,
                                             int col0, int nvalid, Pf<T>& pf, const GemmW& after,
@@ -773,11 +764,11 @@ __device__ __forceinline__ void mlp_forward(const AS_C NetDev& net, lf* Xb, lf* 
     lf* Yl = out ? Yout : Y;
     const int ldyl = out ? ldo : ld;
     if (HELD && l == 0)
-      layer_fwd<T, ROWS, COH, 1>(X, ld, Ly, net.P + Ly.b_off, act, Pl, ldpl, Yl, ldyl, nullptr, 0, pf, next, h0);
+      layer_fwd<T, ROWS, 1>(X, ld, Ly, net.P + Ly.b_off, act, Pl, ldpl, Yl, ldyl, nullptr, 0, pf, next, h0);
     else if (HELD && l == 1)
-      layer_fwd<T, ROWS, COH, 8>(X, ld, Ly, net.P + Ly.b_off, act, Pl, ldpl, Yl, ldyl, nullptr, 0, pf, next, h1);
+      layer_fwd<T, ROWS, 8>(X, ld, Ly, net.P + Ly.b_off, act, Pl, ldpl, Yl, ldyl, nullptr, 0, pf, next, h1);
     else
-      layer_fwd<T, ROWS, COH>(X, ld, Ly, net.P + Ly.b_off, act, Pl, ldpl, Yl, ldyl, nullptr, 0, pf, next);
+      layer_fwd<T, ROWS>(X, ld, Ly, net.P + Ly.b_off, act, Pl, ldpl, Yl, ldyl, nullptr, 0, pf, next);
     __syncthreads();
     lf* t = X;
     X = Y;
@@ -790,7 +781,7 @@ __device__ __forceinline__ void mlp_forward(const AS_C NetDev& net, lf* Xb, lf* 
 // Returns the buffer (stride ld) holding d(pre-act of layer 0).
 // HELD: the output layer's and layer Lh-1's dX steps start on fragments held
 // in h0 / h1 (see Held).
-template <typename T, int ROWS, bool COH = false, bool HELD = false>
+template <typename T, int ROWS, bool HELD = false>
 __device__ __forceinline__ lf* mlp_backward(const AS_C NetDev& net, const lf* Gout, int ldo, lf* Xb, lf* Yb, int ld,
                                             const AS_C int* o_P, const AS_C int* ldp, lf* lds, bool storeGT, int Bp, int col0,
                                             int nvalid, Pf<T>& pf, const GemmW& after,
@@ -798,7 +789,7 @@ __device__ __forceinline__ lf* mlp_backward(const AS_C NetDev& net, const lf* Go
   const int Lh = net.L - 1;
   const AS_C LayerDev& Lo = net.l[Lh];
   if (storeGT) store_T<T, ROWS>(Gout, ldo, Lo.Np, Lo.N, Lo.GT, Bp, col0, nvalid, Lo.dbp);
-  layer_bwd<T, ROWS, COH, HELD ? 1 : 0>(Gout, ldo, Lo, lds + o_P[Lh - 1], ldp[Lh - 1], net.hid_act, Yb, ld, pf,
+  layer_bwd<T, ROWS, HELD ? 1 : 0>(Gout, ldo, Lo, lds + o_P[Lh - 1], ldp[Lh - 1], net.hid_act, Yb, ld, pf,
                                         Lh - 1 >= 1 ? gw_bwd(net.l[Lh - 1]) : after, (const Held<T, 1>*)h0);
   __syncthreads();
   lf* G = Yb;
@@ -808,10 +799,10 @@ __device__ __forceinline__ lf* mlp_backward(const AS_C NetDev& net, const lf* Go
     if (storeGT) store_T<T, ROWS>(G, ld, Ly.Np, Ly.N, Ly.GT, Bp, col0, nvalid, Ly.dbp);
     if (l == 0) break;
     if (HELD && l == Lh - 1)
-      layer_bwd<T, ROWS, COH, 8>(G, ld, Ly, lds + o_P[l - 1], ldp[l - 1], net.hid_act, Gn, ld, pf,
+      layer_bwd<T, ROWS, 8>(G, ld, Ly, lds + o_P[l - 1], ldp[l - 1], net.hid_act, Gn, ld, pf,
                                  l - 1 >= 1 ? gw_bwd(net.l[l - 1]) : after, h1);
     else
-      layer_bwd<T, ROWS, COH>(G, ld, Ly, lds + o_P[l - 1], ldp[l - 1], net.hid_act, Gn, ld, pf,
+      layer_bwd<T, ROWS>(G, ld, Ly, lds + o_P[l - 1], ldp[l - 1], net.hid_act, Gn, ld, pf,
                        l - 1 >= 1 ? gw_bwd(net.l[l - 1]) : after);
     __syncthreads();
     lf* t = G;
@@ -831,15 +822,15 @@ __device__ __forceinline__ float fmin_nan(float a, float b) { return (a != a) ? 
 // for a seed of 1 per row; writes U_l = d(pre-act of hidden layer l) for every
 // hidden layer into lds + E.o_P2[l] (stride E.ldp2[l]).  Pre-activations are in
 // the E.o_P1 buffers (critic forward with keepP).
-template <typename T, int ROWS, bool COH = false>
+template <typename T, int ROWS>
 __device__ __forceinline__ void critic_unit_backward(const AS_C EngineDev& E, const AS_C NetDev& net, const lf* Gout, int ldo,
                                                      lf* lds, Pf<T>& pf) {
   const int Lh = net.L - 1;
-  layer_bwd<T, ROWS, COH>(Gout, ldo, net.l[Lh], lds + E.o_P1[Lh - 1], E.ldp1[Lh - 1], net.hid_act, lds + E.o_P2[Lh - 1],
+  layer_bwd<T, ROWS>(Gout, ldo, net.l[Lh], lds + E.o_P1[Lh - 1], E.ldp1[Lh - 1], net.hid_act, lds + E.o_P2[Lh - 1],
                      E.ldp2[Lh - 1], pf, Lh - 1 >= 1 ? gw_bwd(net.l[Lh - 1]) : gw_none());
   __syncthreads();
   for (int l = Lh - 1; l >= 1; --l) {
-    layer_bwd<T, ROWS, COH>(lds + E.o_P2[l], E.ldp2[l], net.l[l], lds + E.o_P1[l - 1], E.ldp1[l - 1], net.hid_act,
+    layer_bwd<T, ROWS>(lds + E.o_P2[l], E.ldp2[l], net.l[l], lds + E.o_P1[l - 1], E.ldp1[l - 1], net.hid_act,
                        lds + E.o_P2[l - 1], E.ldp2[l - 1], pf, l - 1 >= 1 ? gw_bwd(net.l[l - 1]) : gw_none());
     __syncthreads();
   }
@@ -913,8 +904,9 @@ __device__ __forceinline__ void dw_adam_tile(const AS_C EngineDev& E, const Tile
   static_assert(PPO >= 1 && (32 * (SAC_UPD_BCH / EPR)) % UT == 0, "whole pieces per thread");
   const int rstep = ns * SAC_UPD_BCH;          // batch columns per round
   u32x4 rg[MAXS][GS + 1][PPO];                 // [slot][dY part 0..GS-1, then X][piece]
-  const AS_G float* const seedp = sizeof(T) == 4 ? GPC(float, td.seed) : nullptr;  // uniform
-  f32x4 sdr[sizeof(T) == 4 ? MAXS : 1][PPO];   // the seeds of this thread's dY pieces
+  const AS_G float* const seedp = GPC(float, td.seed);  // uniform
+  constexpr int SQ = EPR / 4;                  // seed f32x4 per 16-B piece (fp32 1, bf16 2)
+  f32x4 sdr[MAXS][PPO][SQ];                    // the seeds of this thread's dY pieces
   // the operands' bases as separate values: a per-lane choice between two
   // descriptor fields was compiled into a per-lane LOAD of the chosen field and a
   // wait before every piece (the pieces' loads ran one round trip after another)
@@ -938,8 +930,9 @@ __device__ __forceinline__ void dw_adam_tile(const AS_C EngineDev& E, const Tile
           const int row = i / per_row, pc = i % per_row;
           const AS_G T* src = op < GS ? gsrc + op * goff + (size_t)row * ldg : xsrc + (size_t)row * ldx;
           if (i < 32 * per_row) rg[sl][op][pi] = *(const AS_G u32x4*)(src + b0 + pc * EPR);
-          if constexpr (sizeof(T) == 4)
-            if (op == 0 && seedp && i < 32 * per_row) sdr[sl][pi] = *(const AS_G f32x4*)(seedp + b0 + pc * EPR);
+          if (op == 0 && seedp && i < 32 * per_row)
+#pragma unroll
+            for (int q = 0; q < SQ; ++q) sdr[sl][pi][q] = *(const AS_G f32x4*)(seedp + b0 + pc * EPR + 4 * q);
         }
     }
   };
@@ -1011,31 +1004,35 @@ __device__ __forceinline__ void dw_adam_tile(const AS_C EngineDev& E, const Tile
             const int i = tid + pi * UT;
             const int row = i / per_row + 32 * op, pc = i % per_row;
             u32x4 v = rg[sl][op ? GS : 0][pi];
-            if constexpr (GS > 1)
-              if (op == 0) {  // dY: the parts' partials added in part order (fp32)
-                if constexpr (sizeof(T) == 4) {
+            if constexpr (sizeof(T) == 4) {
+              if constexpr (GS > 1)
+                if (op == 0) {  // dY: the parts' partials added in part order
                   f32x4 a = __builtin_bit_cast(f32x4, v);
 #pragma unroll
                   for (int q = 1; q < GS; ++q) a += __builtin_bit_cast(f32x4, rg[sl][q][pi]);
                   v = __builtin_bit_cast(u32x4, a);
-                } else {  // bf16: added in fp32, rounded to bf16 once
-                  bf16x8 h = __builtin_bit_cast(bf16x8, v);
-                  float a[8];
-#pragma unroll
-                  for (int e = 0; e < 8; ++e) a[e] = (float)h[e];
-#pragma unroll
-                  for (int q = 1; q < GS; ++q) {
-                    const bf16x8 hq = __builtin_bit_cast(bf16x8, rg[sl][q][pi]);
-#pragma unroll
-                    for (int e = 0; e < 8; ++e) a[e] += (float)hq[e];
-                  }
-#pragma unroll
-                  for (int e = 0; e < 8; ++e) h[e] = (bf16)a[e];
-                  v = __builtin_bit_cast(u32x4, h);
                 }
+              if (op == 0 && seedp) v = __builtin_bit_cast(u32x4, __builtin_bit_cast(f32x4, v) * sdr[sl][pi][0]);
+            } else if (op == 0 && (GS > 1 || seedp)) {
+              // bf16 dY: the parts added in fp32 (part order), scaled by the
+              // rows' seeds in fp32, rounded to bf16 once
+              bf16x8 h = __builtin_bit_cast(bf16x8, v);
+              float a[8];
+#pragma unroll
+              for (int e = 0; e < 8; ++e) a[e] = (float)h[e];
+#pragma unroll
+              for (int q = 1; q < GS; ++q) {
+                const bf16x8 hq = __builtin_bit_cast(bf16x8, rg[sl][q][pi]);
+#pragma unroll
+                for (int e = 0; e < 8; ++e) a[e] += (float)hq[e];
               }
-            if constexpr (sizeof(T) == 4)
-              if (op == 0 && seedp) v = __builtin_bit_cast(u32x4, __builtin_bit_cast(f32x4, v) * sdr[sl][pi]);
+              if (seedp)
+#pragma unroll
+                for (int e = 0; e < 8; ++e) a[e] *= sdr[sl][pi][e >> 2][e & 3];
+#pragma unroll
+              for (int e = 0; e < 8; ++e) h[e] = (bf16)a[e];
+              v = __builtin_bit_cast(u32x4, h);
+            }
             if (i < 32 * per_row) *(AS_L u32x4*)(stage + sl * slot_el + row * lds_row + pc * EPR) = v;
           }
         issue(r0 + rstep, slc);
@@ -1799,11 +1796,11 @@ __device__ __forceinline__ void target_critic_body(const EngineDev* __restrict__
       const int ldl = out ? ldo : ld;
       const GemmW nx = out ? gw_fwd(E.net[NET_Q1T].l[0]) : gw_fwd(pi.l[l + 1]);
       if (l == 0)
-        layer_fwd<T, ROWS, false, 1>(X, ld, Ly, pi.P + Ly.b_off, act_l, Pl, ldl, Yl, ldl, stash, a0, pf, nx, &ph0);
+        layer_fwd<T, ROWS, 1>(X, ld, Ly, pi.P + Ly.b_off, act_l, Pl, ldl, Yl, ldl, stash, a0, pf, nx, &ph0);
       else if (l == 1)
-        layer_fwd<T, ROWS, false, 8>(X, ld, Ly, pi.P + Ly.b_off, act_l, Pl, ldl, Yl, ldl, stash, a0, pf, nx, &ph1);
+        layer_fwd<T, ROWS, 8>(X, ld, Ly, pi.P + Ly.b_off, act_l, Pl, ldl, Yl, ldl, stash, a0, pf, nx, &ph1);
       else
-        layer_fwd<T, ROWS, false>(X, ld, Ly, pi.P + Ly.b_off, act_l, Pl, ldl, Yl, ldl, stash, a0, pf, nx);
+        layer_fwd<T, ROWS>(X, ld, Ly, pi.P + Ly.b_off, act_l, Pl, ldl, Yl, ldl, stash, a0, pf, nx);
       __syncthreads();
       STAMP(2 + l);
       lf* t = X;
@@ -1892,7 +1889,7 @@ __device__ __forceinline__ void target_critic_body(const EngineDev* __restrict__
         Xb[r * ld + k] = k < O ? s2B[r * O + k] : (k < O + A ? a2B[r * A + (k - O)] : 0.f);
       }
       __syncthreads();
-      mlp_forward<T, R, false, ROLES>(q, Xb, Yb, ld, outP, outB, ldo, E.o_P1, E.ldp1, lds, false, false, Bp, r0,
+      mlp_forward<T, R, ROLES>(q, Xb, Yb, ld, outP, outB, ldo, E.o_P1, E.ldp1, lds, false, false, Bp, r0,
                                       nvalid, pf, gw_fwd(E.net[t ? NET_Q1 : NET_Q2T].l[0]), &qh0, &qh1);
       if (tid < R) {
         qtB[t * R + tid] = outB[tid * ldo];
@@ -2088,7 +2085,7 @@ __device__ __forceinline__ void actor_body(const EngineDev* __restrict__ Ep, int
         Xb[r * ld + k] = k < O ? sB[r * O + k] : (k < O + A ? aB[r * A + (k - O)] : 0.f);
       }
       __syncthreads();
-      mlp_forward<T, R, false, ROLES>(q, Xb, Yb, ld, qi ? outP2 : outP1, qi ? out2 : out1, ldo,
+      mlp_forward<T, R, ROLES>(q, Xb, Yb, ld, qi ? outP2 : outP1, qi ? out2 : out1, ldo,
                                        qi ? E.o_P2 : E.o_P1, qi ? E.ldp2 : E.ldp1, lds, true, false, Bp, r0, nvalid, pf,
                                        ROLES ? gw_bwd(q.l[q.L - 1])
                                        : qi ? gw_bwd(E.net[NET_Q1].l[E.net[NET_Q1].L - 1]) : gw_fwd(E.net[NET_Q2].l[0]),
@@ -2131,10 +2128,10 @@ __device__ __forceinline__ void actor_body(const EngineDev* __restrict__ Ep, int
     // ---- d a~ through the critics: dX of layer 0, action columns
     for (int qi = q_lo; qi < q_hi; ++qi) {
       const AS_C NetDev& q = E.net[NET_Q1 + qi];
-      lf* G0 = mlp_backward<T, R, false>(q, qi ? g2B : g1B, ldo, Xb, Yb, ld, qi ? E.o_P2 : E.o_P1, qi ? E.ldp2 : E.ldp1,
+      lf* G0 = mlp_backward<T, R>(q, qi ? g2B : g1B, ldo, Xb, Yb, ld, qi ? E.o_P2 : E.o_P1, qi ? E.ldp2 : E.ldp1,
                                   lds, false, Bp, r0, nvalid, pf, gw_bwd(q.l[0]));
       lf* Gx = (G0 == Xb) ? Yb : Xb;
-      layer_bwd<T, R, false>(G0, ld, q.l[0], nullptr, 0, -1, Gx, ld, pf,
+      layer_bwd<T, R>(G0, ld, q.l[0], nullptr, 0, -1, Gx, ld, pf,
                       qi ? gw_bwd(pi.l[pi.L - 1]) : gw_bwd(E.net[NET_Q2].l[E.net[NET_Q2].L - 1]));
       __syncthreads();
       if (ROLES) {
@@ -2231,7 +2228,7 @@ __device__ __forceinline__ void actor_body(const EngineDev* __restrict__ Ep, int
     for (int i = tid; i < R * pad; i += SAC_THREADS) goutB[(i / pad) * ldo + 2 * A + i % pad] = 0.f;
   }
   __syncthreads();
-  mlp_backward<T, R, false, true>(pi, goutB, ldo, Xb, Yb, ld, E.o_P1, E.ldp1, lds, true, Bp, r0, nvalid, pf, gw_none(),
+  mlp_backward<T, R, true>(pi, goutB, ldo, Xb, Yb, ld, E.o_P1, E.ldp1, lds, true, Bp, r0, nvalid, pf, gw_none(),
                                   &bh0, &bh1);
   STAMP(35);
 }

@@ -345,7 +345,6 @@ __device__ __forceinline__ void target_critic_split_body(const EngineDev* __rest
   lf* dB = lds + E.o_d;
   lf* epsB = lds + E.o_et;
   lf* lpB = lds + E.o_lp;
-  lf* qtB = lds + E.o_qt;
   AS_L int64_t* slotB = (AS_L int64_t*)(lds + E.o_slot);
   AS_G float* stats = GP(float, E.stats);
 
@@ -536,10 +535,10 @@ __device__ __forceinline__ void target_critic_split_body(const EngineDev* __rest
 
   // ---- layer 0 (full) and layer 1 (this half) forward: H0, H1 in LDS; P0 / P1 kept
   auto no_hook = [] {};
-  auto forward01 = [&](bool keepP, bool stXT, bool pi_actor, auto&& after_l1) {
-    // layer 0: X [R][Kp0] -> P0 / H0 [R][H]
+  auto forward01 = [&](bool keepP, bool stXT, bool pi_actor, auto&& after_l1, bool l0_done = false) {
+    // layer 0: X [R][Kp0] -> P0 / H0 [R][H] (l0_done: the caller computed H0)
     const int act = net.hid_act;
-    gemm_hs<T, 2, HC0, false>(Xb, ld, w0, &h0, [&](int j, int col, const f32x4& acc) {
+    if (!l0_done) gemm_hs<T, 2, HC0, false>(Xb, ld, w0, &h0, [&](int j, int col, const f32x4& acc) {
       const bool nv = col < L0.N;
       const float bn = h0.b[j];
 #pragma unroll
@@ -550,8 +549,10 @@ __device__ __forceinline__ void target_critic_split_body(const EngineDev* __rest
         H0[r * ld + col] = act == ACT_RELU ? (p > 0.f ? p : 0.f) : p;
       }
     });
-    if (act != ACT_RELU && act != ACT_ID) act_pass_fwd<R>(H0, ld, L0.Np >> 4, act);
-    __syncthreads();
+    if (!l0_done) {
+      if (act != ACT_RELU && act != ACT_ID) act_pass_fwd<R>(H0, ld, L0.Np >> 4, act);
+      __syncthreads();
+    }
     if (pi_actor && h == 0) {  // pi's layer-0 pre-activations for phase C's relu masks
       float* ps = L0.pstash + (size_t)r0 * L0.Np;
       for (int i = tid; i < R * L0.Np; i += SAC_THREADS) st_f<false>(ps + i, P0[(i / L0.Np) * ldp0 + i % L0.Np]);
@@ -627,18 +628,80 @@ __device__ __forceinline__ void target_critic_split_body(const EngineDev* __rest
     // ---- target critic t (agent.py:195-211): a~', log pi' from pi(s')'s two partials
     const int t = role - 1;
     if (sizeof(T) == 4) ks_issue<T, KsHeld<T>::MAXC, false>(kh2, w2n);
-    head(gs_at(E, GS_PI, rbi, 0), nullptr, true, a2B, lpB, false);
-    if (t == 0 && h == 0 && tid < R) gran_put(gs_at(E, GS_LP, rbi, 0) + tid, lpB[tid], ep);
-    STAMP(7);
-    build_x(s2B, a2B, A);
-    forward01(false, false, false, no_hook);
+    // Layer 0 over the s' columns runs BEFORE the pi(s') hand-off (round 5,
+    // VERDICT r04 item 2c): only the chunks holding a~' columns are left for
+    // after the head.  Chunks [0, O / KC) are s' only; a chunk that holds both
+    // (O % KC != 0: bf16 at C2, one 32-deep chunk) is multiplied once with its
+    // a~' columns still 0 and once, after the head, with its s' columns
+    // zeroed.  Chunk c goes to accumulator c & 1 as in gemm_hs, so with no
+    // shared chunk (fp32 C2 / C4, bf16 C4) the result is the same bits.
+    const int Kp0 = L0.Kp, nch0 = Kp0 / KC;
+    const bool early0 = nch0 <= HC0;  // every layer-0 chunk held (C2, C4): else the plain path
+    if (early0) {
+      build_x(s2B, a2B, 0);  // [s', 0]
+      const int cs = O / KC, cb = (O + KC - 1) / KC;  // s'-only chunks; chunks with any s' column
+      const int lane = tid & 63, wave = wave_id(), c = lane & 15, g = lane >> 4;
+      const lf* arow = Xb + c * ld + g * MM<T>::KL;
+      f32x4 acc[2][2];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[j][0] = acc[j][1] = (f32x4){0.f, 0.f, 0.f, 0.f};
+      auto chunks = [&](int c0, int c1) __attribute__((always_inline)) {
+        static_for<HC0>([&](auto uc) {
+          constexpr int u = decltype(uc)::value;
+          if (u >= c0 && u < c1) {  // uniform
+            const typename MM<T>::Frag a = MM<T>::from_lds(arow + u * KC);
+            static_for<2>([&](auto jc) {
+              constexpr int j = decltype(jc)::value;
+              if (wave + j * SAC_NW < w0.NT) MM<T>::mma(acc[j][u & 1], a, h0.f[j][u]);
+            });
+          }
+        });
+      };
+      chunks(0, cb);
+      __syncthreads();  // every wave has read the shared chunk's s' columns
+      if (cb > cs)  // the shared chunk keeps only its a~' columns for the second pass
+        for (int i = tid; i < R * KC; i += SAC_THREADS) {
+          const int r = i / KC, k = cs * KC + i % KC;
+          if (k < O) Xb[r * ld + k] = 0.f;
+        }
+      head(gs_at(E, GS_PI, rbi, 0), nullptr, true, a2B, lpB, false);
+      if (t == 0 && h == 0 && tid < R) gran_put(gs_at(E, GS_LP, rbi, 0) + tid, lpB[tid], ep);
+      STAMP(7);
+      for (int i = tid; i < R * A; i += SAC_THREADS) Xb[(i / A) * ld + O + i % A] = a2B[i];
+      __syncthreads();
+      chunks(cs, nch0);
+      const int act = net.hid_act;
+      static_for<2>([&](auto jc) {
+        constexpr int j = decltype(jc)::value;
+        const int tt = wave + j * SAC_NW;
+        if (tt < w0.NT) {
+          const int col = tt * 16 + c;
+          const bool nv = col < L0.N;
+          const f32x4 sum = acc[j][0] + acc[j][1];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const float p = nv ? sum[i] + h0.b[j] : 0.f;
+            H0[(g * 4 + i) * ld + col] = act == ACT_RELU ? (p > 0.f ? p : 0.f) : p;
+          }
+        }
+      });
+      if (act != ACT_RELU && act != ACT_ID) act_pass_fwd<R>(H0, ld, L0.Np >> 4, act);
+      __syncthreads();
+      forward01(false, false, false, no_hook, true);
+    } else {
+      head(gs_at(E, GS_PI, rbi, 0), nullptr, true, a2B, lpB, false);
+      if (t == 0 && h == 0 && tid < R) gran_put(gs_at(E, GS_LP, rbi, 0) + tid, lpB[tid], ep);
+      STAMP(7);
+      build_x(s2B, a2B, A);
+      forward01(false, false, false, no_hook);
+    }
     if (tid < R) gran_put(gs_at(E, t ? GS_QT2 : GS_QT1, rbi, h) + tid, outB[tid * ldo], ep);
     STAMP(9);
-    if (sizeof(T) == 4 && t == 0 && h == 0 && tid < 64) {
-      // fp32: this half (Qt1, half 0) computes the row tile's targets y and both
+    if (t == 0 && h == 0 && tid < 64) {
+      // this half (Qt1, half 0) computes the row tile's targets y and both
       // critics' seeds dL/dq = 2 (q - y) / B and loss partials (agent.py:
-      // 195-236; the critic roles, which used to wait for y, store unit-seed
-      // operands and finish).  Same float operations as the critics' code below.
+      // 195-236; the critic roles store unit-seed operands and finish without
+      // waiting for y: phase B applies the seeds).
       float sq[2] = {0.f, 0.f};
       if (tid < R) {
         const int b = r0 + tid;
@@ -719,70 +782,22 @@ __device__ __forceinline__ void target_critic_split_body(const EngineDev* __rest
       __syncthreads();
     }
     STAMP(16);
-    if constexpr (sizeof(T) == 4) {
-      // fp32: the role does not wait for y.  It stores every layer's UNIT-seed
-      // dY^T (layer 2's: the indicator row); phase B scales each batch column
-      // by the seed the first target-critic half computed (E.seedq) and sums
-      // the bias gradients from the scaled rows.
-      store_T<T, R>(U1, ldu1, HH, HH, (T*)L1.GT + (size_t)h * HH * Bp, Bp, r0, nvalid, nullptr);
-      store_T<T, R>(Xb, ld, L0.Np, L0.N, L0.GT, 2 * Bp, h * Bp + r0, nvalid, nullptr);
-      if (h == 0) {
-        lf* g2 = outB;  // this half's q partial went out as a granule above
-        for (int i = tid; i < R * 32; i += SAC_THREADS) g2[(i / 32) * ldo + i % 32] = (i % 32) == 0 ? 1.f : 0.f;
-        __syncthreads();
-        store_T<T, R>(g2, ldo, L2.Np, L2.N, L2.GT, Bp, r0, nvalid, nullptr);
-      }
-      STAMP(15);
-    } else {
-      if (tid < 64) {  // wave 0: q, y, loss partial, seed dL/dq = 2(q - y)/B  (mse_loss backward)
-        float sq = 0.f;
-        if (tid < R) {
-          const int b = r0 + tid;
-          const bool v = tid < nvalid;
-          const float b2 = ldf<false>(L2.bias);
-          const AS_C NetDev& t1 = E.net[NET_Q1T];
-          const AS_C NetDev& t2 = E.net[NET_Q2T];
-          const float bt1 = ldf<false>(t1.l[2].bias), bt2 = ldf<false>(t2.l[2].bias);  // before the poll
-          const float mine = outB[tid * ldo];
-          // every granule this row needs, polled together: peer half's q partial,
-          // both target critics' two halves, log pi(a'|s')
-          const AS_G uint64_t* gg[6] = {gs_at(E, qi ? GS_QA2 : GS_QA1, rbi, 1 - h) + tid,
-                                        gs_at(E, GS_QT1, rbi, 0) + tid, gs_at(E, GS_QT1, rbi, 1) + tid,
-                                        gs_at(E, GS_QT2, rbi, 0) + tid, gs_at(E, GS_QT2, rbi, 1) + tid,
-                                        gs_at(E, GS_LP, rbi, 0) + tid};
-          float gv[6];
-          gran_getn<6>(E, gg, ep, gv);
-          const float peer = gv[0];
-          const float qpre = (h == 0 ? mine + peer : peer + mine) + b2;
-          const float q = net.out_act == ACT_ID ? qpre : act_fwd(net.out_act, qpre);
-          const float q1tp = gv[1] + gv[2] + bt1;
-          const float q2tp = gv[3] + gv[4] + bt2;
-          const float q1t = t1.out_act == ACT_ID ? q1tp : act_fwd(t1.out_act, q1tp);
-          const float q2t = t2.out_act == ACT_ID ? q2tp : act_fwd(t2.out_act, q2tp);
-          const float lp2 = gv[5];
-          const float y = rB[tid] + (E.gamma * (1.f - dB[tid])) * (fmin_nan(q1t, q2t) - alpha32 * lp2);
-          if (qi == 0 && h == 0 && b < B) stats[4 + b] = y;
-          const float d = q - y;
-          sq = v ? d * d : 0.f;
-          float seed = v ? (2.0f / (float)B) * d : 0.f;
-          if (net.out_act != ACT_ID) seed = act_bwd(net.out_act, qpre, seed);
-          qtB[tid] = seed;
-        }
-        sq = wave_sum(sq);
-        if (tid == 0 && h == 0) st_f<false>(E.lossp + (par * E.nrt + rbi) * 4 + qi, sq);
-      }
+    // the role does not wait for y.  It stores every layer's UNIT-seed dY^T
+    // (layer 2's: the indicator row); phase B scales each batch column by the
+    // seed the first target-critic half computed (E.seedq) and sums the bias
+    // gradients from the scaled rows.  (bf16: the unit dY is rounded to bf16
+    // here and the scaled value once more in phase B, within the bf16 mode's
+    // tolerances; round 5, VERDICT r04 item 2a -- before, the bf16 critics
+    // waited for y and stored seed-scaled rows.)
+    store_T<T, R>(U1, ldu1, HH, HH, (T*)L1.GT + (size_t)h * HH * Bp, Bp, r0, nvalid, nullptr);
+    store_T<T, R>(Xb, ld, L0.Np, L0.N, L0.GT, 2 * Bp, h * Bp + r0, nvalid, nullptr);
+    if (h == 0) {
+      lf* g2 = outB;  // this half's q partial went out as a granule above
+      for (int i = tid; i < R * 32; i += SAC_THREADS) g2[(i / 32) * ldo + i % 32] = (i % 32) == 0 ? 1.f : 0.f;
       __syncthreads();
-      STAMP(15);
-      // dY^T of every layer (seed x unit dY) + bias partials for phase B
-      if (h == 0) {  // layer 2: dY2 = seed (N = 1)
-        lf* g2 = outB;
-        for (int i = tid; i < R * 32; i += SAC_THREADS) g2[(i / 32) * ldo + i % 32] = (i % 32) == 0 ? 1.f : 0.f;
-        __syncthreads();
-        store_T<T, R>(g2, ldo, L2.Np, L2.N, L2.GT, Bp, r0, nvalid, L2.dbp, qtB);
-      }
-      store_T<T, R>(U1, ldu1, HH, HH, (T*)L1.GT + (size_t)h * HH * Bp, Bp, r0, nvalid, L1.dbp ? L1.dbp + h * HH : nullptr, qtB, L1.N);
-      store_T<T, R>(Xb, ld, L0.Np, L0.N, L0.GT, 2 * Bp, h * Bp + r0, nvalid, L0.dbp, qtB);
+      store_T<T, R>(g2, ldo, L2.Np, L2.N, L2.GT, Bp, r0, nvalid, nullptr);
     }
+    STAMP(15);
     STAMP(11 + 2 * qi);
   }
 }

@@ -35,7 +35,7 @@ def short(name: str) -> str:
 
 
 def one_db(pattern: str) -> sqlite3.Connection:
-    dbs = sorted(glob.glob(pattern))
+    dbs = sorted(glob.glob(pattern, recursive=True))
     if not dbs:
         raise SystemExit(f"no database matches {pattern}")
     return sqlite3.connect(dbs[-1])
@@ -65,7 +65,7 @@ def main():
     dst = a.dst
     os.makedirs(dst, exist_ok=True)
 
-    kt = one_db(os.path.join(src, "kt", "*.db"))
+    kt = one_db(os.path.join(src, "kt", "**", "*.db"))
     rows = list(kt.execute("select name, total_calls, total_duration, average, percentage from top_kernels"))
     with open(os.path.join(dst, f"{rnd}_kernel_stats{tag}.csv"), "w", newline="") as f:
         w = csv.writer(f)
@@ -73,8 +73,8 @@ def main():
         for name, calls, tot, avg, pct in rows:
             w.writerow([short(name), calls, round(tot, 3), round(avg, 3), round(pct, 3)])
 
-    fetch = counter_avg(one_db(os.path.join(src, "fetch", "*.db")), "FETCH_SIZE")
-    write = counter_avg(one_db(os.path.join(src, "write", "*.db")), "WRITE_SIZE")
+    fetch = counter_avg(one_db(os.path.join(src, "fetch", "**", "*.db")), "FETCH_SIZE")
+    write = counter_avg(one_db(os.path.join(src, "write", "**", "*.db")), "WRITE_SIZE")
     durations = {short(n): avg for n, _, _, avg, _ in rows}
     summary = {"config": a.config, "precision": a.precision,
                "source": "rocprofv3 --kernel-trace --stats; separate --pmc FETCH_SIZE / --pmc WRITE_SIZE passes",
