@@ -193,20 +193,32 @@ struct Feistel {
   uint32_t half, mask;
 };
 
-__host__ __device__ inline Feistel feistel_make(uint64_t seed, uint64_t step, int64_t size) {
+// The round keys depend on (seed, step) only, so a launch whose step is known on
+// the host takes them as kernel arguments (FeistelKeys) instead of evaluating two
+// Philox blocks per lane; the width depends on the device-side buffer size.
+struct FeistelKeys {
+  uint32_t k[6];
+};
+__host__ __device__ inline FeistelKeys feistel_keys(uint64_t seed, uint64_t step) {
+  uint32_t c[4] = {(uint32_t)step, (uint32_t)(step >> 32), 0xFFFFFFFFu, 0x5A3F0001u};
+  philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+  uint32_t d[4] = {(uint32_t)step, (uint32_t)(step >> 32), 0xFFFFFFFFu, 0x5A3F0002u};
+  philox4x32_10(d, (uint32_t)seed, (uint32_t)(seed >> 32));
+  return FeistelKeys{{c[0], c[1], c[2], c[3], d[0], d[1]}};
+}
+__host__ __device__ inline Feistel feistel_from_keys(const FeistelKeys& k, int64_t size) {
   Feistel f;
   uint32_t bits = 2;
   while (bits < 62 && ((int64_t)1 << bits) < size) ++bits;
   if (bits & 1) ++bits;
   f.half = bits / 2;
   f.mask = (f.half >= 32) ? 0xFFFFFFFFu : ((1u << f.half) - 1u);
-  uint32_t c[4] = {(uint32_t)step, (uint32_t)(step >> 32), 0xFFFFFFFFu, 0x5A3F0001u};
-  philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
-  uint32_t d[4] = {(uint32_t)step, (uint32_t)(step >> 32), 0xFFFFFFFFu, 0x5A3F0002u};
-  philox4x32_10(d, (uint32_t)seed, (uint32_t)(seed >> 32));
-  f.key[0] = c[0]; f.key[1] = c[1]; f.key[2] = c[2]; f.key[3] = c[3];
-  f.key[4] = d[0]; f.key[5] = d[1];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) f.key[i] = k.k[i];
   return f;
+}
+__host__ __device__ inline Feistel feistel_make(uint64_t seed, uint64_t step, int64_t size) {
+  return feistel_from_keys(feistel_keys(seed, step), size);
 }
 
 __host__ __device__ inline uint64_t feistel_perm(const Feistel& f, uint64_t x) {

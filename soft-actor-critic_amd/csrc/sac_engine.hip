@@ -133,7 +133,7 @@ __device__ __forceinline__ void gather_field(const float* __restrict__ src, int 
 // iteration (piece = lane % P).
 template <bool SAMPLE>
 __global__ void __launch_bounds__(256) replay_gather_records_kernel(
-    sac_replay rb, const int32_t* __restrict__ idx, int B, uint64_t seed, uint64_t step, int32_t* __restrict__ idx_out,
+    sac_replay rb, const int32_t* __restrict__ idx, int B, FeistelKeys fk, int32_t* __restrict__ idx_out,
     float* __restrict__ s, float* __restrict__ a, float* __restrict__ r, float* __restrict__ s2, float* __restrict__ d,
     int rpw) {
   // rpw rows per wave (64, or 16 for smaller batches: 4x the waves in flight)
@@ -147,7 +147,7 @@ __global__ void __launch_bounds__(256) replay_gather_records_kernel(
   if (lane < nrow) {
     int64_t li;
     if (SAMPLE) {
-      const Feistel f = feistel_make(seed, step, size);
+      const Feistel f = feistel_from_keys(fk, size);
       li = feistel_sample(f, b0 + lane, size);
       if (idx_out) idx_out[b0 + lane] = (int32_t)li;
     } else {
@@ -215,7 +215,7 @@ static bool standard_records(const sac_replay* rb) {
 
 template <bool SAMPLE>
 __global__ void __launch_bounds__(256) replay_gather_kernel(sac_replay rb, const int32_t* __restrict__ idx, int B,
-                                                            uint64_t seed, uint64_t step, int32_t* __restrict__ idx_out,
+                                                            FeistelKeys fk, int32_t* __restrict__ idx_out,
                                                             float* __restrict__ s, float* __restrict__ a,
                                                             float* __restrict__ r, float* __restrict__ s2,
                                                             float* __restrict__ d) {
@@ -229,7 +229,7 @@ __global__ void __launch_bounds__(256) replay_gather_kernel(sac_replay rb, const
   if (lane < nrow) {
     int64_t li;
     if (SAMPLE) {
-      const Feistel f = feistel_make(seed, step, size);
+      const Feistel f = feistel_from_keys(fk, size);
       li = feistel_sample(f, b0 + lane, size);
       if (idx_out) idx_out[b0 + lane] = (int32_t)li;
     } else {
@@ -280,10 +280,9 @@ __global__ void eps_draw_kernel(uint64_t seed, uint64_t step, int B, int A, floa
   }
 }
 
-__global__ void replay_sample_kernel(const int64_t* __restrict__ state, int B, uint64_t seed, uint64_t step,
-                                     int32_t* __restrict__ out) {
+__global__ void replay_sample_kernel(const int64_t* __restrict__ state, int B, FeistelKeys fk, int32_t* __restrict__ out) {
   const int64_t size = state[0];
-  const Feistel f = feistel_make(seed, step, size);
+  const Feistel f = feistel_from_keys(fk, size);
   for (int b = blockIdx.x * blockDim.x + threadIdx.x; b < B; b += gridDim.x * blockDim.x)
     out[b] = (int32_t)feistel_sample(f, b, size);
 }
@@ -1540,9 +1539,9 @@ int sac_replay_gather(const sac_replay* rb, const int32_t* logical_idx, int32_t 
   const int rpw = gather_rpw(batch);
   if (standard_records(rb))
     replay_gather_records_kernel<false><<<(batch + 4 * rpw - 1) / (4 * rpw), 256, 0, (hipStream_t)stream>>>(
-        *rb, logical_idx, batch, 0, 0, nullptr, s, a, r, s2, d, rpw);
+        *rb, logical_idx, batch, FeistelKeys{}, nullptr, s, a, r, s2, d, rpw);
   else
-    replay_gather_kernel<false><<<blocks, 256, 0, (hipStream_t)stream>>>(*rb, logical_idx, batch, 0, 0, nullptr, s,
+    replay_gather_kernel<false><<<blocks, 256, 0, (hipStream_t)stream>>>(*rb, logical_idx, batch, FeistelKeys{}, nullptr, s,
                                                                          a, r, s2, d);
   HIPCHK(hipGetLastError());
   return SAC_OK;
@@ -1555,9 +1554,9 @@ int sac_replay_sample_gather(const sac_replay* rb, int32_t batch, uint64_t seed,
   const int rpw = gather_rpw(batch);
   if (standard_records(rb))
     replay_gather_records_kernel<true><<<(batch + 4 * rpw - 1) / (4 * rpw), 256, 0, (hipStream_t)stream>>>(
-        *rb, nullptr, batch, seed, step, idx_out, s, a, r, s2, d, rpw);
+        *rb, nullptr, batch, feistel_keys(seed, step), idx_out, s, a, r, s2, d, rpw);
   else
-    replay_gather_kernel<true><<<blocks, 256, 0, (hipStream_t)stream>>>(*rb, nullptr, batch, seed, step, idx_out, s,
+    replay_gather_kernel<true><<<blocks, 256, 0, (hipStream_t)stream>>>(*rb, nullptr, batch, feistel_keys(seed, step), idx_out, s,
                                                                         a, r, s2, d);
   HIPCHK(hipGetLastError());
   return SAC_OK;
@@ -1587,7 +1586,7 @@ int sac_replay_sample_indices(const sac_replay* rb, int32_t batch, uint64_t seed
                               void* stream) {
   if (!rb || !out || batch < 1) return fail(SAC_E_INVALID, "bad sample arguments");
   const int blocks = std::min(4096, (batch + 255) / 256);
-  replay_sample_kernel<<<blocks, 256, 0, (hipStream_t)stream>>>(rb->state, batch, seed, step, out);
+  replay_sample_kernel<<<blocks, 256, 0, (hipStream_t)stream>>>(rb->state, batch, feistel_keys(seed, step), out);
   HIPCHK(hipGetLastError());
   return SAC_OK;
 }

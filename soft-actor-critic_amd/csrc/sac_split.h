@@ -553,7 +553,9 @@ __device__ __forceinline__ void target_critic_split_body(const EngineDev* __rest
       if (act != ACT_RELU && act != ACT_ID) act_pass_fwd<R>(H0, ld, L0.Np >> 4, act);
       __syncthreads();
     }
-    if (pi_actor && h == 0) {  // pi's layer-0 pre-activations for phase C's relu masks
+    // pi's pre-activations for phase C's backward: only for a non-ReLU hidden
+    // activation (a ReLU mask is read back from the next layer's stashed X^T)
+    if (pi_actor && h == 0 && act != ACT_RELU) {
       float* ps = L0.pstash + (size_t)r0 * L0.Np;
       for (int i = tid; i < R * L0.Np; i += SAC_THREADS) st_f<false>(ps + i, P0[(i / L0.Np) * ldp0 + i % L0.Np]);
     }
@@ -575,7 +577,7 @@ __device__ __forceinline__ void target_critic_split_body(const EngineDev* __rest
     after_l1();  // layer 1's held weights are dead from here
     if (act != ACT_RELU && act != ACT_ID) act_pass_fwd<R>(H1, ldh1, HHr >> 4, act);
     __syncthreads();
-    if (pi_actor) {  // this half's layer-1 pre-activations
+    if (pi_actor && act != ACT_RELU) {  // this half's layer-1 pre-activations
       float* ps = L1.pstash + (size_t)r0 * L1.Np + h * HH;
       for (int i = tid; i < R * HH; i += SAC_THREADS) st_f<false>(ps + (i / HH) * L1.Np + i % HH, P1[(i / HH) * ldp1 + i % HH]);
     }
@@ -992,12 +994,27 @@ __device__ __forceinline__ void actor_split_body(const EngineDev* __restrict__ E
   HTiles<T, 2, NCH_HH> ht1;
   ht_issue<T, 1, NCH_32, false>(ht2, wt2);
   ht_issue<T, 2, NCH_HH, false>(ht1, wt1);
-  {  // relu masks: pi's pre-activations stashed by phase A's pi(s) role
-    const float* p0 = L0.pstash + (size_t)r0 * L0.Np;
-    for (int i = tid; i < R * L0.Np; i += SAC_THREADS) P0[(i / L0.Np) * ldp0 + i % L0.Np] = ldf<false>(p0 + i);
-    const float* p1 = L1.pstash + (size_t)r0 * L1.Np + h * HH;
-    for (int i = tid; i < R * HH; i += SAC_THREADS)
-      P1[(i / HH) * ldp1 + i % HH] = ldf<false>(p1 + (i / HH) * L1.Np + i % HH);
+  {  // the hidden layers' activation derivatives: for ReLU the masks, read from
+     // the next layer's X^T that phase A's pi(s) role stashed for phase D
+     // (relu(p) > 0 <=> p > 0); otherwise the stashed pre-activations
+    if (pi.hid_act == ACT_RELU) {
+      const AS_G T* x1 = GPC(T, L1.XT) + par * L1.xt_par + r0;  // relu(P0)^T [K1][Bp]
+      for (int i = tid; i < R * L0.Np; i += SAC_THREADS) {
+        const int k = i / R, r = i % R;
+        P0[r * ldp0 + k] = k < L1.K ? (float)x1[(size_t)k * Bp + r] : 0.f;
+      }
+      const AS_G T* x2 = GPC(T, L2.XT) + par * L2.xt_par + (size_t)h * HH * Bp + r0;  // this half's relu(P1)^T
+      for (int i = tid; i < R * HH; i += SAC_THREADS) {
+        const int k = i / R, r = i % R;
+        P1[r * ldp1 + k] = (float)x2[(size_t)k * Bp + r];
+      }
+    } else {
+      const float* p0 = L0.pstash + (size_t)r0 * L0.Np;
+      for (int i = tid; i < R * L0.Np; i += SAC_THREADS) P0[(i / L0.Np) * ldp0 + i % L0.Np] = ldf<false>(p0 + i);
+      const float* p1 = L1.pstash + (size_t)r0 * L1.Np + h * HH;
+      for (int i = tid; i < R * HH; i += SAC_THREADS)
+        P1[(i / HH) * ldp1 + i % HH] = ldf<false>(p1 + (i / HH) * L1.Np + i % HH);
+    }
     if (tid < R) lpB[tid] = ldf<false>(E.lp_st + par * E.Br + r0 + tid);
   }
   // the head stash of this thread's (row, dim) and the critics' output biases,
