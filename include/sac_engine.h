@@ -97,9 +97,11 @@ typedef struct sac_engine_config {
 } sac_engine_config;
 
 enum sac_layout {         /* phase A / C workgroup layouts (sac_engine_config.layout) */
-  SAC_LAYOUT_AUTO = 0,    /* hidden-split role kernels where they apply, else roles, else row tiles */
+  SAC_LAYOUT_AUTO = 0,    /* hidden-split role kernels where they apply, else roles, else pair tiles
+                             (row tiles where the pair layout's LDS does not fit) */
   SAC_LAYOUT_ROLES = 1,   /* one workgroup per (network role, row tile): no hidden split */
-  SAC_LAYOUT_ROWS = 2     /* one workgroup per row tile running every network */
+  SAC_LAYOUT_ROWS = 2,    /* one workgroup per row tile running every network */
+  SAC_LAYOUT_PAIRS = 3    /* one workgroup per (pair of row tiles, group of networks): large batches */
 };
 
 /* Caller-owned device state of one learner. */

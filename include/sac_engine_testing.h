@@ -25,6 +25,9 @@ int sac_engine_uses_roles(const sac_engine *e);
 /* 1 if phases A/C run the hidden-split role kernels (sac_split.h: two
  * workgroups per role and row tile, each with half of the 256-wide layer 1). */
 int sac_engine_uses_split(const sac_engine *e);
+/* 1 if phases A/C run the pair-tile kernels (sac_pairs.h: one workgroup per
+ * pair of row tiles and group of networks; config.layout = SAC_LAYOUT_PAIRS). */
+int sac_engine_uses_pairs(const sac_engine *e);
 /* Launches per gradient step of the large-batch stage path (sac_wide.h:
  * layer-synchronous GEMM stages for phases A and C, used where the per-network
  * role kernels do not fit), else 0. */

@@ -35,6 +35,7 @@
 #include "sac_phases.h"
 #include "sac_split.h"
 #include "sac_wide.h"
+#include "sac_pairs.h"
 
 // ============================================================================ params / replay
 template <typename T>
@@ -378,7 +379,7 @@ static int validate(const sac_engine_config* c) {
   for (int a : acts)
     if (a < 0 || a > 6) return fail(SAC_E_INVALID, "bad activation code");
   if (c->precision != SAC_PREC_FP32 && c->precision != SAC_PREC_BF16) return fail(SAC_E_INVALID, "bad precision");
-  if (c->layout < SAC_LAYOUT_AUTO || c->layout > SAC_LAYOUT_ROWS || c->stage_path < -1 || c->stage_path > 1 ||
+  if (c->layout < SAC_LAYOUT_AUTO || c->layout > SAC_LAYOUT_PAIRS || c->stage_path < -1 || c->stage_path > 1 ||
       c->stage_batch < -1 || c->stage_batch > 0 || c->upd_parts < 0 || c->upd_parts > 4 ||
       (c->upd_threads != 0 && c->upd_threads != 512 && c->upd_threads != 1024))
     return fail(SAC_E_INVALID, "bad layout override (layout 0..2, stage_path -1..1, stage_batch -1..0, "
@@ -643,7 +644,8 @@ static void build_wide(sac_engine* e, char* base) {
 
 static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
   const int esz = c->precision == SAC_PREC_BF16 ? 2 : 4;
-  const int B = c->batch, Bp = rup(B, 32), nrt = (B + SAC_ROWS - 1) / SAC_ROWS, Br = nrt * SAC_ROWS;
+  // Br: rows of the per-row stashes, whole pairs of row tiles (the pair-tile kernels write 2R rows)
+  const int B = c->batch, Bp = rup(B, 32), nrt = (B + SAC_ROWS - 1) / SAC_ROWS, Br = rup(nrt, 2) * SAC_ROWS;
   const int O = c->obs_dim, A = c->act_dim;
   Layout lay;
   const size_t o_E = lay.take(4096);  // EngineDev, padded for prefetch_engine()
@@ -669,8 +671,10 @@ static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
     }
   }
   int split = 0;  // decided below; the layout lambda reads it
-  auto lds_layout = [&](EngineDev& hh, int xrows, bool full) -> int {
-    const int R = SAC_ROWS;
+  // pairs: the pair-tile kernels (sac_pairs.h): every per-row buffer 2R rows,
+  // pre-activations for one critic or pi at a time (no P2 / second outputs)
+  auto lds_layout = [&](EngineDev& hh, int xrows, bool full, bool pairs = false) -> int {
+    const int R = pairs ? 2 * SAC_ROWS : SAC_ROWS;
     hh.ld = maxKp + 4;
     hh.ldo = maxNo + 4;
     int lo = 0;
@@ -690,7 +694,7 @@ static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
       hh.ldp1[l] = np + 4;
       hh.o_P1[l] = lt(R * hh.ldp1[l]);
     }
-    for (int l = 0; full && l < Lhq; ++l) {
+    for (int l = 0; full && !pairs && l < Lhq; ++l) {
       hh.ldp2[l] = hh.net[NET_Q2].l[l].Np + 4;
       hh.o_P2[l] = lt(R * hh.ldp2[l]);
     }
@@ -704,13 +708,13 @@ static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
     hh.o_ea = lt(R * A);
     hh.o_out = lt(xrows * hh.ldo);
     hh.o_outp = lt(xrows * hh.ldo);
-    hh.o_out2 = lt(R * hh.ldo);
-    hh.o_outp2 = lt(R * hh.ldo);
+    hh.o_out2 = pairs ? 0 : lt(R * hh.ldo);
+    hh.o_outp2 = pairs ? 0 : lt(R * hh.ldo);
     hh.o_lp = lt(R);
     hh.o_qt = lt(2 * R);
     hh.o_y = lt(R);
-    hh.o_g = lt(R * hh.ldo);
-    hh.o_g2 = lt(R * hh.ldo);
+    hh.o_g = lt(pairs ? 2 * R : R * hh.ldo);
+    hh.o_g2 = pairs ? 0 : lt(R * hh.ldo);
     hh.o_ga = lt(R * A);
     hh.o_gout = lt(R * hh.ldo);
     hh.o_slot = lt(2 * R);  // int64[R]
@@ -721,6 +725,7 @@ static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
   // block per row tile: pi on [s'; s], 2R rows)
   const bool lds_fits_roles = (size_t)lds_layout(probe, SAC_ROWS, true) * 4 <= 160 * 1024;
   const bool lds_fits_rows = (size_t)lds_layout(probe, 2 * SAC_ROWS, true) * 4 <= 160 * 1024;
+  const bool lds_fits_pairs = (size_t)lds_layout(probe, 2 * SAC_ROWS, true, true) * 4 <= 160 * 1024;
   // hidden-split role kernels (sac_split.h): two hidden layers of width 256 in
   // both nets, identity pi output, 2 act <= 32, and 12 * nrt co-resident blocks
   split = lds_fits_roles && c->q_layers == 3 && c->pi_layers == 3 && c->q_dims[1] == SPLIT_H && c->q_dims[2] == SPLIT_H &&
@@ -860,7 +865,8 @@ static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
   // path on any batch past the hidden split, -1 refuses it.
   WideLay wl;
   {
-    const int roles_pre = 6 * nrt0 <= 256 && SAC_ROWS * (A + 1) <= SAC_HAND_STRIDE && c->layout != SAC_LAYOUT_ROWS;
+    const int roles_pre = 6 * nrt0 <= 256 && SAC_ROWS * (A + 1) <= SAC_HAND_STRIDE && c->layout != SAC_LAYOUT_ROWS &&
+                          c->layout != SAC_LAYOUT_PAIRS;
     const bool too_big = !(roles_pre ? lds_fits_roles : lds_fits_rows);
     const bool able = !split && c->q_layers >= 3 && c->pi_layers >= 3 && 2 * A <= WJMAX;
     int on = able && too_big;
@@ -920,9 +926,18 @@ static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
   // tile kernels run pi on [s'; s] (2R rows); with roles every MLP pass is R rows.
   // The stage path (wl.on) launches none of them but policy_act: R rows, no
   // pre-activation buffers.
-  int roles = 6 * nrt <= 256 && SAC_ROWS * (A + 1) <= SAC_HAND_STRIDE && c->layout != SAC_LAYOUT_ROWS;
+  int roles = 6 * nrt <= 256 && SAC_ROWS * (A + 1) <= SAC_HAND_STRIDE && c->layout != SAC_LAYOUT_ROWS &&
+              c->layout != SAC_LAYOUT_PAIRS;
   roles = roles && !wl.on;
-  const int lo = lds_layout(h, wl.on || roles ? SAC_ROWS : 2 * SAC_ROWS, !wl.on);
+  // pair-tile kernels (sac_pairs.h): two row tiles and one group of networks per
+  // workgroup; the critics' seeds are applied by phase B (TileDesc::seed).  The
+  // default past the role split wherever its LDS layout fits: C3 4.66K -> 4.90K
+  // steps/s fp32, 8.26K -> 9.58K bf16 (profiles/r05_ab_pair_tiles_c3.txt)
+  const int pairs = !split && !roles && !wl.on &&
+                    (c->layout == SAC_LAYOUT_PAIRS || c->layout == SAC_LAYOUT_AUTO) && lds_fits_pairs &&
+                    SAC_ROWS * (A + 1) <= SAC_HAND_STRIDE;
+  const int lo = pairs ? lds_layout(h, 2 * SAC_ROWS, true, true)
+                       : lds_layout(h, wl.on || roles ? SAC_ROWS : 2 * SAC_ROWS, !wl.on);
 
   if (e) {
     h.B = B;
@@ -941,6 +956,7 @@ static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
       h.role_xcd = split && (10 + split_wpi(esz)) * nrt % 8 == 0;
       // role split of phases A/C: 6 * nrt workgroups must be co-resident (one per CU)
       h.roles = roles;
+      h.pairs = pairs;
       // phase C stages the next step's batch (config.stage_batch = -1 turns it off)
       h.stage = c->stage_batch >= 0;
     }
@@ -1052,7 +1068,7 @@ static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
             t.gsum = 1;
             t.goff = 0;
             t.seed = nullptr;
-            if (split && ni != NET_PI) t.seed = h.seedq + (size_t)(ni - NET_Q1) * Bp;
+            if ((split || pairs) && ni != NET_PI) t.seed = h.seedq + (size_t)(ni - NET_Q1) * Bp;
             if (l == 0 && split) {  // one block: dY parts [p Bp, (p+1) Bp) summed, X^T [0, Bp)
               t.gsum = ni == NET_PI ? wc : 2;
               t.goff = Bp;
@@ -1156,6 +1172,8 @@ static void set_lds_attrs(size_t bytes) {
   (void)hipFuncSetAttribute((const void*)sac_actor<T, true>, hipFuncAttributeMaxDynamicSharedMemorySize, b);
   (void)hipFuncSetAttribute((const void*)sac_policy_act_kernel<T>, hipFuncAttributeMaxDynamicSharedMemorySize, b);
   (void)hipFuncSetAttribute((const void*)sac_target_critic_split<T>, hipFuncAttributeMaxDynamicSharedMemorySize, b);
+  (void)hipFuncSetAttribute((const void*)sac_target_critic_pairs<T>, hipFuncAttributeMaxDynamicSharedMemorySize, b);
+  (void)hipFuncSetAttribute((const void*)sac_actor_pairs<T>, hipFuncAttributeMaxDynamicSharedMemorySize, b);
   (void)hipFuncSetAttribute((const void*)sac_actor_split<T>, hipFuncAttributeMaxDynamicSharedMemorySize, b);
   (void)hipFuncSetAttribute((const void*)sac_critic_update<T>, hipFuncAttributeMaxDynamicSharedMemorySize, b);
   (void)hipFuncSetAttribute((const void*)sac_critic_update<T, 512>, hipFuncAttributeMaxDynamicSharedMemorySize, b);
@@ -1195,6 +1213,8 @@ static void launch_kind(sac_engine* e, int kind, const sac_replay* rb, const int
                                                                                                   eps);
       else if (e->h.roles)
         sac_target_critic<T, true><<<e->nrt * 6, SAC_THREADS, lf, s>>>(e->d, *rb, idx, eps);
+      else if (e->h.pairs)
+        sac_target_critic_pairs<T><<<2 * ((e->nrt + 1) / 2), SAC_THREADS, lf, s>>>(e->d, *rb, idx, eps);
       else
         sac_target_critic<T, false><<<e->nrt * e->h.xs, SAC_THREADS, lf, s>>>(e->d, *rb, idx, eps);
       break;
@@ -1209,6 +1229,8 @@ static void launch_kind(sac_engine* e, int kind, const sac_replay* rb, const int
         sac_actor_split<T><<<e->nrt * 3 * split_wc((int)sizeof(T)) + stg, SAC_THREADS, lf, s>>>(e->d, *rb);
       else if (e->h.roles)
         sac_actor<T, true><<<e->nrt * 3 + stg, SAC_THREADS, lf, s>>>(e->d, *rb);
+      else if (e->h.pairs)
+        sac_actor_pairs<T><<<2 * ((e->nrt + 1) / 2) + stg, SAC_THREADS, lf, s>>>(e->d, *rb);
       else
         sac_actor<T, false><<<e->nrt * e->h.xs + stg, SAC_THREADS, lf, s>>>(e->d, *rb);
       break;
@@ -1635,6 +1657,8 @@ int sac_debug_eps_device(uint64_t seed, uint64_t step, int32_t batch, int32_t ac
 int sac_engine_uses_roles(const sac_engine* e) { return e && e->h.roles ? 1 : 0; }
 
 int sac_engine_uses_split(const sac_engine* e) { return e && e->h.split ? 1 : 0; }
+
+int sac_engine_uses_pairs(const sac_engine* e) { return e && e->h.pairs ? 1 : 0; }
 
 int sac_engine_uses_wide(const sac_engine* e) { return e && e->wide ? (int)e->wst.size() : 0; }
 

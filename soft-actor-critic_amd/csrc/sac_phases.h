@@ -81,6 +81,7 @@ struct EngineDev {
   int xs;
   int role_xcd;  // phase A role kernel: a weight part's workgroups on at most two XCDs (SAC_ROLE_XCD)
   int roles;  // phases A / C split into per-network workgroups (see "role hand-offs")
+  int pairs;  // phases A / C as pair-tile workgroups (sac_pairs.h)
   int gstride;     // granules per (kind, row tile): SAC_ROWS * (act_dim + 1)
   uint64_t* gran;  // [G_COUNT][nrt][gstride] data-tagged hand-off granules (gran_put)
   int upd_slots;  // update tiles: batch chunks staged per round (LDS slots, 1..4)

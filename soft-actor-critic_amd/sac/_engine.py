@@ -56,7 +56,7 @@ class EngineConfig(ctypes.Structure):
 
 
 # sac_engine_config.layout (include/sac_engine.h enum sac_layout)
-LAYOUTS = {"auto": 0, "roles": 1, "rows": 2}
+LAYOUTS = {"auto": 0, "roles": 1, "rows": 2, "pairs": 3}
 # the overrides a caller may pass to SacEngine(layout={...}), with their C field
 LAYOUT_KEYS = ("layout", "stage_path", "stage_batch", "upd_parts", "upd_threads")
 

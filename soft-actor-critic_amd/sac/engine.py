@@ -152,6 +152,9 @@ class SacEngine:
         self._calls = 0
         self.lib.sac_engine_uses_roles.argtypes = [ctypes.c_void_p]
         self.roles = bool(self.lib.sac_engine_uses_roles(h))
+        # pair-tile kernels (csrc/sac_pairs.h): layout={"layout": "pairs"}
+        self.lib.sac_engine_uses_pairs.argtypes = [ctypes.c_void_p]
+        self.pairs = bool(self.lib.sac_engine_uses_pairs(h))
         # large-batch stage path (csrc/sac_wide.h): launches per step, 0 when the phase kernels run
         self.lib.sac_engine_uses_wide.argtypes = [ctypes.c_void_p]
         self.wide = int(self.lib.sac_engine_uses_wide(h))

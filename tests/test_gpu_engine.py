@@ -248,18 +248,20 @@ def test_role_split_equals_row_tiles(precision):
         assert torch.equal(out["1"][k], out["0"][k]), k
 
 
-def test_large_batch_uses_row_tile_kernels_and_runs():
-    """C3 (B=4096): 256 row tiles do not fit the role split; the one-block-per-
-    row-tile kernels run (C3's default; stage_path=-1 also refuses the stage path)."""
-    eng, rb, c = _engine("c3", "bf16", capacity=20_000, stage_path=-1)
-    assert not eng.roles and not eng.wide
+@pytest.mark.parametrize("layout", ["auto", "rows"])
+def test_large_batch_uses_pair_or_row_tile_kernels_and_runs(layout):
+    """C3 (B=4096): 256 row tiles do not fit the role split; the pair-tile kernels
+    run (C3's default), or with layout "rows" the one-block-per-row-tile kernels
+    (stage_path=-1 also refuses the stage path)."""
+    eng, rb, c = _engine("c3", "bf16", capacity=20_000, stage_path=-1, layout=layout)
+    assert not eng.roles and not eng.wide and eng.pairs == (layout == "auto")
     eng.train_graph(rb, 20, chunk=10)
     eng.check()
     assert all(np.isfinite(eng.losses()))
 
 
 @pytest.mark.parametrize("cfg,precision,layout", [("c2", "bf16", "auto"), ("c2", "fp32", "roles"),
-                                                  ("c3", "bf16", "auto")])
+                                                  ("c3", "bf16", "auto"), ("c3", "fp32", "rows")])
 def test_staged_batch_equals_in_step_gather(cfg, precision, layout):
     """Phase C staging step t+1's batch (sampled and gathered one launch early)
     gives the same bits as phase A gathering it, across graph replays, a replay

@@ -107,6 +107,33 @@ def test_c3_stage_path_matches_oracle(precision):
     test_baseline_config_matches_oracle("c3", 12_288, 2, precision, layout={"stage_path": 1})
 
 
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_c3_row_tiles_match_oracle(precision):
+    """C3 through the one-workgroup-per-row-tile kernels (layout "rows"; C3's
+    default is the pair-tile kernels, csrc/sac_pairs.h), against the oracle like
+    test_baseline_config_matches_oracle."""
+    test_baseline_config_matches_oracle("c3", 12_288, 2, precision, layout={"layout": "rows"})
+
+
+# The layout the default does not take at these shapes: the pair-tile kernels at
+# one row and with 4-layer nets (the role split's batches), the row-tile kernels
+# at B = 4001 (251 row tiles; by default the pairs run it, the last pair with one
+# row tile)
+FORCED_EDGES = {"pairs_b1": ("b1", "pairs"), "pairs_deep4": ("deep4", "pairs"),
+                "rows_b4001": ("rowtile_b4001", "rows")}
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+@pytest.mark.parametrize("shape", sorted(FORCED_EDGES))
+def test_forced_layout_edges_match_oracle(shape, precision):
+    """Ragged and small shapes on the kernel layout the default does not pick
+    there, against the oracle with the edge-shape tolerances."""
+    base, lay = FORCED_EDGES[shape]
+    c = dict(EDGE_SHAPES[base], name=shape)
+    _check_config_against_oracle(c, precision, 2 if c["batch"] > 1024 else 3, traj_tol=2e-3,
+                                 layout={"layout": lay})
+
+
 @pytest.mark.parametrize("name", ["c1_auto", "c2"])
 def test_engine_matches_reference_golden_directly(name):
     """Step 1 against the reference's own captured outputs (no oracle in between)."""
@@ -157,7 +184,7 @@ def test_baseline_config_matches_oracle(cfg, capacity, steps, precision, layout=
 
 # Shapes at the edges of the kernels' tiling, none of them a BASELINE config:
 # ragged last row tiles (B % 16 != 0) on each of the three phase-kernel layouts
-# (hidden split, per-network roles, one block per row tile), a one-row batch,
+# (hidden split, per-network roles, pair tiles: the row-tile kernels in FORCED_EDGES), a one-row batch,
 # the widest input the [256, 256] nets take (obs 256 + act 6: Kp 288 > 256 for
 # the critics) and four-layer nets.
 EDGE_SHAPES = {
@@ -244,6 +271,8 @@ def _check_config_against_oracle(c, precision, steps, roles=None, traj_tol=1e-4,
         del bench.CONFIGS[ckey]
     if roles is not None:
         assert eng.roles == roles
+    if layout and layout.get("layout") == "pairs":
+        assert eng.pairs and not eng.roles and not eng.wide
     B, A = cc["batch"], cc["act"]
     sds = {k: {kk: v.detach().cpu().numpy().copy() for kk, v in m.state_dict().items()} for k, m in eng.nets.items()}
     hp = O.SacHyper(alpha=0.1, auto_entropy_tuning=True)  # bench.build_engine's hyper-parameters
@@ -341,7 +370,7 @@ def _oracle_state_from_engine(eng, act):
                       opt_alpha_v=float(al[3]), opt_alpha_step=float(steps[3]))
 
 
-@pytest.mark.parametrize("shape", ["c2_split", "c4", "roles_b384", "rowtile_b2000", "stage_b2000",
+@pytest.mark.parametrize("shape", ["c2_split", "c4", "roles_b384", "rowtile_b2000", "pairs_b2000", "stage_b2000",
                                    "wide512_b384", "wide400_300"])
 def test_one_step_from_the_engine_state(shape):
     """Per-step parity without trajectory drift (fp32): before every step the
@@ -358,12 +387,14 @@ def test_one_step_from_the_engine_state(shape):
          "c4": dict(obs=32, act=2, hidden=[256, 256], batch=256, capacity=2048),
          "roles_b384": dict(obs=24, act=4, hidden=[256, 256], batch=384, capacity=2048),
          "rowtile_b2000": dict(obs=17, act=6, hidden=[128, 128], batch=2000, capacity=4096),
+         "pairs_b2000": dict(obs=17, act=6, hidden=[128, 128], batch=2000, capacity=4096),
          "stage_b2000": dict(obs=17, act=6, hidden=[128, 128], batch=2000, capacity=4096),
          "wide512_b384": dict(obs=24, act=4, hidden=[512, 512], batch=384, capacity=2048),
          "wide400_300": dict(obs=17, act=6, hidden=[400, 300], batch=256, capacity=2048)}[shape]
     # roles_b384: the role kernels without the hidden split; stage_b2000: the
     # stage path (the row-tile kernels fit B = 2000)
-    lay = {"roles_b384": {"layout": "roles"}, "stage_b2000": {"stage_path": 1}}.get(shape)
+    lay = {"roles_b384": {"layout": "roles"}, "stage_b2000": {"stage_path": 1},
+           "rowtile_b2000": {"layout": "rows"}}.get(shape)
     bench.CONFIGS["_local"] = c
     try:
         eng, rb, cc = bench.build_engine("_local", "fp32", 3, torch.device("cuda", 0), layout=lay)

@@ -107,7 +107,7 @@ def test_one_wide_hidden_layer_is_refused():
     assert rc == SAC_E_INVALID and "B of LDS per workgroup (max 163840)" in msg, (rc, msg)
 
 
-@pytest.mark.parametrize("field,value", [("layout", 3), ("stage_path", 2), ("stage_batch", 1), ("upd_parts", 5),
+@pytest.mark.parametrize("field,value", [("layout", 4), ("stage_path", 2), ("stage_batch", 1), ("upd_parts", 5),
                                          ("upd_threads", 256)])
 def test_bad_layout_override_is_refused(field, value):
     """Out-of-range override fields fail validation (SAC_E_INVALID) in both the

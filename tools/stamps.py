@@ -20,7 +20,9 @@ cfg = sys.argv[1] if len(sys.argv) > 1 else "c2"
 prec = sys.argv[2] if len(sys.argv) > 2 else "bf16"
 dev = torch.device("cuda", 0)
 bench.CONFIGS[cfg]["capacity"] = min(bench.CONFIGS[cfg]["capacity"], 100_000)
-eng, rb, c = bench.build_engine(cfg, prec, 0, dev)
+# optional "layout=NAME" argument: a kernel layout override (e.g. layout=pairs)
+lay = [a.split("=", 1)[1] for a in sys.argv[3:] if a.startswith("layout=")]
+eng, rb, c = bench.build_engine(cfg, prec, 0, dev, layout={"layout": lay[0]} if lay else None)
 lib = E.load_library()
 lib.sac_engine_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
 assert lib.sac_engine_debug_stamped() == 1, "not the stamps build"
@@ -38,6 +40,8 @@ n_d = _tiles([O_] + H_ + [2 * A_])
 OFF = {"A": 0, "C": 0}  # role blocks are the launches' first blocks
 lib.sac_engine_uses_split.argtypes = [ctypes.c_void_p]
 SPLIT = bool(lib.sac_engine_uses_split(eng.handle))
+lib.sac_engine_uses_pairs.argtypes = [ctypes.c_void_p]
+PAIRS = bool(lib.sac_engine_uses_pairs(eng.handle))
 GROUP = 2 * nrt if SPLIT else nrt  # blocks per role group (hidden split: two halves per row tile in A)
 GROUP_C = (4 if prec == "fp32" else 2) * nrt if SPLIT else nrt  # phase C: split_wc parts per row tile
 buf = torch.zeros(nblk * 64, dtype=torch.int64, device=dev)
@@ -77,6 +81,11 @@ if SPLIT:  # sac_split.h stamps
     names.update({2: "L0", 3: "L1 half", 4: "L2 partial", 6: "partials published", 7: "pi head (s')",
                   9: "Qt partial published", 33: "inputs", 34: "pi inputs", 36: "Q1 fwd", 37: "Q2 fwd",
                   38: "Q1 da partial", 39: "pi: critics combined", 35: "pi bwd + GT"})
+if PAIRS:  # sac_pairs.h stamps
+    names.update({6: "pi(s') head", 7: "Qt1", 8: "Qt2 + y", 9: "pi(s) + stashes", 14: "seeds (critics polled)",
+                  10: "Q1 fwd", 11: "Q1 bwd + GT", 12: "Q2 fwd", 13: "Q2 bwd + GT", 33: "inputs",
+                  36: "Q1 fwd", 37: "Q2 fwd", 38: "Q1 da", 39: "Q2 da published / combined", 35: "pi bwd + GT"})
+    GROUP = GROUP_C = (nrt + 1) // 2  # pair tiles per group
 WPI = (4 if prec == "fp32" else 2) if SPLIT else 1  # phase A: pi(s') parts (split_wpi)
 
 
@@ -105,6 +114,8 @@ def role_of(ph, b, G):
 PH = {"A": list(range(0, 17)) + [20, 21, 22, 23, 56, 57, 59, 60],  # 20-23: free for DSTAMP probes
       "C": list(range(32, 40)) + [61], "B": [48, 51, 49, 50, 62], "D": [52, 55, 53, 54, 63]}
 ROLES = {"A": ["pi(s')", "Qt1", "Qt2", "Q1", "Q2", "pi(s)"], "C": ["Q1", "Q2", "pi"]}  # block-group order
+if PAIRS:
+    ROLES = {"A": ["critics", "target + pi(s)"], "C": ["Q2", "Q1 + pi"]}
 # shader clock during phase A: s_memtime ticks (slots 40/41) per realtime tick (slots 0/60)
 clk = []
 for r in runs:
@@ -119,7 +130,7 @@ for ph, ids in PH.items():
     if rows.size == 0:
         continue
     groups = {"all": np.ones(len(blk), bool)}
-    if ph in ROLES and eng.roles:
+    if ph in ROLES and (eng.roles or PAIRS):
         rb_ = blk - OFF[ph]
         G = GROUP_C if ph == "C" else GROUP
         ridx = role_of(ph, rb_, G)
