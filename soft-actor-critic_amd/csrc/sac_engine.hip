@@ -783,6 +783,7 @@ static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
         ly.dbp = nullptr;
       }
       if (is_pi) ly.pstash = (float*)P(lay.take((size_t)Br * ly.Np * 4));
+      if (is_pi) ly.pmask = (uint32_t*)P(lay.take((size_t)Br * ((ly.Np + 31) / 32) * 4));
     }
   }
   h.s_st = (float*)P(lay.take((size_t)Br * O * 4));

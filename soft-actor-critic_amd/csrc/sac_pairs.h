@@ -249,12 +249,26 @@ __global__ void __launch_bounds__(SAC_THREADS) sac_target_critic_pairs(const Eng
       if (actor)  // the actor rows' layer input, into this step's parity copy (phase D)
         store_T<T, PR>(X, ld, Ly.Kp, Ly.K, (T*)Ly.XT + par * Ly.xt_par, Bp, r0, nvalid, nullptr);
       const bool out = l == pi.L - 1;
-      // pre-activations for phase C's pi backward (every layer, as the row-tile kernels)
-      float* stash = actor ? Ly.pstash + (size_t)r0 * Ly.Np : nullptr;
+      // for phase C's pi backward: a ReLU hidden layer's mask as bits (written
+      // below from the activations), every other layer's pre-activations
+      const bool bits = !out && pi.hid_act == ACT_RELU;
+      float* stash = actor && !bits ? Ly.pstash + (size_t)r0 * Ly.Np : nullptr;
       const GemmW nx = out ? gw_fwd(E.net[NET_Q1T].l[0]) : gw_fwd(pi.l[l + 1]);
       layer_fwd<T, PR>(X, ld, Ly, pi.P + Ly.b_off, out ? pi.out_act : pi.hid_act, out ? outP : nullptr,
                        out ? ldo : ld, out ? outB : Y, out ? ldo : ld, stash, 0, pf, nx);
       __syncthreads();
+      if (actor && bits) {  // relu(p) > 0 <=> p > 0: one 32-unit word per (row, word) lane
+        const int nw = Ly.Np >> 5;
+        AS_G uint32_t* mk = GP(uint32_t, Ly.pmask) + (size_t)r0 * nw;
+        for (int i = tid; i < PR * nw; i += SAC_THREADS) {
+          const int r = i / nw, w = i % nw;
+          const lf* y = Y + r * ld + 32 * w;
+          uint32_t m = 0;
+#pragma unroll
+          for (int u = 0; u < 32; ++u) m |= (y[u] > 0.f ? 1u : 0u) << u;
+          mk[i] = m;
+        }
+      }
       lf* t = X;
       X = Y;
       Y = t;
@@ -444,8 +458,20 @@ __device__ __forceinline__ void actor_pairs_body(const AS_C EngineDev& E, int bi
     const AS_C LayerDev& Ly = pi.l[l];
     const int ldp = E.ldp1[l];
     lf* P = lds + E.o_P1[l];
-    const AS_G float* ps = GPC(float, Ly.pstash) + (size_t)r0 * Ly.Np;
-    for (int i = tid; i < PR * Ly.Np; i += SAC_THREADS) P[(i / Ly.Np) * ldp + i % Ly.Np] = ps[i];
+    if (pi.hid_act == ACT_RELU) {  // phase A's mask bits: 1 / 0 stand in for the pre-activation's sign
+      const int nw = Ly.Np >> 5;
+      const AS_G uint32_t* mk = GPC(uint32_t, Ly.pmask) + (size_t)r0 * nw;
+      for (int i = tid; i < PR * nw; i += SAC_THREADS) {
+        const int r = i / nw, w = i % nw;
+        const uint32_t m = mk[i];
+        lf* pr = P + r * ldp + 32 * w;
+#pragma unroll
+        for (int u = 0; u < 32; ++u) pr[u] = (m >> u) & 1u ? 1.f : 0.f;
+      }
+    } else {
+      const AS_G float* ps = GPC(float, Ly.pstash) + (size_t)r0 * Ly.Np;
+      for (int i = tid; i < PR * Ly.Np; i += SAC_THREADS) P[(i / Ly.Np) * ldp + i % Ly.Np] = ps[i];
+    }
   }
   __syncthreads();
   // ---- combine the critics' unit-seed gradients with the min-Q weights

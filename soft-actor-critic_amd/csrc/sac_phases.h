@@ -57,6 +57,7 @@ struct LayerDev {
   void* GT;       // [Np][Bp] d(pre-activation), transposed
   float* dbp;     // [nrt][N] bias-gradient partial sums per row tile
   float* pstash;  // pi only: pre-activations of the actor rows [Br][Np]
+  uint32_t* pmask;  // pi hidden layers: ReLU masks of the actor rows [Br][Np / 32] (pair-tile kernels)
   const float* bias;  // = net P + b_off (fp32 master bias [N])
   long xt_par;        // pi only: element offset of the second (odd-step) X^T copy
 };

@@ -26,5 +26,13 @@ for cp in ${R05_PROF_SET:-c2:bf16 c3:bf16}; do
   step 60 "python3 $R/tools/pmc_read.py $P/tcc > $S/${R05_ROUND:-r05}_tcc_${cfg}_${prec}.txt"
   rm -rf $P
 done
+if [ -n "${R05_GATHER:-}" ]; then  # the gather leg's roofline traffic (bench roofline_gather.traffic)
+  P=$S/prof_gather
+  step 200 "rocprofv3 --kernel-trace --stats -d $P/kt -o kt -- python3 $R/tools/gather_bench.py 20 1048576 > $S/kt_gather.log 2>&1"
+  step 200 "rocprofv3 --pmc FETCH_SIZE -d $P/fetch -o p -- python3 $R/tools/gather_bench.py 5 1048576 > $S/fetch_gather.log 2>&1"
+  step 200 "rocprofv3 --pmc WRITE_SIZE -d $P/write -o p -- python3 $R/tools/gather_bench.py 5 1048576 > $S/write_gather.log 2>&1"
+  step 60 "python3 $R/tools/pmc_summary.py ${R05_ROUND:-r05} $P --tag _gather --config gather --precision fp32 --dst $S > /dev/null"
+  rm -rf $P
+fi
 fi
 exit $STEP_RC
