@@ -936,7 +936,8 @@ static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
   // steps/s fp32, 8.26K -> 9.58K bf16 (profiles/r05_ab_pair_tiles_c3.txt)
   const int pairs = !split && !roles && !wl.on &&
                     (c->layout == SAC_LAYOUT_PAIRS || c->layout == SAC_LAYOUT_AUTO) && lds_fits_pairs &&
-                    SAC_ROWS * (A + 1) <= SAC_HAND_STRIDE;
+                    SAC_ROWS * (A + 1) <= SAC_HAND_STRIDE &&
+                    SAC_ROWS * (2 * O + A + 2) <= 4 * SAC_THREADS;  // pair_batch: a record in 4 loads per thread
   const int lo = pairs ? lds_layout(h, 2 * SAC_ROWS, true, true)
                        : lds_layout(h, wl.on || roles ? SAC_ROWS : 2 * SAC_ROWS, !wl.on);
 

@@ -35,52 +35,74 @@
 #define SAC_PR (2 * SAC_ROWS)  // rows per pair tile
 
 // The pair's batch rows (s, s', a, r, d) into LDS: the two 16-row records phase
-// C staged, or the tile's own sample + gather.  Returns whether every live
-// sub-tile came from a staged record (uniform).
+// C staged, or the tile's own sample + gather.  Both records' loads (and both
+// headers') are issued before any LDS store: one round trip for the pair, not
+// one per record.  Returns whether every live sub-tile came from a staged
+// record (uniform).
 __device__ __forceinline__ bool pair_batch(const AS_C EngineDev& E, const sac_replay& rb, uint64_t step, int pt,
                                            const AS_G int32_t* inj_idx, lf* sB, lf* s2B, lf* aB, lf* rB, lf* dB,
                                            AS_L int64_t* slotB) {
   constexpr int R = SAC_ROWS;
   const int tid = threadIdx.x, O = E.O, A = E.A;
   const int64_t rb_size = GPC(int64_t, rb.state)[0], rb_pos = GPC(int64_t, rb.state)[1];
+  const int RO = R * O, RA = R * A, per = 2 * RO + RA + 2 * R;  // floats of one record
+  bool staged[2] = {false, false};
+  const bool live1 = 2 * pt + 1 < E.nrt;
+  if (E.stage && !inj_idx) {  // uniform
+    const AS_G float* rec[2] = {GPC(float, E.stg) + stage_rec(E, step, 2 * pt),
+                                GPC(float, E.stg) + stage_rec(E, step, live1 ? 2 * pt + 1 : 2 * pt)};
+    uint64_t h[2][5];
+#pragma unroll
+    for (int sub = 0; sub < 2; ++sub)
+#pragma unroll
+      for (int k = 0; k < 5; ++k) h[sub][k] = ((const AS_C uint64_t*)rec[sub])[k];
+    constexpr int MV = 4;  // record floats per thread and record, at most (R * (2 O + A + 2) <= 2048)
+    float v[2][MV];
+#pragma unroll
+    for (int sub = 0; sub < 2; ++sub)
+#pragma unroll
+      for (int u = 0; u < MV; ++u) {
+        const int i = tid + u * SAC_THREADS;
+        v[sub][u] = i < per ? rec[sub][16 + i] : 0.f;
+      }
+#pragma unroll
+    for (int sub = 0; sub < 2; ++sub) {
+      staged[sub] = h[sub][0] == step && h[sub][1] == (uint64_t)rb_size && h[sub][2] == (uint64_t)rb_pos &&
+                    h[sub][3] == (uint64_t)(uintptr_t)rb.obs && h[sub][4] == (uint64_t)GPC(int64_t, rb.state)[2];
+#pragma unroll
+      for (int u = 0; u < MV; ++u) {
+        const int i = tid + u * SAC_THREADS;
+        if (i < per) {
+          if (i < RO) sB[sub * RO + i] = v[sub][u];
+          else if (i < 2 * RO) s2B[sub * RO + i - RO] = v[sub][u];
+          else if (i < 2 * RO + RA) aB[sub * RA + i - 2 * RO] = v[sub][u];
+          else if (i < 2 * RO + RA + R) rB[sub * R + i - 2 * RO - RA] = v[sub][u];
+          else dB[sub * R + i - 2 * RO - RA - R] = v[sub][u];
+        }
+      }
+    }
+  }
   bool all_staged = true;
 #pragma unroll
   for (int sub = 0; sub < 2; ++sub) {
     const int rbi = 2 * pt + sub;
-    lf* s = sB + sub * R * O;
-    lf* s2 = s2B + sub * R * O;
-    lf* a = aB + sub * R * A;
+    lf* s = sB + sub * RO;
+    lf* s2 = s2B + sub * RO;
+    lf* a = aB + sub * RA;
     lf* r = rB + sub * R;
     lf* d = dB + sub * R;
     if (rbi >= E.nrt) {  // the pair's second tile past the batch: zero rows
-      for (int i = tid; i < R * O; i += SAC_THREADS) s[i] = s2[i] = 0.f;
-      for (int i = tid; i < R * A; i += SAC_THREADS) a[i] = 0.f;
+      for (int i = tid; i < RO; i += SAC_THREADS) s[i] = s2[i] = 0.f;
+      for (int i = tid; i < RA; i += SAC_THREADS) a[i] = 0.f;
       if (tid < R) r[tid] = d[tid] = 0.f;
       continue;
     }
-    bool staged = false;
-    if (E.stage && !inj_idx) {
-      const AS_G float* rec = GPC(float, E.stg) + stage_rec(E, step, rbi);
-      const AS_C uint64_t* hdr = (const AS_C uint64_t*)rec;
-      const AS_G float* p = rec + 16;
-      for (int i = tid; i < R * O; i += SAC_THREADS) {
-        s[i] = p[i];
-        s2[i] = p[R * O + i];
-      }
-      for (int i = tid; i < R * A; i += SAC_THREADS) a[i] = p[2 * R * O + i];
-      if (tid < R) {
-        r[tid] = p[2 * R * O + R * A + tid];
-        d[tid] = p[2 * R * O + R * A + R + tid];
-      }
-      staged = hdr[0] == step && hdr[1] == (uint64_t)rb_size && hdr[2] == (uint64_t)rb_pos &&
-               hdr[3] == (uint64_t)(uintptr_t)rb.obs && hdr[4] == (uint64_t)GPC(int64_t, rb.state)[2];
-    }
-    if (!staged) {  // uniform
+    if (!staged[sub]) {  // uniform
       tile_slots(E, rb, step, rb_size, rb_pos, rbi * R, inj_idx, slotB + sub * R);
       __syncthreads();
       gather_rows<lf*>(rb, slotB + sub * R, O, A, s, s2, a, r, d);
     }
-    all_staged = all_staged && staged;
+    all_staged = all_staged && staged[sub];
   }
   return all_staged;
 }

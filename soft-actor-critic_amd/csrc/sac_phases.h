@@ -870,10 +870,10 @@ __device__ __forceinline__ float adam_elem(float& p, float& m, float& v, float g
 #define SAC_UPD_THREADS 1024
 #endif
 #define SAC_UPD_BCH (512 / (int)sizeof(T))  // batch columns staged per chunk (512 B per row)
-// dynamic LDS of an update tile: upd_slots x stage 64 x 528 B | 2 x [32][33] f32 | [32][17] f32
-// (>= the alpha block's 5 x 1024 floats)
+// dynamic LDS of an update tile: upd_slots x stage 64 x 528 B | 2 x [32][33] f32 | [32][17] f32 |
+// upd_slots x [256] f32 seeds (>= the alpha block's 5 x 1024 floats)
 #define SAC_UPD_SLOT_BYTES (64 * 528)
-#define SAC_UPD_LDS_FOR(slots) ((slots) * SAC_UPD_SLOT_BYTES + 2 * 32 * 33 * 4 + 32 * 17 * 4)
+#define SAC_UPD_LDS_FOR(slots) ((slots) * SAC_UPD_SLOT_BYTES + 2 * 32 * 33 * 4 + 32 * 17 * 4 + (slots) * 256 * 4)
 template <typename T, int UT, int GS = 1, int MS = 4>
 __device__ __forceinline__ void dw_adam_tile(const AS_C EngineDev& E, const TileDesc* tdp_, bool polyak, int par,
                                              int par_x, lf* lds) {
@@ -906,9 +906,18 @@ __device__ __forceinline__ void dw_adam_tile(const AS_C EngineDev& E, const Tile
   static_assert(PPO >= 1 && (32 * (SAC_UPD_BCH / EPR)) % UT == 0, "whole pieces per thread");
   const int rstep = ns * SAC_UPD_BCH;          // batch columns per round
   u32x4 rg[MAXS][GS + 1][PPO];                 // [slot][dY part 0..GS-1, then X][piece]
+  // the batch columns' seeds (TileDesc::seed).  Per dY piece (sdr) they are 16x
+  // redundant loads, as many bytes as the dY pieces themselves through each CU's
+  // load path; with several rounds (fp32 at C3) each chunk's seeds are instead
+  // loaded ONCE (by the first bch / 4 threads) and handed over through LDS, a
+  // round's written at the end of the round before: C3 fp32 +3%, while at C2
+  // (one round) the extra barrier cost phase B 0.5 us (profiles/r05_ab_seeds_lds.txt)
   const AS_G float* const seedp = GPC(float, td.seed);  // uniform
-  constexpr int SQ = EPR / 4;                  // seed f32x4 per 16-B piece (fp32 1, bf16 2)
-  f32x4 sdr[MAXS][PPO][SQ];                    // the seeds of this thread's dY pieces
+  const bool lseeds = seedp && sizeof(T) == 4 && Bp > rstep;  // uniform
+  AS_L float* seedL = (AS_L float*)(red + 32 * 17);      // [MAXS][SAC_UPD_BCH]
+  f32x4 sreg[MAXS];                                       // lseeds: the next round's seeds of slot sl (tid < bch / 4)
+  constexpr int SQ = EPR / 4;                             // seed f32x4 per 16-B piece (fp32 1, bf16 2)
+  f32x4 sdr[MAXS][PPO][SQ];                               // !lseeds: the seeds of this thread's dY pieces
   // the operands' bases as separate values: a per-lane choice between two
   // descriptor fields was compiled into a per-lane LOAD of the chosen field and a
   // wait before every piece (the pieces' loads ran one round trip after another)
@@ -918,12 +927,24 @@ __device__ __forceinline__ void dw_adam_tile(const AS_C EngineDev& E, const Tile
   const int ldg = td.ld, ldx = td.ldx;
   // round r0's slot sl -> rg[sl] (16-B pieces of the 32 dY^T rows of every part, then of the 32 X^T rows)
   // what: 1 operands, 2 seeds, 3 both
-  auto issue = [&](int r0, auto slc) {
+  auto issue_seeds = [&](int r0, auto slc) __attribute__((always_inline)) {
+    constexpr int sl = decltype(slc)::value;
+    const int b0 = r0 + sl * SAC_UPD_BCH;
+    if (lseeds && sl < ns && b0 < Bp) {  // uniform
+      const int bch = Bp - b0 < SAC_UPD_BCH ? Bp - b0 : SAC_UPD_BCH;
+      if (threadIdx.x * 4 < bch) sreg[sl] = *(const AS_G f32x4*)(seedp + b0 + threadIdx.x * 4);
+    }
+  };
+  // pieces: seeds = false for round 0 (its seeds were issued before any piece)
+  auto issue = [&](int r0, auto slc, bool seeds = true) {
     constexpr int sl = decltype(slc)::value;
     const int b0 = r0 + sl * SAC_UPD_BCH;
     if (sl < ns && b0 < Bp) {  // uniform
       const int bch = Bp - b0 < SAC_UPD_BCH ? Bp - b0 : SAC_UPD_BCH;
       const int per_row = bch / EPR;  // 16-B pieces per operand row of this chunk
+      // the slot's seeds before its pieces: their wait (end of round) then does
+      // not include this slot's pieces
+      if (seeds) issue_seeds(r0, slc);
 #pragma unroll
       for (int op = 0; op <= GS; ++op)
 #pragma unroll
@@ -932,13 +953,27 @@ __device__ __forceinline__ void dw_adam_tile(const AS_C EngineDev& E, const Tile
           const int row = i / per_row, pc = i % per_row;
           const AS_G T* src = op < GS ? gsrc + op * goff + (size_t)row * ldg : xsrc + (size_t)row * ldx;
           if (i < 32 * per_row) rg[sl][op][pi] = *(const AS_G u32x4*)(src + b0 + pc * EPR);
-          if (op == 0 && seedp && i < 32 * per_row)
+          if (op == 0 && seedp && !lseeds && i < 32 * per_row)
 #pragma unroll
             for (int q = 0; q < SQ; ++q) sdr[sl][pi][q] = *(const AS_G f32x4*)(seedp + b0 + pc * EPR + 4 * q);
         }
     }
   };
-  static_for<MAXS>([&](auto sl) { issue(0, sl); });
+  // round 0: every slot's seeds, then the pieces (the seeds' wait below includes no piece)
+  static_for<MAXS>([&](auto sl) { issue_seeds(0, sl); });
+  static_for<MAXS>([&](auto sl) { issue(0, sl, false); });
+  // the seeds of round r0 + rstep's slots -> LDS (after round r0's last reads of seedL)
+  auto seeds_to_lds = [&](int r0) __attribute__((always_inline)) {
+    if (lseeds)  // uniform
+      static_for<MAXS>([&](auto slc) {
+        constexpr int sl = decltype(slc)::value;
+        const int b0 = r0 + sl * SAC_UPD_BCH;
+        if (sl < ns && b0 < Bp) {
+          const int bch = Bp - b0 < SAC_UPD_BCH ? Bp - b0 : SAC_UPD_BCH;
+          if (tid * 4 < bch) *(AS_L f32x4*)(seedL + sl * SAC_UPD_BCH + tid * 4) = sreg[sl];
+        }
+      });
+  };
   AS_G float* W = GP(float, td.W);
   AS_G float* Wm = GP(float, td.Wm);
   AS_G float* Wv = GP(float, td.Wv);
@@ -989,6 +1024,10 @@ __device__ __forceinline__ void dw_adam_tile(const AS_C EngineDev& E, const Tile
   f32x4 acc[PPW];
 #pragma unroll
   for (int j = 0; j < PPW; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // round 0's seeds -> LDS: issued first, so this waits for them alone, after
+  // every load of the tile (operands, element state, bias) is in flight
+  seeds_to_lds(0);
+  if (lseeds) __syncthreads();  // uniform
   for (int r0 = 0; r0 < Bp; r0 += rstep) {
     // slot by slot: its pieces -> LDS (waits only for this slot's loads: they
     // complete in issue order), the next round's loads into its registers,
@@ -1014,7 +1053,10 @@ __device__ __forceinline__ void dw_adam_tile(const AS_C EngineDev& E, const Tile
                   for (int q = 1; q < GS; ++q) a += __builtin_bit_cast(f32x4, rg[sl][q][pi]);
                   v = __builtin_bit_cast(u32x4, a);
                 }
-              if (op == 0 && seedp) v = __builtin_bit_cast(u32x4, __builtin_bit_cast(f32x4, v) * sdr[sl][pi][0]);
+              if (op == 0 && seedp)
+                v = __builtin_bit_cast(u32x4, __builtin_bit_cast(f32x4, v) *
+                                                  (lseeds ? *(const AS_L f32x4*)(seedL + sl * SAC_UPD_BCH + pc * EPR)
+                                                          : sdr[sl][pi][0]));
             } else if (op == 0 && (GS > 1 || seedp)) {
               // bf16 dY: the parts added in fp32 (part order), scaled by the
               // rows' seeds in fp32, rounded to bf16 once
@@ -1028,7 +1070,7 @@ __device__ __forceinline__ void dw_adam_tile(const AS_C EngineDev& E, const Tile
 #pragma unroll
                 for (int e = 0; e < 8; ++e) a[e] += (float)hq[e];
               }
-              if (seedp)
+              if (seedp)  // bf16: per-piece seeds (lseeds is fp32 only)
 #pragma unroll
                 for (int e = 0; e < 8; ++e) a[e] *= sdr[sl][pi][e >> 2][e & 3];
 #pragma unroll
@@ -1080,6 +1122,7 @@ __device__ __forceinline__ void dw_adam_tile(const AS_C EngineDev& E, const Tile
         }
       }
     });
+    seeds_to_lds(r0 + rstep);  // every thread's reads of this round's seeds are behind a slot barrier
     __syncthreads();  // the stage is refilled by the next round
   }
   STAMP(polyak ? 49 : 53);
