@@ -30,18 +30,20 @@
 
 #define SPLIT_H 256
 #define SPLIT_HH 128
-// Phase C splits layer 1 into split_wc = 4 parts (3 roles x 4 parts x nrt = 192
-// workgroups at C2: its critical path is three layer-1 GEMMs -- critic forward,
-// critic dX, pi dX -- each then a quarter of the work and of the weight bytes
-// per workgroup).  bf16 kept halves until round 5 (the extra batch parts of
-// phase D's layer-0 tiles cost more than the quarters saved); on the round-5
-// build quarters win in bf16 too: C2 26.0K -> 26.8K steps/s
-// (profiles/r05_ab_bf16_quarters_c.txt).  Phase A keeps halves.
-__host__ __device__ constexpr int split_wc(int elem_bytes) { return (void)elem_bytes, 4; }
-// Phase A's pi(s') role -- the head of the y chain -- in quarters in fp32 (the
-// other five roles keep halves: (4 + 10) x nrt = 224 workgroups at C2), halves
-// in bf16 (quarters measured 1.5% slower there, profiles/r05_ab_misc.txt).
-__host__ __device__ constexpr int split_wpi(int elem_bytes) { return elem_bytes == 4 ? 4 : 2; }
+// Phase C splits layer 1 into split_wc parts: four in fp32 (3 roles x 4 parts x
+// nrt = 192 workgroups at C2: its critical path is three layer-1 GEMMs -- critic
+// forward, critic dX, pi dX -- each then a quarter of the MFMA-bound fp32 work
+// per workgroup), two in bf16.  Quarters in bf16 ran faster on the round-5 build
+// (C2 26.0K -> 26.8K steps/s) but failed the bf16 parity bar: pi's layer-0 dY
+// arrives as four bf16-rounded partials instead of two, and the policy's
+// per-step parameter drift against the oracle rose from under to above
+// 0.05 lr (profiles/r05_ab_bf16_quarters_c.txt).
+// Phase A keeps halves (6 roles x 2 x nrt = 192).
+__host__ __device__ constexpr int split_wc(int elem_bytes) { return elem_bytes == 4 ? 4 : 2; }
+// Phase A's pi(s') role -- the head of the y chain -- gets the same parts as
+// phase C (fp32: 4; the other five roles keep halves: (4 + 10) x nrt = 224
+// workgroups at C2; quarters in bf16 measured 1.5% slower, profiles/r05_ab_misc.txt).
+__host__ __device__ constexpr int split_wpi(int elem_bytes) { return split_wc(elem_bytes); }
 #define SPLIT_GP 4  // granule part slots per (kind, row tile): max over precisions of split_wc
 
 // Split granule kinds: [GS_COUNT][nrt][SPLIT_GP parts][E.gs2] 8-B granules
