@@ -730,7 +730,7 @@ static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
   // both nets, identity pi output, 2 act <= 32, and 12 * nrt co-resident blocks
   split = lds_fits_roles && c->q_layers == 3 && c->pi_layers == 3 && c->q_dims[1] == SPLIT_H && c->q_dims[2] == SPLIT_H &&
               c->pi_dims[1] == SPLIT_H && c->pi_dims[2] == SPLIT_H && c->pi_out_act == SAC_ACT_IDENTITY &&
-              2 * A <= 32 && (10 + split_wpi(esz)) * nrt0 <= 256 && (3 * split_wc(esz) + 1) * nrt0 <= 256 &&
+              2 * A <= 32 && (10 + split_wpi(esz)) * nrt0 <= 256 && (2 * split_wcq(esz) + split_wc(esz) + 1) * nrt0 <= 256 &&
               SAC_ROWS * (A + 1) <= SAC_HAND_STRIDE;
   split = split && c->layout == SAC_LAYOUT_AUTO;
   // batch columns of layer 0's operands under the split: X^T 2 Bp (phase A's two
@@ -1228,7 +1228,8 @@ static void launch_kind(sac_engine* e, int kind, const sac_replay* rb, const int
       break;
     case L_C:
       if (e->h.split)
-        sac_actor_split<T><<<e->nrt * 3 * split_wc((int)sizeof(T)) + stg, SAC_THREADS, lf, s>>>(e->d, *rb);
+        sac_actor_split<T><<<e->nrt * (2 * split_wcq((int)sizeof(T)) + split_wc((int)sizeof(T))) + stg, SAC_THREADS,
+                             lf, s>>>(e->d, *rb);
       else if (e->h.roles)
         sac_actor<T, true><<<e->nrt * 3 + stg, SAC_THREADS, lf, s>>>(e->d, *rb);
       else if (e->h.pairs)

@@ -40,6 +40,10 @@
 // 0.05 lr (profiles/r05_ab_bf16_quarters_c.txt).
 // Phase A keeps halves (6 roles x 2 x nrt = 192).
 __host__ __device__ constexpr int split_wc(int elem_bytes) { return elem_bytes == 4 ? 4 : 2; }
+// Phase C's critic roles: quarters in both precisions.  Their parts hand fp32
+// granules to pi (no bf16-rounded partial is stored), so bf16 quarters change
+// only fp32 summation order: C2 bf16 (profiles/r05_ab_bf16_critic_quarters.txt).
+__host__ __device__ constexpr int split_wcq(int elem_bytes) { return (void)elem_bytes, 4; }
 // Phase A's pi(s') role -- the head of the y chain -- gets the same parts as
 // phase C (fp32: 4; the other five roles keep halves: (4 + 10) x nrt = 224
 // workgroups at C2; quarters in bf16 measured 1.5% slower, profiles/r05_ab_misc.txt).
@@ -844,19 +848,21 @@ __device__ __forceinline__ void actor_split_body(const EngineDev* __restrict__ E
   const AS_C EngineDev& E = *(const AS_C EngineDev*)Ep;
   extern __shared__ float lds_raw[];
   lf* lds = (lf*)lds_raw;
-  constexpr int R = SAC_ROWS, W = split_wc(sizeof(T)), HH = SPLIT_H / W;  // HH: layer-1 outputs of a part
+  // WQ: the critic roles' parts of layer 1, WP: pi's (HQ / HH: layer-1 outputs of a part)
+  constexpr int R = SAC_ROWS, WQ = split_wcq(sizeof(T)), WP = split_wc(sizeof(T));
+  constexpr int HQ = SPLIT_H / WQ, HH = SPLIT_H / WP;
   constexpr int KC = MM<T>::KC;
   constexpr int HC0 = 64 / KC;
   constexpr int NCH_H = SPLIT_H / KC;
-  constexpr int NCH_HH = HH / KC;
+  constexpr int NCH_HH = HH / KC, NCH_HQ = HQ / KC;
   constexpr int NCH_32 = 32 / KC;
   const int tid = threadIdx.x;
-  const int n2 = W * E.nrt;
-  const int grp = bid / n2, idx = bid % n2;
-  const int h = idx % W, rbi = idx / W;  // h: this workgroup's part of layer 1
-  // producers first: groups 0 / 1 the critics, group 2 pi
-  const bool is_pi = grp == 2;
-  const int qi = grp;  // critics
+  // producers first: groups 0 / 1 the critics (WQ parts per row tile), group 2 pi (WP parts)
+  const int nq = WQ * E.nrt;
+  const bool is_pi = bid >= 2 * nq;
+  const int qi = is_pi ? 0 : bid / nq;  // critics
+  const int idx = is_pi ? bid - 2 * nq : bid % nq;
+  const int h = is_pi ? idx % WP : idx % WQ, rbi = is_pi ? idx / WP : idx / WQ;  // h: this workgroup's part of layer 1
   STAMP(32);
   const int B = E.B, Bp = E.Bp, O = E.O, A = E.A, ld = E.ld, ldo = E.ldo;
   const int r0 = rbi * R;
@@ -888,30 +894,30 @@ __device__ __forceinline__ void actor_split_body(const EngineDev* __restrict__ E
     const AS_C LayerDev& L1 = net.l[1];
     const AS_C LayerDev& L2 = net.l[2];
     const GemmW w0 = gw_fwd(L0);
-    const GemmW w1 = gw_sub<T>(L1.Wc, L1.Kp, h * HH, HH, 0, L1.Kp, L1.bias + h * HH, HH);
+    const GemmW w1 = gw_sub<T>(L1.Wc, L1.Kp, h * HQ, HQ, 0, L1.Kp, L1.bias + h * HQ, HQ);
     HTiles<T, 2, HC0> h0;
     HTiles<T, 1, NCH_H> h1;
     // layer-1 dX operand of this half, held from the start as well (its fetch
     // would otherwise sit between the forward pass and the backward GEMM)
-    const GemmW wt1 = gw_sub<T>(L1.WTc, L1.Np, 0, L1.Kp, h * HH, HH, nullptr, 0);
-    HTiles<T, 2, NCH_HH> ht1;
+    const GemmW wt1 = gw_sub<T>(L1.WTc, L1.Np, 0, L1.Kp, h * HQ, HQ, nullptr, 0);
+    HTiles<T, 2, NCH_HQ> ht1;
     ht_issue<T, 2, HC0>(h0, w0);
     ht_issue<T, 1, NCH_H>(h1, w1);
-    ht_issue<T, 2, NCH_HH>(ht1, wt1);
+    ht_issue<T, 2, NCH_HQ>(ht1, wt1);
     // the two k-split steps of the critic's chain (layer 2's partial q, then
     // layer 0's dX for the action columns) read weights phase B has just
     // written: held (issued behind the inputs), not a cold round trip each
     // after layer 1 / after dY0 (SAC_KS_C=0: streamed)
-    GemmW w2 = gw_sub<T>(L2.Wc, L2.Kp, 0, L2.Np, h * HH, HH, nullptr, 0);
+    GemmW w2 = gw_sub<T>(L2.Wc, L2.Kp, 0, L2.Np, h * HQ, HQ, nullptr, 0);
     w2.NT = (L2.N + 15) >> 4;
     const int k0 = (O >> 4) << 4, k1 = (O + A + 15) >> 4 << 4;
     GemmW wt0 = gw_sub<T>(L0.WTc, L0.Np, k0, k1 - k0, 0, L0.Np, nullptr, 0);
     KsHeld<T, sizeof(T) == 4 ? 2 : 1> kc2;
     KsHeld<T, sizeof(T) == 4 ? 8 : 1> kc0;
     kc2.ok = kc0.ok = false;
-    // the W2 (fp32 master) element of this thread's column n = tid % HH of the unit-seed backward
-    static_assert(SAC_THREADS % HH == 0, "one W2 column per thread in the unit-seed loop");
-    const float w2n = GPC(float, net.P + L2.w_off)[h * HH + tid % HH];
+    // the W2 (fp32 master) element of this thread's column n = tid % HQ of the unit-seed backward
+    static_assert(SAC_THREADS % HQ == 0, "one W2 column per thread in the unit-seed loop");
+    const float w2n = GPC(float, net.P + L2.w_off)[h * HQ + tid % HQ];
     for (int i = tid; i < R * O; i += SAC_THREADS) sB[i] = GPC(float, E.s_st)[(size_t)r0 * O + i];
     for (int i = tid; i < R * A; i += SAC_THREADS) aB[i] = GPC(float, E.a_st)[(size_t)r0 * A + i];
     if (SAC_KS_C) {  // behind the inputs: waiting for s / a~ must not wait for these (loads retire in order)
@@ -951,18 +957,18 @@ __device__ __forceinline__ void actor_split_body(const EngineDev* __restrict__ E
       }
     });
     if (SAC_KS_C && sizeof(T) == 4) ks_issue<T, decltype(kc0)::MAXC>(kc0, wt0);
-    if (act != ACT_RELU && act != ACT_ID) act_pass_fwd<R>(H1, ldh1, HH >> 4, act);
+    if (act != ACT_RELU && act != ACT_ID) act_pass_fwd<R>(H1, ldh1, HQ >> 4, act);
     __syncthreads();
     gemm_ksplit<T, false, decltype(kc2)::MAXC>(H1, ldh1, w2, red, outB, ldo, &kc2);  // partial q
     STAMP(36 + qi);
     // unit-seed backward down to a~ (the pi role applies the min-Q weights and act'(q))
     {
-      for (int i = tid; i < R * HH; i += SAC_THREADS) {
-        const int r = i / HH, n = i % HH;  // n == tid % HH
+      for (int i = tid; i < R * HQ; i += SAC_THREADS) {
+        const int r = i / HQ, n = i % HQ;  // n == tid % HQ
         U1[r * ldu1 + n] = act_bwd(act, P1[r * ldp1 + n], w2n);
       }
       __syncthreads();
-      gemm_hs<T, 2, NCH_HH, false>(U1, ldu1, wt1, &ht1, [&](int j, int col, const f32x4& acc) {
+      gemm_hs<T, 2, NCH_HQ, false>(U1, ldu1, wt1, &ht1, [&](int j, int col, const f32x4& acc) {
         const bool kv = col < L1.K;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
@@ -1033,10 +1039,10 @@ __device__ __forceinline__ void actor_split_body(const EngineDev* __restrict__ E
   STAMP(34);
   // combine the critics' unit-seed partials with the min-Q weights (L_pi = mean(alpha logpi - min Q))
   // the critics' parts, summed in part order by every consumer
-  const AS_G uint64_t* c1p[W];
-  const AS_G uint64_t* c2p[W];
+  const AS_G uint64_t* c1p[WQ];
+  const AS_G uint64_t* c2p[WQ];
 #pragma unroll
-  for (int p = 0; p < W; ++p) {
+  for (int p = 0; p < WQ; ++p) {
     c1p[p] = gs_at(E, GS_C1, rbi, p);
     c2p[p] = gs_at(E, GS_C2, rbi, p);
   }
@@ -1049,26 +1055,26 @@ __device__ __forceinline__ void actor_split_body(const EngineDev* __restrict__ E
     if (tid < 64) {
       const bool live = tid < R * A;
       const int i = live ? tid : 0, r = i / A, rq = tid < R ? tid : 0;
-      const AS_G uint64_t* gg[4 * W];
+      const AS_G uint64_t* gg[4 * WQ];
 #pragma unroll
-      for (int p = 0; p < W; ++p) {
+      for (int p = 0; p < WQ; ++p) {
         gg[p] = c1p[p] + i;
-        gg[W + p] = c2p[p] + i;
-        gg[2 * W + p] = c1p[p] + R * A + rq;
-        gg[3 * W + p] = c2p[p] + R * A + rq;
+        gg[WQ + p] = c2p[p] + i;
+        gg[2 * WQ + p] = c1p[p] + R * A + rq;
+        gg[3 * WQ + p] = c2p[p] + R * A + rq;
       }
-      float gv[4 * W];
-      gran_getn1<4 * W>(E, gg, ep, gv);
+      float gv[4 * WQ];
+      gran_getn1<4 * WQ>(E, gg, ep, gv);
       float term = 0.f, w1 = 0.f, w2 = 0.f;
       if (tid < R) {
         const bool v = tid < nvalid;
         const AS_C NetDev& q1n = E.net[NET_Q1];
         const AS_C NetDev& q2n = E.net[NET_Q2];
-        float q1p = gv[2 * W], q2p = gv[3 * W];
+        float q1p = gv[2 * WQ], q2p = gv[3 * WQ];
 #pragma unroll
-        for (int p = 1; p < W; ++p) {
-          q1p += gv[2 * W + p];
-          q2p += gv[3 * W + p];
+        for (int p = 1; p < WQ; ++p) {
+          q1p += gv[2 * WQ + p];
+          q2p += gv[3 * WQ + p];
         }
         q1p += bq1;
         q2p += bq2;
@@ -1086,11 +1092,11 @@ __device__ __forceinline__ void actor_split_body(const EngineDev* __restrict__ E
       if (tid == 0 && h == 0) st_f<false>(E.lossp + (par * E.nrt + rbi) * 4 + 2, term);
       const float w1r = __shfl(w1, r, 64), w2r = __shfl(w2, r, 64);
       if (live) {
-        float da1 = gv[0], da2 = gv[W];
+        float da1 = gv[0], da2 = gv[WQ];
 #pragma unroll
-        for (int p = 1; p < W; ++p) {
+        for (int p = 1; p < WQ; ++p) {
           da1 += gv[p];
-          da2 += gv[W + p];
+          da2 += gv[WQ + p];
         }
         gaB[i] = w1r * da1 + w2r * da2;
       }
@@ -1103,19 +1109,19 @@ __device__ __forceinline__ void actor_split_body(const EngineDev* __restrict__ E
       const bool v = tid < nvalid;
       const AS_C NetDev& q1n = E.net[NET_Q1];
       const AS_C NetDev& q2n = E.net[NET_Q2];
-      const AS_G uint64_t* gg[2 * W];
+      const AS_G uint64_t* gg[2 * WQ];
 #pragma unroll
-      for (int p = 0; p < W; ++p) {
+      for (int p = 0; p < WQ; ++p) {
         gg[p] = c1p[p] + R * A + tid;
-        gg[W + p] = c2p[p] + R * A + tid;
+        gg[WQ + p] = c2p[p] + R * A + tid;
       }
-      float gv[2 * W];
-      gran_getn<2 * W>(E, gg, ep, gv);
-      float q1p = gv[0], q2p = gv[W];
+      float gv[2 * WQ];
+      gran_getn<2 * WQ>(E, gg, ep, gv);
+      float q1p = gv[0], q2p = gv[WQ];
 #pragma unroll
-      for (int p = 1; p < W; ++p) {
+      for (int p = 1; p < WQ; ++p) {
         q1p += gv[p];
-        q2p += gv[W + p];
+        q2p += gv[WQ + p];
       }
       q1p += bq1;
       q2p += bq2;
@@ -1137,19 +1143,19 @@ __device__ __forceinline__ void actor_split_body(const EngineDev* __restrict__ E
   __syncthreads();
   for (int i = tid; i < R * A; i += SAC_THREADS) {
     const int r = i / A;
-    const AS_G uint64_t* gg[2 * W];
+    const AS_G uint64_t* gg[2 * WQ];
 #pragma unroll
-    for (int p = 0; p < W; ++p) {
+    for (int p = 0; p < WQ; ++p) {
       gg[p] = c1p[p] + i;
-      gg[W + p] = c2p[p] + i;
+      gg[WQ + p] = c2p[p] + i;
     }
-    float gv[2 * W];
-    gran_getn<2 * W>(E, gg, ep, gv);  // all in by now (the q granules above came after them)
-    float da1 = gv[0], da2 = gv[W];
+    float gv[2 * WQ];
+    gran_getn<2 * WQ>(E, gg, ep, gv);  // all in by now (the q granules above came after them)
+    float da1 = gv[0], da2 = gv[WQ];
 #pragma unroll
-    for (int p = 1; p < W; ++p) {
+    for (int p = 1; p < WQ; ++p) {
       da1 += gv[p];
-      da2 += gv[W + p];
+      da2 += gv[WQ + p];
     }
     gaB[i] = g1B[r] * da1 + g2B[r] * da2;
   }
@@ -1219,7 +1225,7 @@ __device__ __forceinline__ void actor_split_body(const EngineDev* __restrict__ E
   });
   if (act != ACT_RELU && act != ACT_ID) act_pass_bwd<R>(Xb, ld, P0, ldp0, L1.Kp >> 4, L1.K, act);
   __syncthreads();
-  store_T<T, R>(Xb, ld, L0.Np, L0.N, L0.GT, W * Bp, h * Bp + r0, nvalid, L0.dbp);
+  store_T<T, R>(Xb, ld, L0.Np, L0.N, L0.GT, WP * Bp, h * Bp + r0, nvalid, L0.dbp);
   STAMP(35);
 }
 
@@ -1229,7 +1235,7 @@ __global__ void __launch_bounds__(SAC_THREADS) sac_actor_split(const EngineDev* 
   const AS_C EngineDev& E = *(const AS_C EngineDev*)Ep;
   extern __shared__ float lds_raw[];
   const int bid = (int)blockIdx.x;
-  const int nrole = 3 * split_wc(sizeof(T)) * E.nrt;  // 3 roles x parts x nrt
+  const int nrole = (2 * split_wcq(sizeof(T)) + split_wc(sizeof(T))) * E.nrt;  // critics' + pi's parts x nrt
   if (bid >= nrole) {
     stage_next_batch(E, rb, bid - nrole, (lf*)lds_raw, *GPC(uint64_t, E.rng_step));
   } else {

@@ -43,7 +43,7 @@ SPLIT = bool(lib.sac_engine_uses_split(eng.handle))
 lib.sac_engine_uses_pairs.argtypes = [ctypes.c_void_p]
 PAIRS = bool(lib.sac_engine_uses_pairs(eng.handle))
 GROUP = 2 * nrt if SPLIT else nrt  # blocks per role group (hidden split: two halves per row tile in A)
-GROUP_C = (4 if prec == "fp32" else 2) * nrt if SPLIT else nrt  # phase C: split_wc parts per row tile
+GROUP_C = 4 * nrt if SPLIT else nrt  # phase C: the critic roles' parts per row tile (split_wcq; pi: the rest)
 buf = torch.zeros(nblk * 64, dtype=torch.int64, device=dev)
 E.check(lib.sac_engine_debug_stamps(eng.handle, E.ptr(buf), eng._stream()))
 eng.train(rb, 20)
