@@ -1002,10 +1002,10 @@ static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
     e->h.nB = nB;
     e->h.nD = nD;
     e->lds_bytes = (size_t)lo * 4;
-    {  // update tiles stage up to 4 batch chunks of 512 B per operand row per round
+    {  // update tiles stage up to 2 batch chunks of 512 B per operand row per round
        // (every tile reduces over at most Bp columns: split layer 0 is two half tiles)
       const int bch = 512 / esz;
-      e->h.upd_slots = std::min(4, (Bp + bch - 1) / bch);
+      e->h.upd_slots = std::min(2, (Bp + bch - 1) / bch);
       e->upd_lds = SAC_UPD_LDS_FOR(e->h.upd_slots);
       // phase B in 2 rounds of 1024-thread blocks (C3: 480 blocks) -> 512-thread
       // blocks with 2 slots, two per CU, one round: C3 B 37.0 -> 33.5 us fp32,
@@ -1018,7 +1018,7 @@ static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
       e->upd_lds_b = e->upd_lds;
       if (ut512 && !split) {
         e->upd_ut_b = 512;
-        e->upd_lds_b = SAC_UPD_LDS_FOR(std::min(2, e->h.upd_slots));
+        e->upd_lds_b = SAC_UPD_LDS_FOR(1);  // one slot (sac_phases.h, dw_adam_tile)
       }
     }
     e->nrt = nrt;

@@ -85,7 +85,7 @@ struct EngineDev {
   int pairs;  // phases A / C as pair-tile workgroups (sac_pairs.h)
   int gstride;     // granules per (kind, row tile): SAC_ROWS * (act_dim + 1)
   uint64_t* gran;  // [G_COUNT][nrt][gstride] data-tagged hand-off granules (gran_put)
-  int upd_slots;  // update tiles: batch chunks staged per round (LDS slots, 1..4)
+  int upd_slots;  // update tiles: batch chunks staged per round (LDS slots, 1..2)
   // update tiles of phases B and D
   const TileDesc* tilesB;
   const TileDesc* tilesD;
@@ -874,7 +874,7 @@ __device__ __forceinline__ float adam_elem(float& p, float& m, float& v, float g
 // upd_slots x [256] f32 seeds (>= the alpha block's 5 x 1024 floats)
 #define SAC_UPD_SLOT_BYTES (64 * 528)
 #define SAC_UPD_LDS_FOR(slots) ((slots) * SAC_UPD_SLOT_BYTES + 2 * 32 * 33 * 4 + 32 * 17 * 4 + (slots) * 256 * 4)
-template <typename T, int UT, int GS = 1, int MS = 4>
+template <typename T, int UT, int GS = 1, int MS = 2>
 __device__ __forceinline__ void dw_adam_tile(const AS_C EngineDev& E, const TileDesc* tdp_, bool polyak, int par,
                                              int par_x, lf* lds) {
   constexpr int KC = MM<T>::KC, KL = MM<T>::KL;
@@ -889,9 +889,11 @@ __device__ __forceinline__ void dw_adam_tile(const AS_C EngineDev& E, const Tile
   const int lds_row = SAC_UPD_BCH + 16 / (int)sizeof(T);  // +16 B per row: rows start on different banks
   AS_L T* stage = (AS_L T*)lds;
   const int nslot = E.upd_slots;
-  // slots (2 with summed dY parts: register room; MS: the kernel's cap), pieces
-  // per thread per operand (32 rows) per full chunk
-  constexpr int MAXS = GS > 1 ? (MS < 2 ? MS : 2) : MS, PPO = 32 * (SAC_UPD_BCH / EPR) / UT;
+  // slots (MS: the kernel's cap -- 2, or 1 for the 512-thread phase B: a
+  // second slot in flight bought nothing there, one slot is C3 bf16 +1%,
+  // profiles/r05_ab_update_slots.txt), pieces per thread per operand (32 rows)
+  // per full chunk
+  constexpr int MAXS = MS, PPO = 32 * (SAC_UPD_BCH / EPR) / UT;
   const int ns = nslot < MAXS ? nslot : MAXS;  // slots per round
   const int slot_el = 64 * lds_row;  // T elements per stage slot
   lf* accs = lds + (ns * slot_el * (int)sizeof(T) + 15) / 16 * 4;
@@ -1152,7 +1154,7 @@ __device__ __forceinline__ void dw_adam_tile(const AS_C EngineDev& E, const Tile
   }
   __syncthreads();
   // producer parts a consumer takes (the 512-thread tiles: up to 7, else 3)
-  constexpr int MAXP = MS == 2 ? 7 : 3;
+  constexpr int MAXP = UT == 512 ? 7 : 3;
   float gbx[MAXP];  // staged-row bias: the producer parts' column sums (consumer, tid < 32)
 #pragma unroll
   for (int q = 0; q < MAXP; ++q) gbx[q] = 0.f;
@@ -1285,10 +1287,10 @@ __device__ __forceinline__ void dw_adam_tile(const AS_C EngineDev& E, const Tile
 }
 
 // a tile with summed dY parts (hidden-split layer 0) runs its own instance
-template <typename T, int UT, int MS = 4>
+template <typename T, int UT, int MS = 2>
 __device__ __forceinline__ void dw_adam_tile_any(const AS_C EngineDev& E, const TileDesc* tdp_, bool polyak, int par,
                                                  int par_x, lf* lds) {
-  if constexpr (MS >= 4) {  // (MS 2: the 512-thread phase B, never with the hidden split's summed tiles)
+  if constexpr (UT != 512) {  // (the 512-thread phase B never runs the hidden split's summed tiles)
     const int gs = ((const AS_C TileDesc*)tdp_)->gsum;  // uniform
     if constexpr (sizeof(T) == 4)
       if (gs == 4) return dw_adam_tile<T, UT, 4, MS>(E, tdp_, polyak, par, par_x, lds);
@@ -2310,15 +2312,15 @@ __global__ void __launch_bounds__(SAC_THREADS) sac_actor(const EngineDev* __rest
 }
 
 // ============================================================================ phases B / D kernels
-// UT = 512 (SAC_UPD_UT=512): two slots per round and at most 128 VGPRs, so two
-// workgroups share a CU (SAC_UPD_LDS_FOR(2) = 76 KB each)
+// UT = 512 (SAC_UPD_UT=512): one slot per round and at most 128 VGPRs, so two
+// workgroups share a CU (SAC_UPD_LDS_FOR(1) = 45 KB each)
 template <typename T, int UT = SAC_UPD_THREADS>
 __global__ void __launch_bounds__(UT, UT == 512 ? 4 : 1) sac_critic_update(const EngineDev* __restrict__ Ep,
                                                          const TileDesc* __restrict__ tiles) {
   const AS_C EngineDev& E = *(const AS_C EngineDev*)Ep;
   extern __shared__ float upd_lds[];
   // critic tiles: one X^T copy (xt_par = 0), so their operand loads need not wait for the step's parity
-  dw_adam_tile_any<T, UT, UT == 512 ? 2 : 4>(E, tiles + blockIdx.x, true,
+  dw_adam_tile_any<T, UT, UT == 512 ? 1 : 2>(E, tiles + blockIdx.x, true,
                                                           (int)(*GPC(uint64_t, E.rng_step) & 1), 0, (lf*)upd_lds);
   END_STAMP(62);  // standalone: the launch boundary publishes (no counter)
 }
