@@ -413,6 +413,7 @@ __device__ __forceinline__ void target_critic_split_body(const EngineDev* __rest
         rB[tid] = rr;
         dB[tid] = rd;
       }
+      STAMP(22);  // probe: thread 0's record loads landed
     } else {
       for (int i = tid; i < R * O; i += SAC_THREADS) {
         sB[i] = p[i];
@@ -815,10 +816,19 @@ template <typename T>
 __global__ void __launch_bounds__(SAC_THREADS) sac_target_critic_split(const EngineDev* __restrict__ Ep, sac_replay rb,
                                                                         const int32_t* __restrict__ inj_idx_,
                                                                         const float* __restrict__ inj_eps_) {
+#ifdef SAC_STAMPS
+  const long long t_entry = __builtin_amdgcn_s_memrealtime();  // probe 20: before the descriptor prefetch
+#endif
   PREFETCH_ARG(Ep);
   const AS_C EngineDev& E0 = *(const AS_C EngineDev*)Ep;
   const uint64_t step = *GPC(uint64_t, E0.rng_step);
   const StepCtx sc{step, *GPC(uint32_t, E0.sync) + 1u, (int)(step & 1)};
+#ifdef SAC_STAMPS
+  if (threadIdx.x == 0 && E0.stamps) {  // probe 21: the step counter loaded (the index depends on it)
+    GP(long long, E0.stamps)[blockIdx.x * 64 + 20] = t_entry;
+    GP(long long, E0.stamps)[blockIdx.x * 64 + 21 + (step == ~0ull ? 1 : 0)] = __builtin_amdgcn_s_memrealtime();
+  }
+#endif
   int bidA = (int)blockIdx.x;
   if (E0.role_xcd) {  // uniform
     // blocks are dealt round-robin to the 8 XCDs (block b on XCD b % 8): XCD x

@@ -81,6 +81,7 @@ if SPLIT:  # sac_split.h stamps
     names.update({2: "L0", 3: "L1 half", 4: "L2 partial", 6: "partials published", 7: "pi head (s')",
                   9: "Qt partial published", 33: "inputs", 34: "pi inputs", 36: "Q1 fwd", 37: "Q2 fwd",
                   38: "Q1 da partial", 39: "pi: critics combined", 35: "pi bwd + GT"})
+    names.update({20: "kernel entry", 21: "step loaded", 22: "record in registers"})
 if PAIRS:  # sac_pairs.h stamps
     names.update({6: "pi(s') head", 7: "Qt1", 8: "Qt2 + y", 9: "pi(s) + stashes", 14: "seeds (critics polled)",
                   10: "Q1 fwd", 11: "Q1 bwd + GT", 12: "Q2 fwd", 13: "Q2 bwd + GT", 33: "inputs",
