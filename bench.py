@@ -617,6 +617,28 @@ def c3_legs(args, timed):
     return out
 
 
+def copy_ceiling(nbytes, device, reps=20):
+    """Same-box ceiling for the gather leg: plain device
+    copies of `nbytes` (nbytes read + nbytes written per launch, contiguous),
+    timed like gather_sweep.  Returns {form: GB/s read + write}."""
+    src = torch.rand(nbytes // 4, device=device)
+    dst = torch.empty_like(src)
+    out = {}
+    for name, fn in (("copy_", lambda: dst.copy_(src)), ("mul_out", lambda: torch.mul(src, 1.0, out=dst))):
+        for _ in range(3):
+            fn()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            fn()
+        e1.record()
+        torch.cuda.synchronize()
+        out[name] = round(2 * nbytes / (e0.elapsed_time(e1) / reps * 1e-3) / 1e9, 1)
+    del src, dst
+    return out
+
+
 def sweep_fields(rb, c, device):
     sweep = gather_sweep(rb, device)
     sweep_soa = gather_sweep(soa_copy(rb), device, sizes=(65536, 1_048_576))
@@ -641,10 +663,16 @@ def sweep_fields(rb, c, device):
         "achieved_read_write": round(2 * sweep["gather"][str(bmax)], 3),
         "frac_read_write": round(2 * sweep["gather"][str(bmax)] / PEAK_HBM_GBS, 5),
         "traffic_source": gsrc, "bytes_per_launch": bmax * W * 4, "avg_launch_ms": ms,
+        "copy_ceiling_GBps_read_write": None, "frac_of_copy_ceiling": None,
         "note": "B_gather = 4 B (2 obs + act + 2) bytes read per launch (SURVEY §8d); the kernel writes "
                 "as many again (the minibatch it returns), counted in achieved_read_write; reads exceed "
                 "B_gather by the record padding (2O+A+2 floats stored in whole 128-B lines); rows uniform "
                 "with replacement over the 1e6-row buffer"}
+    cc = copy_ceiling(bmax * W * 4, device)
+    rg = line["roofline_gather"]
+    rg["copy_ceiling_GBps_read_write"] = max(cc.values())
+    rg["copy_ceiling_forms"] = cc
+    rg["frac_of_copy_ceiling"] = round(rg["achieved_read_write"] / max(cc.values()), 4)
     return line
 
 
