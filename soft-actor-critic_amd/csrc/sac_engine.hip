@@ -382,7 +382,7 @@ static int validate(const sac_engine_config* c) {
   if (c->layout < SAC_LAYOUT_AUTO || c->layout > SAC_LAYOUT_PAIRS || c->stage_path < -1 || c->stage_path > 1 ||
       c->stage_batch < -1 || c->stage_batch > 0 || c->upd_parts < 0 || c->upd_parts > 4 ||
       (c->upd_threads != 0 && c->upd_threads != 512 && c->upd_threads != 1024))
-    return fail(SAC_E_INVALID, "bad layout override (layout 0..2, stage_path -1..1, stage_batch -1..0, "
+    return fail(SAC_E_INVALID, "bad layout override (layout 0..3, stage_path -1..1, stage_batch -1..0, "
                                "upd_parts 0..4, upd_threads 0 / 512 / 1024)");
   return SAC_OK;
 }
@@ -1400,6 +1400,17 @@ int sac_engine_create(const sac_engine_config* cfg, const sac_engine_buffers* bu
       e->ncu = n;
   }
   plan(cfg, e, (char*)buf->workspace);
+  {  // an explicit layout override runs the kernels it names or fails (as stage_path = -1 does)
+    const bool rows = !e->h.split && !e->h.roles && !e->h.pairs && !e->wide;
+    const char* miss = nullptr;
+    if (cfg->layout == SAC_LAYOUT_ROLES && !e->h.roles) miss = "roles (needs 6 * row tiles <= 256 co-resident workgroups)";
+    if (cfg->layout == SAC_LAYOUT_PAIRS && !e->h.pairs) miss = "pairs (the pair-tile LDS layout or record does not fit)";
+    if (cfg->layout == SAC_LAYOUT_ROWS && !rows) miss = "rows (the row-tile LDS layout does not fit: stage path)";
+    if (miss) {
+      delete e;
+      return fail(SAC_E_INVALID, std::string("layout override cannot be honoured: ") + miss);
+    }
+  }
   if (std::max(e->lds_bytes, e->upd_lds) > 160 * 1024) {
     const size_t lb = e->lds_bytes;
     delete e;

@@ -69,6 +69,9 @@ __device__ __forceinline__ bool pair_batch(const AS_C EngineDev& E, const sac_re
     for (int sub = 0; sub < 2; ++sub) {
       staged[sub] = h[sub][0] == step && h[sub][1] == (uint64_t)rb_size && h[sub][2] == (uint64_t)rb_pos &&
                     h[sub][3] == (uint64_t)(uintptr_t)rb.obs && h[sub][4] == (uint64_t)GPC(int64_t, rb.state)[2];
+      // a sub-tile past the batch (odd nrt) is zero-filled below by other
+      // threads of the same slots: no copy of the duplicate record into it
+      if (sub == 1 && !live1) continue;  // uniform
 #pragma unroll
       for (int u = 0; u < MV; ++u) {
         const int i = tid + u * SAC_THREADS;

@@ -63,7 +63,8 @@ class SacEngine:
         """``layout`` (tests and A/B runs only; None = the engine's choice, which
         every measured number uses): kernel layout overrides, the fields of
         sac_engine_config named in sac._engine.LAYOUT_KEYS -- layout ("auto" |
-        "roles" | "rows"), stage_path (1 force / -1 refuse the stage path),
+        "roles" | "rows" | "pairs"; an override the shape cannot take fails in
+        create), stage_path (1 force / -1 refuse the stage path),
         stage_batch (-1: phase A gathers its own batch), upd_parts (batch parts
         of the large-batch update tiles), upd_threads (512 / 1024)."""
         self.device = torch.device(device)

@@ -42,6 +42,17 @@ def _initialised() -> bool:
     return dist.is_available() and dist.is_initialized()
 
 
+def _collective_device() -> Optional[torch.device]:
+    """Where a host-built metric vector must live for the default process
+    group's collectives: this process's HIP device under RCCL ("nccl", which
+    rejects CPU tensors), the host otherwise (gloo, or no process group)."""
+    import torch.distributed as dist
+
+    if _initialised() and dist.get_backend() == "nccl":
+        return torch.device("cuda", torch.cuda.current_device())
+    return None
+
+
 def aggregate_metrics(values: Sequence[float], group=None, device: Optional[torch.device] = None):
     """All-reduce one replica's metric vector -> (sum, mean, max) over replicas.
 
@@ -71,7 +82,8 @@ def metric_vector(engine, wall_s: float = 0.0, mean_return: float = float("nan")
     ret = [float(mean_return) if has_ret else 0.0, 1.0 if has_ret else 0.0]
     if engine is None:
         nan = float("nan")
-        return torch.tensor([float(steps or 0), float(wall_s), nan, nan, nan, nan, nan] + ret, dtype=torch.float64)
+        return torch.tensor([float(steps or 0), float(wall_s), nan, nan, nan, nan, nan] + ret, dtype=torch.float64,
+                            device=_collective_device())
     dev = engine.stats.device
     host = lambda x: torch.full((1,), float(x), dtype=torch.float64, device=dev)  # noqa: E731
     return torch.cat([engine.rng_step.double().reshape(1), host(wall_s), engine.stats[:4].double(),

@@ -261,21 +261,36 @@ def test_large_batch_uses_pair_or_row_tile_kernels_and_runs(layout):
 
 
 @pytest.mark.parametrize("cfg,precision,layout", [("c2", "bf16", "auto"), ("c2", "fp32", "roles"),
-                                                  ("c3", "bf16", "auto"), ("c3", "fp32", "rows")])
+                                                  ("c3", "bf16", "auto"), ("c3", "fp32", "rows"),
+                                                  ("c3_b4001", "fp32", "auto"), ("c3_b4001", "bf16", "auto")])
 def test_staged_batch_equals_in_step_gather(cfg, precision, layout):
     """Phase C staging step t+1's batch (sampled and gathered one launch early)
     gives the same bits as phase A gathering it, across graph replays, a replay
     push between calls (the staged record goes stale and phase A gathers), and
-    injected indices.  The staged path must actually run."""
+    injected indices.  The staged path must actually run.  B = 4001 (ADVICE
+    r05): 251 row tiles, so the last pair tile's second tile lies past the
+    batch and its LDS rows are zero-filled instead of staged (device RNG)."""
     import ctypes
 
+    import bench
     from sac import _engine as E
 
+    if cfg == "c3_b4001":
+        bench.CONFIGS[cfg] = dict(bench.CONFIGS["c3"], batch=4001)
+    try:
+        _staged_vs_gathered(cfg, precision, layout, ctypes, E)
+    finally:
+        bench.CONFIGS.pop("c3_b4001", None)
+
+
+def _staged_vs_gathered(cfg, precision, layout, ctypes, E):
     out = {}
     for stage in ("1", "0"):
         # stage_path=-1 at C3: batch staging is a feature of the row-tile kernels
         eng, rb, c = _engine(cfg, precision, capacity=5000, layout=layout, stage_batch=0 if stage == "1" else -1,
-                             stage_path=-1 if cfg == "c3" else 0)
+                             stage_path=-1 if cfg.startswith("c3") else 0)
+        if cfg == "c3_b4001":
+            assert eng.pairs
         eng.train(rb, 3)
         eng.train_graph(rb, 5, chunk=2)
         if stage == "1":

@@ -163,7 +163,7 @@ BENCH_NETS = {"policy": "pi", "q1": "q1", "q2": "q2", "q1t": "q1t", "q2t": "q2t"
 
 
 @pytest.mark.parametrize("precision", ["fp32", "bf16"])
-@pytest.mark.parametrize("cfg,capacity,steps", [("c4", 4096, 3), ("c4w", 2048, 3), ("c3", 12_288, 2)])
+@pytest.mark.parametrize("cfg,capacity,steps", [("c4", 4096, 3), ("c4w", 2048, 3), ("c3", 12_288, 4)])
 def test_baseline_config_matches_oracle(cfg, capacity, steps, precision, layout=None):
     """The BASELINE.json configs the fixtures do not cover, against the
     fixture-pinned oracle on seeded batches with injected indices and eps:
@@ -171,7 +171,8 @@ def test_baseline_config_matches_oracle(cfg, capacity, steps, precision, layout=
       c4w the reference Donkey env's real observation width (32-D latent + 2x20
           command history, x3 frame stack = 216; SURVEY §7.8), act 2, B 256;
       c3  BipedalWalker at B = 4096 (256 row tiles: the non-role-split phase
-          kernels and the 4-chunk update staging, a different code path).
+          kernels and the 4-chunk update staging, a different code path), a
+          4-step trajectory (the layout variants below run 2).
     No golden fixture exists at these shapes (parity unpinned by the reference
     itself; the oracle is pinned by the 8 reference fixtures).  Checks, per
     step: the four losses, y and log pi, every post-step parameter of the five

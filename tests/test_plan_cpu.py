@@ -47,15 +47,16 @@ def _cfg(name, precision):
     return cfg
 
 
-@pytest.mark.parametrize("override", ["", "stage_batch=-1", "layout=1", "layout=2", "upd_parts=4",
-                                      "upd_threads=1024", "stage_path=1", "stage_path=-1"])
+@pytest.mark.parametrize("override", ["", "stage_batch=-1", "layout=1", "layout=2", "layout=3",
+                                      "layout=3,upd_threads=512", "upd_parts=4", "upd_threads=1024",
+                                      "stage_path=1", "stage_path=-1"])
 @pytest.mark.parametrize("precision", ["fp32", "bf16"])
 @pytest.mark.parametrize("name", sorted(bench.CONFIGS))
 def test_plan_is_consistent(name, precision, override):
     lib = E.load_library()
     cfg = _cfg(name, precision)
-    if override:
-        k, v = override.split("=")
+    for kv in filter(None, override.split(",")):
+        k, v = kv.split("=")
         setattr(cfg, k, int(v))
     ws = lib.sac_engine_workspace_bytes(ctypes.byref(cfg))
     assert ws > 0, lib.sac_last_error()
@@ -67,7 +68,37 @@ def test_plan_is_consistent(name, precision, override):
         lib.sac_engine_destroy(out)
         pytest.skip("GPU present: the planner ran for real")
     assert "internal" not in msg, msg
+    if cfg.layout and rc == SAC_E_INVALID:  # an explicit layout the shape cannot take fails, never falls back
+        assert "layout override cannot be honoured" in msg, msg
+        assert (name, cfg.layout) in HONOUR_REFUSED, (name, cfg.layout, msg)
+        return
+    assert (name, cfg.layout) not in HONOUR_REFUSED, (name, cfg.layout)
     assert rc == SAC_E_HIP, (rc, msg)
+
+
+# (config, forced layout) pairs the planner cannot honour: the per-network role
+# kernels need 6 workgroups per row tile co-resident (C3: 256 row tiles); the
+# row and pair tiles hold 2R rows of every layer, which at obs 216 (C4') does
+# not fit the CU's LDS (that config runs the role kernels by default)
+HONOUR_REFUSED = {("c3", 1), ("c4w", 2), ("c4w", 3)}
+
+
+def test_unhonourable_layout_override_fails():
+    """layout=roles at C3 (1536 role workgroups > 256 CUs) used to
+    fall back silently to other kernels; it now fails in create with
+    SAC_E_INVALID, before any HIP call, like stage_path = -1 on a shape that
+    needs the stage path."""
+    lib = E.load_library()
+    cfg = _cfg("c3", "fp32")
+    cfg.layout = 1
+    ws = lib.sac_engine_workspace_bytes(ctypes.byref(cfg))
+    bufs = E.EngineBuffers(*([0x1000] * 15), 0x100000, ws)
+    out = ctypes.c_void_p()
+    rc = lib.sac_engine_create(ctypes.byref(cfg), ctypes.byref(bufs), None, ctypes.byref(out))
+    if rc == 0:
+        lib.sac_engine_destroy(out)
+        pytest.fail("layout=roles honoured at C3")
+    assert rc == SAC_E_INVALID and "cannot be honoured: roles" in lib.sac_last_error().decode()
 
 
 def _create_rc(obs, act, hidden, batch=64):
