@@ -639,6 +639,74 @@ def copy_ceiling(nbytes, device, reps=20):
     return out
 
 
+def time_gather(rb, idx_sets, B, device, reps=20):
+    """ms per sac_replay_gather launch of B rows, rep k reading idx_sets[k % len]
+    (hipEvents around `reps` back-to-back launches on the launch stream)."""
+    from sac import _engine as E
+    import ctypes
+
+    lib = E.load_library()
+    st = E.stream_handle(device)
+    desc = rb.desc
+    f = dict(dtype=torch.float32, device=device)
+    outs = (torch.empty(B, rb.obs_dim, **f), torch.empty(B, rb.act_dim, **f), torch.empty(B, **f),
+            torch.empty(B, rb.obs_dim, **f), torch.empty(B, **f))
+    ptrs = [E.ptr(t) for t in outs]
+    once = lambda ix: E.check(lib.sac_replay_gather(ctypes.byref(desc), E.ptr(ix), B, *ptrs, st))  # noqa: E731
+    for k in range(3):
+        once(idx_sets[k % len(idx_sets)])
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for k in range(reps):
+        once(idx_sets[k % len(idx_sets)])
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / reps
+
+
+def gather_ceilings(rb, c, device, B=1_048_576, big_rows=4_000_000):
+    """like-for-like ceilings of the gather leg, the SAME
+    kernel (replay_gather_records_kernel) on the same kind of table:
+      * same 1e6-row table, its rows read in table order (logical i % size) --
+        the streaming form of the random-row gather, same MALL residency;
+      * a 4e6-row table (1 GB of records, past the 256 MiB Infinity Cache):
+        random rows (4 independent draws rotating over the reps, ~1 GB touched)
+        and rows in table order (4 disjoint 1M-row windows rotating: every rep
+        streams a fresh 256 MB), so the HBM fraction is not flattered by on-die
+        hits.  GB/s = B_gather (SURVEY §8d bytes read) / launch time."""
+    from sac.replay_buffer import ReplayBuffer
+
+    W = 2 * c["obs"] + c["act"] + 2
+    gbs = lambda ms: round(B * W * 4 / (ms * 1e-3) / 1e9, 3)  # noqa: E731
+    i32 = dict(dtype=torch.int32, device=device)
+    seq = [(torch.arange(B, device=device, dtype=torch.int64) % len(rb)).to(torch.int32)]
+    out = {"B": B, "same_table_rows_in_order_GBps": gbs(time_gather(rb, seq, B, device))}
+    big = ReplayBuffer(big_rows, device=device, obs_dim=c["obs"], act_dim=c["act"])
+    chunk = 500_000
+    for i in range(0, big_rows, chunk):
+        n = min(chunk, big_rows - i)
+        g = torch.Generator(device=device).manual_seed(i)
+        big.push_batch(torch.randn(n, c["obs"], device=device, generator=g),
+                       torch.rand(n, c["act"], device=device, generator=g) * 2 - 1,
+                       torch.randn(n, device=device, generator=g),
+                       torch.randn(n, c["obs"], device=device, generator=g),
+                       torch.rand(n, device=device, generator=g) < 0.01)
+    torch.cuda.synchronize()
+    rnd = [torch.randint(0, big_rows, (B,), generator=torch.Generator(device=device).manual_seed(k), **i32)
+           for k in range(4)]
+    win = [torch.arange(k * B, (k + 1) * B, **i32) % big_rows for k in range(4)]
+    r_ms, s_ms = time_gather(big, rnd, B, device), time_gather(big, win, B, device)
+    out["big_table"] = {"rows": big_rows, "table_MB": round(big_rows * big.row_stride * 4 / 1e6, 1),
+                        "random_GBps": gbs(r_ms), "rows_in_order_GBps": gbs(s_ms),
+                        "random_ms": round(r_ms, 5), "rows_in_order_ms": round(s_ms, 5),
+                        "random_frac_of_hbm_peak": round(gbs(r_ms) / PEAK_HBM_GBS, 5),
+                        "random_frac_of_rows_in_order": round(s_ms / r_ms, 4)}
+    del big, rnd, win
+    torch.cuda.empty_cache()
+    return out
+
+
 def sweep_fields(rb, c, device):
     sweep = gather_sweep(rb, device)
     sweep_soa = gather_sweep(soa_copy(rb), device, sizes=(65536, 1_048_576))
@@ -673,6 +741,10 @@ def sweep_fields(rb, c, device):
     rg["copy_ceiling_GBps_read_write"] = max(cc.values())
     rg["copy_ceiling_forms"] = cc
     rg["frac_of_copy_ceiling"] = round(rg["achieved_read_write"] / max(cc.values()), 4)
+    gc = gather_ceilings(rb, c, device, B=bmax)
+    rg["same_table_rows_in_order_GBps"] = gc["same_table_rows_in_order_GBps"]
+    rg["frac_of_rows_in_order"] = round(rg["achieved"] / gc["same_table_rows_in_order_GBps"], 4)
+    rg["big_table"] = gc["big_table"]
     return line
 
 
