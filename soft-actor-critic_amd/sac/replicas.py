@@ -195,14 +195,15 @@ def timed_region(run, sync, device: Optional[torch.device] = None, group=None) -
     sync()
     if on:
         dist.barrier(group)
-    sync()
+        sync()
     t0 = time.perf_counter()
     run()
     sync()
-    if on:
+    if on:  # one process: the device is idle after the first sync (a second one only adds host latency)
         dist.barrier(group)
-    sync()
-    el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=device)
+        sync()
+    t1 = time.perf_counter()
+    el = torch.tensor([t1 - t0], dtype=torch.float64, device=device)
     if on:
         dist.all_reduce(el, op=dist.ReduceOp.MAX, group=group)
     return float(el.item())
