@@ -1842,12 +1842,23 @@ __device__ __forceinline__ void target_critic_body(const EngineDev* __restrict__
       lf* Yl = out ? outB : Y;
       const int ldl = out ? ldo : ld;
       const GemmW nx = out ? gw_fwd(E.net[NET_Q1T].l[0]) : gw_fwd(pi.l[l + 1]);
-      if (l == 0)
-        layer_fwd<T, ROWS, 1>(X, ld, Ly, pi.P + Ly.b_off, act_l, Pl, ldl, Yl, ldl, stash, a0, pf, nx, &ph0);
-      else if (l == 1)
-        layer_fwd<T, ROWS, 8>(X, ld, Ly, pi.P + Ly.b_off, act_l, Pl, ldl, Yl, ldl, stash, a0, pf, nx, &ph1);
-      else
+      // held fragments exist only under the role split (ROWS = R); the fused
+      // [s'; s] pass (ROWS = 2R) streams every layer.  (With the held variants
+      // instantiated here -- their tags null, the held branch never taken -- the
+      // bf16 build returned wrong accumulator elements 0-1 of the second row
+      // tile, the actor rows, whenever a layer took the streamed path: hidden
+      // widths other than 256.  Found by tests/test_gpu_parity.py::
+      // test_bf16_one_step_from_the_engine_state; profiles/r06_bf16_rows_fault.txt.)
+      if constexpr (ROLES) {
+        if (l == 0)
+          layer_fwd<T, ROWS, 1>(X, ld, Ly, pi.P + Ly.b_off, act_l, Pl, ldl, Yl, ldl, stash, a0, pf, nx, &ph0);
+        else if (l == 1)
+          layer_fwd<T, ROWS, 8>(X, ld, Ly, pi.P + Ly.b_off, act_l, Pl, ldl, Yl, ldl, stash, a0, pf, nx, &ph1);
+        else
+          layer_fwd<T, ROWS>(X, ld, Ly, pi.P + Ly.b_off, act_l, Pl, ldl, Yl, ldl, stash, a0, pf, nx);
+      } else {
         layer_fwd<T, ROWS>(X, ld, Ly, pi.P + Ly.b_off, act_l, Pl, ldl, Yl, ldl, stash, a0, pf, nx);
+      }
       __syncthreads();
       STAMP(2 + l);
       lf* t = X;
@@ -2275,8 +2286,9 @@ __device__ __forceinline__ void actor_body(const EngineDev* __restrict__ Ep, int
     for (int i = tid; i < R * pad; i += SAC_THREADS) goutB[(i / pad) * ldo + 2 * A + i % pad] = 0.f;
   }
   __syncthreads();
-  mlp_backward<T, R, true>(pi, goutB, ldo, Xb, Yb, ld, E.o_P1, E.ldp1, lds, true, Bp, r0, nvalid, pf, gw_none(),
-                                  &bh0, &bh1);
+  // held fragments only under the role split (bh0 / bh1 are issued only there)
+  mlp_backward<T, R, ROLES>(pi, goutB, ldo, Xb, Yb, ld, E.o_P1, E.ldp1, lds, true, Bp, r0, nvalid, pf, gw_none(),
+                                   &bh0, &bh1);
   STAMP(35);
 }
 
