@@ -769,8 +769,9 @@ static size_t plan(const sac_engine_config* c, sac_engine* e, char* base) {
         if (ni == NET_Q2 && l == 0) {
           ly.XT = P(xt_q0);
         } else {
-          // pi: two copies by step parity (phase D of step k reads one while
-          // phase A of step k + 1 writes the other when they share a launch)
+          // pi: two copies by step parity (from the fused step, where phase D of
+          // step k read one while phase A of step k + 1 wrote the other in one
+          // launch; with one phase per launch they only alternate)
           const size_t o = lay.take((size_t)ly.Kp * bpl * esz * (is_pi ? 2 : 1));
           if (ni == NET_Q1 && l == 0) xt_q0 = o;
           ly.XT = P(o);

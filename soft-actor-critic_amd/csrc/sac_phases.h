@@ -524,7 +524,8 @@ __device__ __forceinline__ void gemm_step(const lf* __restrict__ A, int lda, con
   }
 #endif
   if (pf.tag != w.p) pf_issue<T>(pf, w);  // chain broken by the caller: reload (uniform)
-  // weight stream: sc1 buffer loads, coherent with an update phase sharing the launch
+  // weight stream: sc1 buffer loads (from the round-3 fused step, where an update phase
+  // shared the launch; every phase has its own launch since round 5)
   const __amdgpu_buffer_rsrc_t rs = coh_rsrc(w.p, 0xFFFFFFF0u);
   auto pair = [&](int nt0, bool first) __attribute__((always_inline)) {
     const int nt1 = nt0 + SAC_NW;
@@ -863,8 +864,9 @@ __device__ __forceinline__ float adam_elem(float& p, float& m, float& v, float g
 //      any block size);
 //   3. every thread updates 1024 / UT elements: Adam (torch single-tensor op
 //      order), Polyak, master weights; the packed compute copies are written
-//      from LDS as whole 16-B fragment pieces with sc1 stores, so a phase that
-//      shares the launch can read them after the completion counter.
+//      from LDS as whole 16-B fragment pieces with sc1 stores (a reader in the
+//      same launch could use them after the completion counter; since round 5
+//      the reader is always the next launch).
 // 16 waves (measured on C2: 256-thread tiles took B 8.7 / D 7.8 us vs 6.4 / 5.9)
 #ifndef SAC_UPD_THREADS
 #define SAC_UPD_THREADS 1024
@@ -1302,8 +1304,8 @@ __device__ __forceinline__ void dw_adam_tile_any(const AS_C EngineDev& E, const 
 // One block: reduces the step's loss partials into stats[0..3] and runs the
 // float64 alpha Adam step (agent.py:263-280).  All blockDim.x threads take part
 // (no early exit: the caller's completion barrier follows).  alpha_state is
-// stored sc1: the critics of a phase A sharing the launch read alpha after the
-// completion counter.
+// stored sc1 (from the fused step, where phase A's critics read alpha after the
+// completion counter; phase A is the next launch since round 5).
 __device__ __forceinline__ void alpha_and_losses(const AS_C EngineDev& E, int par, lf* red) {
   const int tid = threadIdx.x, NT = blockDim.x, B = E.B;
   const float H = E.target_entropy;
@@ -1693,7 +1695,6 @@ __device__ __forceinline__ void target_critic_body(const EngineDev* __restrict__
   pf_issue<T>(pf, !ROLES || do_pi ? gw_fwd(pi.l[0])
                   : gw_fwd(E.net[role <= 2 ? NET_Q1T + role - 1 : NET_Q1 + role - 3].l[0]));
   // pi(s') (the critical path): layers 0 and 1 held under the sample / gather
-  // (after phase D's count when D shares the launch)
   Held<T, 1> ph0;
   Held<T, 8> ph1;
   ph0.tag = ph1.tag = nullptr;
@@ -2021,7 +2022,8 @@ __device__ __forceinline__ void target_critic_body(const EngineDev* __restrict__
             const float q1t = gran_get(E, gran_at(E, G_Q1T, rbi) + tid, ep);
             const float q2t = gran_get(E, gran_at(E, G_Q2T, rbi) + tid, ep);
             const float lp2 = gran_get(E, gran_at(E, G_LP, rbi) + tid, ep);
-            // alpha after the hand-offs: a phase D sharing the launch finished before pi started
+            // alpha, written by the previous launch's phase D (an atomic load: kept from the
+            // fused step, where D shared this launch)
             const float al = (float)__hip_atomic_load((double*)E.alpha_state + 1, __ATOMIC_RELAXED,
                                                       __HIP_MEMORY_SCOPE_AGENT);
             y = rB[tid] + (E.gamma * (1.f - dB[tid])) * (fmin_nan(q1t, q2t) - al * lp2);
