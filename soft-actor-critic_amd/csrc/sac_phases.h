@@ -524,8 +524,7 @@ __device__ __forceinline__ void gemm_step(const lf* __restrict__ A, int lda, con
   }
 #endif
   if (pf.tag != w.p) pf_issue<T>(pf, w);  // chain broken by the caller: reload (uniform)
-  // weight stream: sc1 buffer loads (from the round-3 fused step, where an update phase
-  // shared the launch; every phase has its own launch since round 5)
+  // weight stream: plain buffer loads through a uniform descriptor (coh_frag<T, false>)
   const __amdgpu_buffer_rsrc_t rs = coh_rsrc(w.p, 0xFFFFFFF0u);
   auto pair = [&](int nt0, bool first) __attribute__((always_inline)) {
     const int nt1 = nt0 + SAC_NW;
