@@ -863,9 +863,8 @@ __device__ __forceinline__ float adam_elem(float& p, float& m, float& v, float g
 //      any block size);
 //   3. every thread updates 1024 / UT elements: Adam (torch single-tensor op
 //      order), Polyak, master weights; the packed compute copies are written
-//      from LDS as whole 16-B fragment pieces with sc1 stores (a reader in the
-//      same launch could use them after the completion counter; since round 5
-//      the reader is always the next launch).
+//      from LDS as whole 16-B fragment pieces (plain stores: the reader is the
+//      next launch).
 // 16 waves (measured on C2: 256-thread tiles took B 8.7 / D 7.8 us vs 6.4 / 5.9)
 #ifndef SAC_UPD_THREADS
 #define SAC_UPD_THREADS 1024
